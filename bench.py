@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Benchmark of the FM-SDR hot path on MI355X (BASELINE.json metric).
+
+One step = one pass of RF front end (101-tap IQ LPF, decimate by 10, atan2 demod;
+configs[1]) + mono (151-tap audio LPF, decimate by 5; configs[2]) over a batch of
+`--blocks` x 1 024 000-complex-sample blocks of one synthetic 2.4 MS/s stream, input
+resident in HBM (block boundaries are carried-state continuations, so the batch is
+one continuous stream; SURVEY §5 "long-context").  Kernels: libsdr.so's fused FE
+kernel and tiled FIR kernel, launched through the C-ABI (no torch in the data path).
+
+Multi-GPU (`torchrun --nproc-per-node N bench.py --gpus N`): one process per GPU,
+each rank processes its own independent stream (seed = rank): weak scaling, no
+data-path collective.  torch.distributed (gloo, CPU) only provides the barrier and
+the max-over-ranks of the timed region.
+
+Prints ONE JSON line (rank 0).  `value` = complex IQ samples processed by all ranks
+per second (MS/s); `roofline` is for the FE kernel (HIP events on the libsdr stream);
+`cpu_baseline` = the C restatement of the Python model (oracle/fm_oracle.c) on the
+host cores (rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "IQ MSamples/s through RF front-end+mono path; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BLOCK = 1_024_000              # complex samples per block (SURVEY §7 hard part 7)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--blocks", type=int, default=64, help="1 024 000-sample blocks per step")
+    ap.add_argument("--taps", type=int, default=101)
+    ap.add_argument("--audio-taps", type=int, default=151)
+    ap.add_argument("--iq", choices=["f32", "u8"], default="f32")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-samples", type=int, default=2_048_000, help="complex samples per CPU stream")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "fe_pmc_traffic.json"),
+                    help="PMC-derived HBM bytes per FE launch (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(ws, value: float) -> float:
+    if ws == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(args, rf_b, au_b):
+    """Oracle C port (f64, model semantics) + reference C++ FE, one stream per thread."""
+    import subprocess
+    lib_path = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(lib_path):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    lib = ctypes.CDLL(lib_path)
+    P = np.ctypeslib.ndpointer
+    lib.orc_fe_mono_streams.argtypes = [P(np.float32), ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                        P(np.float64), ctypes.c_int, P(np.float64), ctypes.c_int,
+                                        P(np.float64), ctypes.c_int64, ctypes.c_int]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16, os.cpu_count() or 1))
+    import rtsdr
+    n = args.cpu_samples
+    iq = np.concatenate([rtsdr.synth.fm_iq(n, seed=100 + s) for s in range(threads)])
+    A = ((n + 9) // 10 + 4) // 5
+    out = np.empty(A * threads)
+    t0 = time.perf_counter()
+    lib.orc_fe_mono_streams(iq, n, n, threads, np.ascontiguousarray(rf_b), len(rf_b),
+                            np.ascontiguousarray(au_b), len(au_b), out, A, threads)
+    dt = time.perf_counter() - t0
+    res = {"value": round(n * threads / dt / 1e6, 3), "unit": "MS/s", "cores": threads, "kind": "port",
+           "sample": f"{threads} streams x {n} complex samples, FE({len(rf_b)} taps)+mono({len(au_b)} taps), "
+                     f"f64 C restatement of the Python model, -O3 OpenMP, {dt:.2f} s wall"}
+    ref = os.path.join(ROOT, "oracle", "_ref", "libref_fe.so")
+    if os.path.exists(ref):
+        rl = ctypes.CDLL(ref)
+        rl.ref_fe_streams.argtypes = [P(np.float32), ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int64,
+                                      P(np.float32), ctypes.c_int, ctypes.c_int, P(np.float32), ctypes.c_int64,
+                                      ctypes.c_int]
+        blk = 153_600
+        nn = (n // blk) * blk
+        dm = np.empty((nn // 10) * threads, dtype=np.float32)
+        t0 = time.perf_counter()
+        rl.ref_fe_streams(iq, nn, n, threads, blk, np.ascontiguousarray(rf_b, dtype=np.float32), len(rf_b), 10,
+                          dm, nn // 10, threads)
+        dt = time.perf_counter() - t0
+        res["reference_cpp_fe"] = {"value": round(nn * threads / dt / 1e6, 3), "unit": "MS/s",
+                                   "cores": threads, "kind": "reference",
+                                   "sample": f"{threads} streams x {nn} complex, src/ convolveWithDecimIQ + "
+                                             f"fmDemodArctan (FE only, f32, -O3), {dt:.2f} s wall"}
+    return res
+
+
+def load_traffic(path, taps, blocks):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("taps") == taps and t.get("n_complex") == blocks * BLOCK:
+            return t.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    ws, rank, local = dist_setup(args)
+    os.environ["SDR_DEVICE"] = str(local)
+    import rtsdr
+    from importlib import import_module
+    _lib = import_module("real-time-software-defined-radio_amd._lib")
+
+    ctx = _lib.Context(local)
+    lib, h = ctx.lib, ctx.handle
+    rf_b, au_b = rtsdr.design.mono_coeffs(args.taps, args.audio_taps)
+    n = args.blocks * BLOCK
+    M = n // 10
+    A = M // 5
+    iq = rtsdr.synth.fm_iq(n, seed=rank, dtype=np.uint8 if args.iq == "u8" else np.float32)
+    dtype_code = _lib.SDR_IQ_U8 if args.iq == "u8" else _lib.SDR_IQ_F32
+    d_iq = _lib.DeviceBuffer.from_array(ctx, iq)
+    del iq
+    d_dm = _lib.DeviceBuffer(ctx, 4 * M)
+    d_au = _lib.DeviceBuffer(ctx, 4 * A)
+    rfp, aup = _lib.f64p(rf_b), _lib.f64p(au_b)
+    T, TA = len(rf_b), len(au_b)
+
+    def fe():
+        _lib.check(lib.sdr_rf_frontend_dev(h, d_iq.ptr, dtype_code, n, n, 0, 1, rfp, T, 10, None, None, 0, None,
+                                           None, None, d_dm.ptr, M, None, None), "fe")
+
+    def mono():
+        _lib.check(lib.sdr_fir_dev(h, d_dm.ptr, None, 1.0, 0, M, M, 0, 1, aup, TA, 5, None, 0, None, d_au.ptr, A),
+                   "mono")
+
+    tm = _lib.Timer(ctx)
+    ev = [(tm.event(), tm.event(), tm.event()) for _ in range(args.steps)]
+    for _ in range(args.warmup):
+        fe()
+        mono()
+    ctx.synchronize()
+    barrier(ws)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1, e2 in ev:
+        tm.record(e0)
+        fe()
+        tm.record(e1)
+        mono()
+        tm.record(e2)
+    ctx.synchronize()
+    barrier(ws)
+    elapsed = max_over_ranks(ws, time.perf_counter() - t0)
+    fe_ms = [tm.elapsed_ms(a, b) for a, b, _ in ev]
+    mono_ms = [tm.elapsed_ms(b, c) for _, b, c in ev]
+    fe_avg = float(np.mean(fe_ms))
+    bpc = 2 if args.iq == "u8" else 8
+    fe_bytes = n * bpc + M * 4                      # compulsory: IQ in + demod out
+    mono_bytes = M * 4 + A * 4
+    achieved = fe_bytes / (fe_avg * 1e-3) / 1e9
+    traffic = load_traffic(args.traffic, args.taps, args.blocks) if args.iq == "f32" else None
+
+    result = None
+    if rank == 0:
+        total = n * args.steps * ws
+        result = {
+            "metric": METRIC,
+            "value": round(total / elapsed / 1e6, 1),
+            "unit": "MS/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic FM IQ (seed=rank), interleaved {args.iq}, device-resident",
+            "config": {"workload": f"RF front end ({args.taps}-tap LPF, decim 10, atan2 demod) + mono "
+                                   f"({args.audio_taps}-tap LPF, decim 5): configs[1]+[2], one stream per GPU",
+                       "block_complex": BLOCK, "blocks_per_step": args.blocks, "complex_per_step": n,
+                       "iq": args.iq, "parallelism": f"independent streams x{ws}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": f"fe_kernel<{args.taps},10> (sdr_rf_frontend_dev)",
+                         "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg, 5)},
+            "kernels_ms": {"fe": round(fe_avg, 5), "mono": round(float(np.mean(mono_ms)), 5),
+                           "mono_gbs": round(mono_bytes / (np.mean(mono_ms) * 1e-3) / 1e9, 1)},
+        }
+    if ws == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args, rf_b, au_b)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    tm.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

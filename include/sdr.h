@@ -1,0 +1,168 @@
+/* libsdr.so — C-ABI of the MI355X-native FM-SDR hot path (gfx950 HIP kernels).
+ *
+ * This is the drop-in boundary for the reference's per-block signal-processing
+ * functions.  Plain pointers and sizes only; no torch/numpy types.
+ * Each entry point names the reference interface it replaces (file:line under the
+ * reference repository m1nty/Real-Time-Software-Defined-Radio).
+ *
+ * Conventions
+ *   - Return value: SDR_OK (0) or a negative SDR_E* code; sdr_last_error() returns
+ *     the calling thread's last error message (the Python layer raises ValueError
+ *     for SDR_EINVAL, NotImplementedError for SDR_EUNSUPPORTED, RuntimeError else;
+ *     mirroring scipy.signal.lfilter's ValueError/NotImplementedError,
+ *     scipy/signal/_signaltools.py:2143-2151).
+ *   - Filter state `zi` uses scipy.signal.lfilter's convention (length taps-1,
+ *     f64): y[n] = (b*x)[n] + zi[n] for n < taps-1, and the returned zf is the tail
+ *     of the full convolution.  Host `*_inout` state arrays are overwritten with the
+ *     new state, so reference and libsdr calls can be mixed block by block.
+ *   - Decimated outputs are y[D*m] for m = 0 .. ceil(n/D)-1 (lfilter(...)[::D]).
+ *   - Demod phase state is the reference's accumulated unwrapped phase
+ *     (model/fmSupportLib.py:40-44), returned as phi_last + 2*pi*(number of wraps).
+ *   - A context (sdr_ctx) owns one HIP stream and scratch memory on one device; it is
+ *     not thread-safe: one context per host thread per GPU.
+ *   - Host-buffer functions are synchronous.  `*_dev` functions take device
+ *     pointers and are asynchronous on the context's stream (sdr_stream()).
+ *   - Numerics: samples are processed in f32 (inputs f32 or u8); filter-state (zf)
+ *     and PLL phase arithmetic are f64.
+ */
+#ifndef SDR_H_
+#define SDR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDR_ABI_VERSION 1
+
+enum {
+  SDR_OK = 0,
+  SDR_EINVAL = -1,      /* bad argument (shape, NULL, range) */
+  SDR_EHIP = -2,        /* HIP runtime error */
+  SDR_ENOMEM = -3,      /* device allocation failed */
+  SDR_EUNSUPPORTED = -4 /* valid but not implemented configuration */
+};
+
+enum { SDR_IQ_F32 = 0, SDR_IQ_U8 = 1 };                  /* interleaved IQ sample types */
+enum { SDR_PRE_NONE = 0, SDR_PRE_SQUARE = 1, SDR_PRE_MIX = 2 }; /* FIR input pre-ops */
+
+typedef struct sdr_ctx sdr_ctx;
+
+/* ---- library / context ------------------------------------------------------- */
+int sdr_abi_version(void);
+const char* sdr_last_error(void);
+int sdr_device_count(int* n);
+int sdr_create(int device, sdr_ctx** out);
+void sdr_destroy(sdr_ctx* ctx);
+int sdr_synchronize(sdr_ctx* ctx);
+void* sdr_stream(sdr_ctx* ctx); /* the hipStream_t all kernels of this context use */
+
+/* ---- device memory and timing (replace the static float[5][307200] ring and the
+ *      std::queue<void*> hand-off of src/fm_radio.cpp:22,51,86-145) ---------------- */
+int sdr_malloc(sdr_ctx* ctx, int64_t bytes, void** out);
+int sdr_free(sdr_ctx* ctx, void* p);
+int sdr_memcpy_h2d(sdr_ctx* ctx, void* dst, const void* src, int64_t bytes);
+int sdr_memcpy_d2h(sdr_ctx* ctx, void* dst, const void* src, int64_t bytes);
+int sdr_memcpy_d2d(sdr_ctx* ctx, void* dst, const void* src, int64_t bytes); /* async */
+int sdr_memset(sdr_ctx* ctx, void* dst, int value, int64_t bytes);          /* async */
+int sdr_event_create(sdr_ctx* ctx, void** ev);
+int sdr_event_record(sdr_ctx* ctx, void* ev);
+int sdr_event_elapsed_ms(void* ev0, void* ev1, float* ms);
+int sdr_event_destroy(void* ev);
+
+/* ================================================================================
+ * Host-buffer drop-in entry points (synchronous)
+ * ================================================================================ */
+
+/* RF front end: lfilter(rf_coeff, 1.0, iq[0::2], zi_i)[::decim], same for Q, then
+ * fmDemodArctan(i_ds, q_ds, prev_phase).
+ * Replaces model/fmMonoBlock.py:86-98 (model/fmSupportLib.py:15-44) and
+ * src/fm_radio.cpp:66-84 -> src/filter.cpp:187-219 (convolveWithDecimIQ) +
+ * src/rf_module.cpp:13-34 (fmDemodArctan).  iq: n complex samples interleaved,
+ * f32 or u8 ((u8-128)/128, src/iofunc.cpp:61-69).  zi_i/zi_q (taps-1, in/out) may
+ * both be NULL (zero initial state, no state out); prev_phase may be NULL (0.0).
+ * demod: ceil(n/decim) floats; i_ds/q_ds (optional, both or neither): the decimated
+ * filter outputs.  Fast tiled kernel for taps 101/151 at decim 10; other f32 shapes
+ * use the generic kernels; u8 needs the fast shape (else SDR_EUNSUPPORTED). */
+int sdr_rf_frontend(sdr_ctx* ctx, const void* iq, int iq_dtype, int64_t n, const double* b,
+                    int taps, int decim, double* zi_i, double* zi_q, double* prev_phase,
+                    float* demod, float* i_ds, float* q_ds);
+
+/* lfilter(b, 1.0, x, zi)[::decim] on a real f32 stream.
+ * Replaces model/fmMonoBlock.py:101-105 (audio), :117/:151 (stereo BPFs, decim 1),
+ * model/fmRDSblock.py:156/:164/:180/:202 and src/filter.cpp:96-185
+ * (convolveFIR, convolveWithDecim, convolveWithDecimPointer). */
+int sdr_lfilter_decim(sdr_ctx* ctx, const float* x, int64_t n, const double* b, int taps,
+                      int decim, double* zi_inout, float* y);
+
+/* lfilter with a fused input pre-op: PRE_SQUARE filters x*x
+ * (model/fmRDSblock.py:161-164, src/filter.cpp:342-370), PRE_MIX filters
+ * (x*mix)*gain (model/fmMonoBlock.py:155-160, model/fmRDSblock.py:173-182,
+ * src/filter.cpp:373-401 convolveWithDecimAndMixer). */
+int sdr_lfilter(sdr_ctx* ctx, const float* x, const float* mix, float gain, int pre, int64_t n,
+                const double* b, int taps, int decim, double* zi_inout, float* y);
+
+/* Rational resampler: lfilter(b, 1.0, zero-stuff(x, up), zi)[::down] * up, without
+ * materialising the zero-stuffed stream; zi lives on the upsampled stream.
+ * Replaces model/fmRDSblock.py:184-199 and src/filter.cpp:301-339
+ * (convolveWithDecimMode1RDS).  y: ceil(n*up/down) floats. */
+int sdr_resample(sdr_ctx* ctx, const float* x, int64_t n, const double* b, int taps, int up,
+                 int down, double* zi_inout, float* y);
+
+/* fmDemodArctan(I, Q, prev_phase): model/fmSupportLib.py:15-44
+ * (C++: src/rf_module.cpp:13-34, which is a non-arctan approximation; this follows
+ * the Python model).  prev_phase in/out (NULL = 0.0, no state out). */
+int sdr_fm_demod(sdr_ctx* ctx, const float* I, const float* Q, int64_t n, double* prev_phase,
+                 float* out);
+
+/* fmPll(pllIn, freq, Fs, state, ncoScale, phaseAdjust, normBandwidth):
+ * model/fmPll.py:4-46 (C++ src/helper.cpp:13-57 fmPLL, src/helper.h:17-19 state).
+ * state6 = [integrator, phaseEst, feedbackI, feedbackQ, ncoOut[0], trigOffset], in/out.
+ * nco_i/nco_q: n+1 floats (index 0 = carried value); nco_q may be NULL. */
+int sdr_pll(sdr_ctx* ctx, const float* in, int64_t n, double freq, double fs, double nco_scale,
+            double phase_adj, double norm_bw, double* state6, float* nco_i, float* nco_q);
+
+/* Fused mono block: RF front end + audio lfilter + [::audio_decim], intermediate demod
+ * kept in HBM.  Replaces the body of model/fmMonoBlock.py:80-109 (one loop
+ * iteration) and src/fm_radio.cpp:66-84 + :258.  demod_out optional. */
+int sdr_mono_block(sdr_ctx* ctx, const void* iq, int iq_dtype, int64_t n, const double* rf_b,
+                   int rf_taps, int rf_decim, double* zi_i, double* zi_q, double* prev_phase,
+                   const double* audio_b, int audio_taps, int audio_decim, double* audio_zi,
+                   float* demod_out, float* audio_out);
+
+/* ================================================================================
+ * Device-pointer entry points (asynchronous on the context stream)
+ * Batched over `nstreams` independent streams laid out `stride` elements apart.
+ * `hist` = number of valid samples in memory before each stream's index 0 (0: zero
+ * pre-history as lfilter).  zf may alias zi (handled through scratch).
+ * ================================================================================ */
+int sdr_rf_frontend_dev(sdr_ctx* ctx, const void* iq, int iq_dtype, int64_t n, int64_t stride,
+                        int64_t hist, int nstreams, const double* b, int taps, int decim,
+                        const double* zi_i, const double* zi_q, int64_t zi_stride, double* zf_i,
+                        double* zf_q, double* prev_phase, float* demod, int64_t out_stride,
+                        float* i_ds, float* q_ds);
+
+int sdr_fir_dev(sdr_ctx* ctx, const float* x, const float* mix, float gain, int pre, int64_t n,
+                int64_t x_stride, int64_t hist, int nstreams, const double* b, int taps, int decim,
+                const double* zi, int64_t zi_stride, double* zf, float* y, int64_t y_stride);
+
+int sdr_resample_dev(sdr_ctx* ctx, const float* x, int64_t n, const double* b, int taps, int up,
+                     int down, const double* zi, double* zf, float* y);
+
+int sdr_fm_demod_dev(sdr_ctx* ctx, const float* I, const float* Q, int64_t n, int64_t stride,
+                     int nstreams, double* prev_phase, float* out, int64_t out_stride);
+
+int sdr_pll_dev(sdr_ctx* ctx, const float* in, int64_t n, int64_t in_stride, int nstreams,
+                double freq, double fs, double nco_scale, double phase_adj, double norm_bw,
+                double* state, float* nco_i, float* nco_q, int64_t out_stride);
+
+/* Stereo combiner, intended form of model/fmMonoBlock.py:166-170 (as in
+ * src/fm_radio.cpp:250-251): left = (mono+side)/2, right = (mono-side)/2. */
+int sdr_stereo_combine_dev(sdr_ctx* ctx, const float* mono, const float* side, int64_t n,
+                           float* left, float* right);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDR_H_ */

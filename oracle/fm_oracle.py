@@ -1,0 +1,236 @@
+"""ORACLE — test infrastructure only (never imported by the product package).
+
+CPU restatement, in float64 numpy, of the reference's per-block signal path, used
+as the checker for the HIP kernels.  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg may import this module.
+
+Pinning: the restatement is checked against golden vectors produced by running
+the reference's own functions (model/fmSupportLib.fmDemodArctan, model/fmPll.fmPll,
+model/fmRRC.impulseResponseRootRaisedCosine) and scipy.signal.lfilter/firwin in the
+reference's block loops -- tests/golden/make_golden.py, fixtures in tests/golden/.
+The reference ships no test vectors of its own, so these fixtures are
+the pin.
+
+Each function cites the reference lines it restates.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+from scipy import signal
+
+
+# ---- filtering ----------------------------------------------------------------------
+def lfilter_fir(b, x, zi=None):
+    """scipy.signal.lfilter(b, 1.0, x, zi) FIR branch, scipy 1.15.3
+    _signaltools.py:2153-2172: full = convolve(b, x); full[:T-1] += zi; y = full[:N];
+    zf = full[N:].  As called at model/fmMonoBlock.py:86-91,101,117,151,160."""
+    b = np.asarray(b, dtype=np.float64)
+    x = np.asarray(x, dtype=np.float64)
+    full = np.convolve(b, x)
+    if zi is not None:
+        zi = np.asarray(zi, dtype=np.float64)
+        full[:len(zi)] += zi
+    n = len(x)
+    y = full[:n]
+    return (y, full[n:].copy()) if zi is not None else y
+
+
+def lfilter_decim(b, x, zi, decim):
+    """lfilter(...)[::decim] (model/fmMonoBlock.py:94-95,105)."""
+    y, zf = lfilter_fir(b, x, zi)
+    return y[::decim].copy(), zf
+
+
+def resample(x, b, zi, up, down):
+    """Zero-stuff by `up`, anti-image lfilter, [::down] * up (model/fmRDSblock.py:184-199)."""
+    u = np.zeros(len(x) * up)
+    u[::up] = x
+    y, zf = lfilter_fir(b, u, zi)
+    return y[::down] * up, zf
+
+
+# ---- FM discriminator ---------------------------------------------------------------
+def fm_demod_arctan_loop(I, Q, prev_phase=0.0):
+    """Literal per-sample restatement of model/fmSupportLib.py:15-44 (small inputs)."""
+    out = np.empty(len(I))
+    for k in range(len(I)):
+        cur = math.atan2(Q[k], I[k])
+        prev_phase, cur = np.unwrap([prev_phase, cur])
+        out[k] = cur - prev_phase
+        prev_phase = cur
+    return out, prev_phase
+
+
+def fm_demod_arctan(I, Q, prev_phase=0.0):
+    """Vectorised model/fmSupportLib.py:15-44: d_k = wrap(phi_k - phi_{k-1}) with
+    np.unwrap's rule (numpy _function_base_impl.py:1790-1800); the returned state is
+    the accumulated unwrapped phase prev + sum(d)."""
+    phi = np.arctan2(np.asarray(Q, dtype=np.float64), np.asarray(I, dtype=np.float64))
+    if len(phi) == 0:
+        return np.empty(0), prev_phase
+    dd = np.diff(np.concatenate([[float(prev_phase)], phi]))
+    ddmod = np.mod(dd + np.pi, 2 * np.pi) - np.pi
+    ddmod[(ddmod == -np.pi) & (dd > 0)] = np.pi
+    d = np.where(np.abs(dd) < np.pi, dd, ddmod)
+    return d, float(prev_phase) + float(np.sum(d))
+
+
+# ---- PLL ------------------------------------------------------------------------------
+def fm_pll(pllIn, freq, Fs, state, ncoScale=1.0, phaseAdjust=0.0, normBandwidth=0.01):
+    """Restatement of model/fmPll.py:4-46 (f64, per-sample loop).  Returns
+    (ncoOut, ncoOutQ, new_state); ncoOutQ[0], never written by the reference
+    (np.empty at :13), is defined as sin(theta_prev*scale + adj) with theta_prev
+    rebuilt from the carried state (0.0 at stream start) -- DESIGN.md §6."""
+    Kp = normBandwidth * 2.666
+    Ki = normBandwidth * normBandwidth * 3.555
+    n = len(pllIn)
+    nco = np.empty(n + 1)
+    ncoq = np.empty(n + 1)
+    integ, phase, fI, fQ, nco[0], off = [float(v) for v in state]
+    w = 2 * math.pi * (freq / Fs)
+    ncoq[0] = math.sin((w * off + phase) * ncoScale + phaseAdjust) if off > 0 else 0.0
+    for k in range(n):
+        e = math.atan2(pllIn[k] * (-fQ), pllIn[k] * (+fI))
+        integ = integ + Ki * e
+        phase = phase + Kp * e + integ
+        arg = w * (off + k + 1) + phase
+        fI = math.cos(arg)
+        fQ = math.sin(arg)
+        nco[k + 1] = math.cos(arg * ncoScale + phaseAdjust)
+        ncoq[k + 1] = math.sin(arg * ncoScale + phaseAdjust)
+    return nco, ncoq, [integ, phase, fI, fQ, nco[-1], off + n]
+
+
+# ---- tap design (model/fmRRC.py:12-47) --------------------------------------------------
+def rrc_taps(Fs, N_taps):
+    Ts, beta = 1 / 2375.0, 0.90
+    h = np.empty(N_taps)
+    for k in range(N_taps):
+        t = float(k - N_taps / 2) / Fs
+        if t == 0.0:
+            h[k] = 1.0 + beta * (4 / math.pi - 1)
+        elif t == -Ts / (4 * beta) or t == Ts / (4 * beta):
+            q = math.pi / (4 * beta)
+            h[k] = beta / np.sqrt(2) * ((1 + 2 / math.pi) * math.sin(q) + (1 - 2 / math.pi) * math.cos(q))
+        else:
+            x = 4 * beta * t / Ts
+            h[k] = (math.sin(math.pi * t * (1 - beta) / Ts) + x * math.cos(math.pi * t * (1 + beta) / Ts)) / \
+                   (math.pi * t * (1 - x * x) / Ts)
+    return h
+
+
+# ---- block loops --------------------------------------------------------------------------
+def mono_coeffs(rf_taps=151, audio_taps=151):
+    """model/fmMonoBlock.py:43-45."""
+    return (signal.firwin(rf_taps, 100e3 / (2.4e6 / 2), window=("hann")),
+            signal.firwin(audio_taps, 16e3 / (240e3 / 2), window=("hann")))
+
+
+def stereo_coeffs(taps=151):
+    """model/fmMonoBlock.py:115,150,159."""
+    fs2 = 240e3 / 2
+    return (signal.firwin(taps, [18.5e3 / fs2, 19.5e3 / fs2], window=("hann"), pass_zero="bandpass"),
+            signal.firwin(taps, [22e3 / fs2, 54e3 / fs2], window=("hann"), pass_zero="bandpass"),
+            signal.firwin(taps, 16e3 / fs2, window=("hann")))
+
+
+def rds_coeffs(taps=151):
+    """model/fmRDSblock.py:88-111."""
+    fs2 = 240000 / 2
+    return dict(
+        extract=signal.firwin(taps, [54000 / fs2, 60000 / fs2], window=("hann"), pass_zero="bandpass"),
+        square=signal.firwin(taps, [113500 / fs2, 114500 / fs2], window=("hann"), pass_zero="bandpass"),
+        lpf=signal.firwin(taps, 3000 / fs2, window=("hann")),
+        anti_img=signal.firwin(taps, (57000 / 2) / ((240000 * 19) / 2), window=("hann")),
+        rrc=rrc_taps(57000, 151),
+    )
+
+
+def mono_stereo_blocks(iq, block_complex, rf_taps=151, audio_taps=151, stereo=True, nblocks=None,
+                       demod_fn=fm_demod_arctan, pll_fn=fm_pll):
+    """Restatement of the model/fmMonoBlock.py:80-173 loop (fmPll unpack fixed, intended
+    combiner).  iq: interleaved float32.  Returns a list of per-block dicts."""
+    rf_b, au_b = mono_coeffs(rf_taps, audio_taps)
+    pil_b, ext_b, st_b = stereo_coeffs(151)
+    B = 2 * block_complex
+    zi_i = np.zeros(rf_taps - 1)
+    zi_q = np.zeros(rf_taps - 1)
+    phase = 0.0
+    au_zi = np.zeros(audio_taps - 1)
+    rec_zi, ext_zi, st_zi = np.zeros(150), np.zeros(150), np.zeros(150)
+    pll_state = [0.0, 0.0, 1.0, 0.0, 1.0, 0.0]
+    out = []
+    k = 0
+    while (k + 1) * B < len(iq) and (nblocks is None or k < nblocks):   # strict "<" as :80
+        blk = iq[k * B:(k + 1) * B]
+        r = {}
+        i_f, zi_i = lfilter_fir(rf_b, blk[0::2], zi_i)
+        q_f, zi_q = lfilter_fir(rf_b, blk[1::2], zi_q)
+        r["i_ds"], r["q_ds"] = i_f[::10].copy(), q_f[::10].copy()
+        r["demod"], phase = demod_fn(r["i_ds"], r["q_ds"], phase)
+        a_f, au_zi = lfilter_fir(au_b, r["demod"], au_zi)
+        r["audio"] = a_f[::5].copy()
+        r["phase"] = phase
+        if stereo:
+            r["bpf_recovery"], rec_zi = lfilter_fir(pil_b, r["demod"], rec_zi)
+            nco, _, pll_state = pll_fn(r["bpf_recovery"], 19e3, 240e3, list(pll_state), 2)
+            r["nco"] = nco
+            r["bpf_extraction"], ext_zi = lfilter_fir(ext_b, r["demod"], ext_zi)
+            mixed = np.multiply(nco[0:len(r["bpf_extraction"])], r["bpf_extraction"]) * 2
+            s_f, st_zi = lfilter_fir(st_b, mixed, st_zi)
+            r["stereo"] = s_f[::5].copy()
+            r["left"] = (r["audio"] + r["stereo"]) / 2
+            r["right"] = (r["audio"] - r["stereo"]) / 2
+        out.append(r)
+        k += 1
+    return out
+
+
+def rds_blocks(iq_u8, block_values=307200, taps=151, nblocks=None, demod_fn=fm_demod_arctan, pll_fn=fm_pll):
+    """Restatement of model/fmRDSblock.py:127-204 (signal path up to the RRC filter).
+    iq_u8: interleaved uint8, normalised (x-128)/128 as :59."""
+    iq = (np.asarray(iq_u8, dtype=np.float64) - 128.0) / 128.0
+    rf_b, _ = mono_coeffs(taps, 151)
+    co = rds_coeffs(taps)
+    z = lambda: np.zeros(taps - 1)  # noqa: E731
+    zi_i, zi_q, phase = z(), z(), 0.0
+    ex_zi, sq_zi, li_zi, lq_zi, ai_zi, aq_zi = z(), z(), z(), z(), z(), z()
+    ri_zi, rq_zi = np.zeros(150), np.zeros(150)
+    pll_state = [0.0, 0.0, 1.0, 0.0, 1.0, 0.0]
+    phase_adj = math.pi / 3.3 - math.pi / 1.5
+    out = []
+    k = 0
+    while (k + 1) * block_values < len(iq) and (nblocks is None or k < nblocks):   # :127
+        blk = iq[k * block_values:(k + 1) * block_values]
+        r = {}
+        i_f, zi_i = lfilter_fir(rf_b, blk[0::2], zi_i)
+        q_f, zi_q = lfilter_fir(rf_b, blk[1::2], zi_q)
+        r["demod"], phase = demod_fn(i_f[::10].copy(), q_f[::10].copy(), phase)
+        r["extract"], ex_zi = lfilter_fir(co["extract"], r["demod"], ex_zi)
+        r["pre_pll"], sq_zi = lfilter_fir(co["square"], np.square(r["extract"]), sq_zi)
+        nco_i, nco_q, pll_state = pll_fn(r["pre_pll"], 114000, 240000, list(pll_state), ncoScale=0.5,
+                                         phaseAdjust=phase_adj, normBandwidth=0.001)
+        r["nco_i"], r["nco_q"] = nco_i, nco_q
+        n = len(r["extract"])
+        r["lpf_i"], li_zi = lfilter_fir(co["lpf"], np.multiply(r["extract"], nco_i[0:n]) * 2, li_zi)
+        r["lpf_q"], lq_zi = lfilter_fir(co["lpf"], np.multiply(r["extract"], nco_q[0:n]) * 2, lq_zi)
+        r["resample_i"], ai_zi = resample(r["lpf_i"], co["anti_img"], ai_zi, 19, 80)
+        r["resample_q"], aq_zi = resample(r["lpf_q"], co["anti_img"], aq_zi, 19, 80)
+        r["rrc_i"], ri_zi = lfilter_fir(co["rrc"], r["resample_i"], ri_zi)
+        r["rrc_q"], rq_zi = lfilter_fir(co["rrc"], r["resample_q"], rq_zi)
+        out.append(r)
+        k += 1
+    return out
+
+
+def mono_basic(iq, rf_taps=101, audio_taps=151, demod_fn=fm_demod_arctan):
+    """Single-pass model/fmMonoBasic.py:67-136: lfilter without state over the whole
+    capture, [::10], demod (prev 0), audio lfilter, [::5], int16(audio/2*32767)."""
+    rf_b, au_b = mono_coeffs(rf_taps, audio_taps)
+    i_f = lfilter_fir(rf_b, iq[0::2])
+    q_f = lfilter_fir(rf_b, iq[1::2])
+    demod, _ = demod_fn(i_f[::10], q_f[::10], 0.0)
+    audio = lfilter_fir(au_b, demod)[::5]
+    return audio, np.int16((audio / 2) * 32767)

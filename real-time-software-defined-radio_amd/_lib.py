@@ -1,0 +1,254 @@
+"""ctypes binding of libsdr.so (the C-ABI in include/sdr.h).
+
+The product path always runs the HIP kernels in libsdr.so.  There is no CPU
+fallback: if the library is missing or no GPU is visible, every compute call
+raises ``SdrUnavailable`` (a RuntimeError) with the reason.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SDR_LIB", os.path.join(_HERE, "libsdr.so"))
+
+SDR_OK, SDR_EINVAL, SDR_EHIP, SDR_ENOMEM, SDR_EUNSUPPORTED = 0, -1, -2, -3, -4
+SDR_IQ_F32, SDR_IQ_U8 = 0, 1
+SDR_PRE_NONE, SDR_PRE_SQUARE, SDR_PRE_MIX = 0, 1, 2
+
+
+class SdrUnavailable(RuntimeError):
+    """libsdr.so cannot be loaded or no HIP device is usable."""
+
+
+class SdrError(RuntimeError):
+    """A HIP runtime failure inside libsdr.so."""
+
+
+_c = ctypes
+_i64, _i32, _f32, _f64 = _c.c_int64, _c.c_int, _c.c_float, _c.c_double
+_vp, _dp, _fp = _c.c_void_p, _c.POINTER(_c.c_double), _c.POINTER(_c.c_float)
+
+# name -> (restype, argtypes); must match include/sdr.h one for one
+SIGNATURES = {
+    "sdr_abi_version": (_i32, []),
+    "sdr_last_error": (_c.c_char_p, []),
+    "sdr_device_count": (_i32, [_c.POINTER(_i32)]),
+    "sdr_create": (_i32, [_i32, _c.POINTER(_vp)]),
+    "sdr_destroy": (None, [_vp]),
+    "sdr_synchronize": (_i32, [_vp]),
+    "sdr_stream": (_vp, [_vp]),
+    "sdr_malloc": (_i32, [_vp, _i64, _c.POINTER(_vp)]),
+    "sdr_free": (_i32, [_vp, _vp]),
+    "sdr_memcpy_h2d": (_i32, [_vp, _vp, _vp, _i64]),
+    "sdr_memcpy_d2h": (_i32, [_vp, _vp, _vp, _i64]),
+    "sdr_memcpy_d2d": (_i32, [_vp, _vp, _vp, _i64]),
+    "sdr_memset": (_i32, [_vp, _vp, _i32, _i64]),
+    "sdr_event_create": (_i32, [_vp, _c.POINTER(_vp)]),
+    "sdr_event_record": (_i32, [_vp, _vp]),
+    "sdr_event_elapsed_ms": (_i32, [_vp, _vp, _c.POINTER(_f32)]),
+    "sdr_event_destroy": (_i32, [_vp]),
+    "sdr_rf_frontend": (_i32, [_vp, _vp, _i32, _i64, _dp, _i32, _i32, _dp, _dp, _dp, _fp, _fp, _fp]),
+    "sdr_lfilter_decim": (_i32, [_vp, _fp, _i64, _dp, _i32, _i32, _dp, _fp]),
+    "sdr_lfilter": (_i32, [_vp, _fp, _fp, _f32, _i32, _i64, _dp, _i32, _i32, _dp, _fp]),
+    "sdr_resample": (_i32, [_vp, _fp, _i64, _dp, _i32, _i32, _i32, _dp, _fp]),
+    "sdr_fm_demod": (_i32, [_vp, _fp, _fp, _i64, _dp, _fp]),
+    "sdr_pll": (_i32, [_vp, _fp, _i64, _f64, _f64, _f64, _f64, _f64, _dp, _fp, _fp]),
+    "sdr_mono_block": (_i32, [_vp, _vp, _i32, _i64, _dp, _i32, _i32, _dp, _dp, _dp, _dp, _i32, _i32,
+                              _dp, _fp, _fp]),
+    "sdr_rf_frontend_dev": (_i32, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _dp, _i32, _i32, _vp, _vp,
+                                   _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "sdr_fir_dev": (_i32, [_vp, _vp, _vp, _f32, _i32, _i64, _i64, _i64, _i32, _dp, _i32, _i32, _vp,
+                           _i64, _vp, _vp, _i64]),
+    "sdr_resample_dev": (_i32, [_vp, _vp, _i64, _dp, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "sdr_fm_demod_dev": (_i32, [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _i64]),
+    "sdr_pll_dev": (_i32, [_vp, _vp, _i64, _i64, _i32, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp,
+                           _i64]),
+    "sdr_stereo_combine_dev": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libsdr.so and declare every prototype (no GPU is touched)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise SdrUnavailable(
+                f"{path} not found: build it with `make -C real-time-software-defined-radio_amd/csrc` "
+                "or `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.sdr_abi_version() != 1:
+            raise SdrUnavailable("libsdr.so ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    return load_library().sdr_last_error().decode(errors="replace")
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == SDR_OK:
+        return
+    msg = f"{what}: {last_error()}" if what else last_error()
+    if rc == SDR_EINVAL:
+        raise ValueError(msg)
+    if rc == SDR_EUNSUPPORTED:
+        raise NotImplementedError(msg)
+    if rc == SDR_ENOMEM:
+        raise MemoryError(msg)
+    raise SdrError(msg)
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = _i32(0)
+    rc = lib.sdr_device_count(_c.byref(n))
+    return n.value if rc == SDR_OK else 0
+
+
+class Context:
+    """One HIP stream + scratch memory on one device (sdr_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        if device_count() <= device:
+            raise SdrUnavailable(f"no HIP device {device} visible to libsdr.so ({last_error() or 'none'})")
+        h = _vp()
+        check(self.lib.sdr_create(int(device), _c.byref(h)), "sdr_create")
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.sdr_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        check(self.lib.sdr_synchronize(self.handle), "sdr_synchronize")
+
+
+_tls = threading.local()
+
+
+def default_device() -> int:
+    for var in ("SDR_DEVICE", "LOCAL_RANK"):
+        if os.environ.get(var, "").strip():
+            return int(os.environ[var])
+    return 0
+
+
+def get_context() -> Context:
+    """Per-thread default context (a context is not thread-safe)."""
+    ctx = getattr(_tls, "ctx", None)
+    if ctx is None:
+        ctx = Context(default_device())
+        _tls.ctx = ctx
+    return ctx
+
+
+# ---- small helpers ----------------------------------------------------------------
+def f32p(a: np.ndarray):
+    return a.ctypes.data_as(_fp) if a is not None else None
+
+
+def f64p(a: np.ndarray):
+    return a.ctypes.data_as(_dp) if a is not None else None
+
+
+def c_f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def c_f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class DeviceBuffer:
+    """Owned device allocation (sdr_malloc) with host copy helpers."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = _vp()
+        check(ctx.lib.sdr_malloc(ctx.handle, self.nbytes, _c.byref(p)), "sdr_malloc")
+        self.ptr = p.value
+
+    @classmethod
+    def from_array(cls, ctx: Context, a: np.ndarray) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        buf = cls(ctx, max(a.nbytes, 16))
+        buf.upload(a)
+        return buf
+
+    def upload(self, a: np.ndarray, offset: int = 0):
+        a = np.ascontiguousarray(a)
+        if a.nbytes + offset > self.nbytes:
+            raise ValueError("upload larger than device buffer")
+        check(self.ctx.lib.sdr_memcpy_h2d(self.ctx.handle, self.ptr + offset, a.ctypes.data, a.nbytes), "h2d")
+
+    def download(self, count: int, dtype=np.float32, offset: int = 0) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes + offset > self.nbytes:
+            raise ValueError("download larger than device buffer")
+        check(self.ctx.lib.sdr_memcpy_d2h(self.ctx.handle, out.ctypes.data, self.ptr + offset, out.nbytes), "d2h")
+        return out
+
+    def zero(self):
+        check(self.ctx.lib.sdr_memset(self.ctx.handle, self.ptr, 0, self.nbytes), "memset")
+
+    def free(self):
+        if self.ptr:
+            self.ctx.lib.sdr_free(self.ctx.handle, self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Timer:
+    """HIP events recorded on the context stream (where the kernels run)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.ev = []
+
+    def event(self):
+        p = _vp()
+        check(self.ctx.lib.sdr_event_create(self.ctx.handle, _c.byref(p)), "event_create")
+        self.ev.append(p.value)
+        return p.value
+
+    def record(self, ev):
+        check(self.ctx.lib.sdr_event_record(self.ctx.handle, ev), "event_record")
+
+    def elapsed_ms(self, e0, e1) -> float:
+        ms = _f32(0.0)
+        check(self.ctx.lib.sdr_event_elapsed_ms(e0, e1, _c.byref(ms)), "event_elapsed")
+        return ms.value
+
+    def close(self):
+        for e in self.ev:
+            self.ctx.lib.sdr_event_destroy(e)
+        self.ev = []

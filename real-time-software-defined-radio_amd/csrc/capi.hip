@@ -1,0 +1,691 @@
+// C-ABI of libsdr.so: the drop-in boundary declared in include/sdr.h.
+//
+// Two families of entry points:
+//   * host-buffer, synchronous ("drop-in"): same argument meaning as the reference
+//     per-block functions (lfilter(b,1,x,zi) + [::D], fmDemodArctan, fmPll, ...);
+//     inputs are copied to HBM, kernels run on the context's stream, outputs and the
+//     updated filter/demod/PLL state are copied back.
+//   * device-pointer, asynchronous (`*_dev`): the same kernels on caller-owned device
+//     buffers, enqueued on the context's stream; used by the batched benchmark and
+//     by the device-resident block pipelines (the Python package keeps all
+//     intermediates and states in HBM and only fetches the outputs).
+// Every entry point returns 0 or a negative SDR_E* code; sdr_last_error() gives the
+// message of the calling thread's last failure.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <deque>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sdr_common.h"
+#include "../../include/sdr.h"
+
+// ---- launchers implemented in fe.hip / fir.hip / pll.hip ----------------------
+struct FeLaunch {
+  const void* iq; int64_t n; int64_t stride; int64_t hist; int nstreams;
+  const float* taps_dev; const TapsF32* taps; int T; int D; int u8;
+  const double* zi_i; const double* zi_q; int64_t zi_stride; const double* prev_phase;
+  float* demod; int64_t out_stride; float* i_ds; float* q_ds; float* last_phi; int* wraps;
+};
+struct FirLaunch {
+  const float* x; const float* c; float gain; int pre; int64_t n; int64_t x_stride; int64_t x_step;
+  int64_t hist; int nstreams; const float* taps_dev; const TapsF32* taps; int T; int D;
+  const double* zi; int64_t zi_stride; float* y; int64_t y_stride;
+};
+struct PllCfg { double freq, fs, scale, adj, kp, ki; };
+
+hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st);
+hipError_t sdr_launch_iq_zf(const void* iq, int u8, int64_t n, int64_t stride, int nstreams,
+                            const double* b_dev, int T, const double* zi_i, const double* zi_q,
+                            int64_t zi_stride, double* zf_i, double* zf_q, hipStream_t st);
+hipError_t sdr_launch_demod(const float* I, const float* Q, int64_t n, int64_t stride, int nstreams,
+                            const double* prev_phase, float* out, int64_t out_stride,
+                            float* last_phi, int* wraps, hipStream_t st);
+hipError_t sdr_launch_demod_state(int nstreams, int64_t m, const float* last_phi, const int* wraps,
+                                  double* prev_phase, hipStream_t st);
+hipError_t sdr_launch_fir(const FirLaunch& a, hipStream_t st);
+hipError_t sdr_launch_resample(const float* x, int64_t n, const float* taps_dev, int T, int U, int D,
+                               const double* zi, float* y, hipStream_t st);
+hipError_t sdr_launch_zf(const float* x, const float* c, float gain, int pre, int64_t n,
+                         int64_t x_stride, int nstreams, int U, const double* b_dev, int T,
+                         const double* zi, int64_t zi_stride, double* zf, hipStream_t st);
+hipError_t sdr_launch_combine(const float* mono, const float* side, int64_t n, float* left,
+                              float* right, hipStream_t st);
+hipError_t sdr_launch_pll(const float* in, int64_t n, int64_t in_stride, int nstreams,
+                          const PllCfg& cfg, double* state_dev, double* theta, int64_t th_stride,
+                          double* nco0, double* ncoq0, float* nco_i, float* nco_q,
+                          int64_t out_stride, hipStream_t st);
+
+// ---- context ------------------------------------------------------------------
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(SDR_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+// scratch slots owned by a context (grown on demand, never shrunk)
+enum Slot {
+  S_IN, S_IN2, S_OUT, S_OUT2, S_OUT3, S_OUT4, S_STATE, S_STATE2, S_MISC, S_THETA, S_PHI, S_WRAP,
+  S_NSLOT
+};
+
+struct TapSet {
+  std::vector<double> b;
+  TapsF32 h;
+  float* dev_f32 = nullptr;
+  double* dev_f64 = nullptr;
+};
+
+}  // namespace
+
+struct sdr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  void* slot[S_NSLOT] = {};
+  size_t cap[S_NSLOT] = {};
+  std::deque<TapSet> taps;  // small cache (deque: stable element addresses) of uploaded tap sets (taps are designed once)
+};
+
+namespace {
+
+int set_dev(sdr_ctx* c) {
+  HIP_TRY(hipSetDevice(c->device));
+  return SDR_OK;
+}
+
+int scratch(sdr_ctx* c, Slot s, size_t bytes, void** out) {
+  if (bytes == 0) bytes = 16;
+  if (c->cap[s] < bytes) {
+    if (c->slot[s]) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(hipFree(c->slot[s]));
+      c->slot[s] = nullptr;
+      c->cap[s] = 0;
+    }
+    size_t want = bytes + bytes / 4;
+    hipError_t e = hipMalloc(&c->slot[s], want);
+    if (e != hipSuccess) return fail(SDR_ENOMEM, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
+    c->cap[s] = want;
+  }
+  *out = c->slot[s];
+  return SDR_OK;
+}
+
+int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out) {
+  if (b == nullptr) return fail(SDR_EINVAL, "taps pointer is NULL");
+  if (T < 1 || T > SDR_MAX_TAPS) return fail(SDR_EINVAL, "taps=%d outside [1, %d]", T, SDR_MAX_TAPS);
+  for (const TapSet& t : c->taps)
+    if ((int)t.b.size() == T && std::memcmp(t.b.data(), b, sizeof(double) * T) == 0) {
+      *out = &t;
+      return SDR_OK;
+    }
+  if (c->taps.size() >= 64) {  // bounded cache: drop everything (rare: taps change per block)
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (TapSet& t : c->taps) { (void)hipFree(t.dev_f32); (void)hipFree(t.dev_f64); }
+    c->taps.clear();
+  }
+  TapSet t;
+  t.b.assign(b, b + T);
+  std::memset(&t.h, 0, sizeof t.h);
+  for (int k = 0; k < T; ++k) t.h.h[k] = (float)b[k];
+  HIP_TRY(hipMalloc(&t.dev_f32, sizeof(float) * SDR_MAX_TAPS));
+  HIP_TRY(hipMalloc(&t.dev_f64, sizeof(double) * SDR_MAX_TAPS));
+  HIP_TRY(hipMemcpy(t.dev_f32, t.h.h, sizeof(float) * T, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(t.dev_f64, b, sizeof(double) * T, hipMemcpyHostToDevice));
+  c->taps.push_back(std::move(t));
+  *out = &c->taps.back();
+  return SDR_OK;
+}
+
+#define TRY(expr)                 \
+  do {                            \
+    int r_ = (expr);              \
+    if (r_ != SDR_OK) return r_;  \
+  } while (0)
+
+#define CHECK_CTX(c) \
+  if ((c) == nullptr) return fail(SDR_EINVAL, "context is NULL")
+
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+int h2d(sdr_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (bytes) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+  return SDR_OK;
+}
+int d2h(sdr_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (bytes) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  return SDR_OK;
+}
+
+}  // namespace
+
+// ================================================================================
+extern "C" {
+
+int sdr_abi_version(void) { return SDR_ABI_VERSION; }
+
+const char* sdr_last_error(void) { return g_err.c_str(); }
+
+int sdr_device_count(int* n) {
+  if (n == nullptr) return fail(SDR_EINVAL, "n is NULL");
+  *n = 0;
+  hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess) { *n = 0; return fail(SDR_EHIP, "hipGetDeviceCount: %s", hipGetErrorString(e)); }
+  return SDR_OK;
+}
+
+int sdr_create(int device, sdr_ctx** out) {
+  if (out == nullptr) return fail(SDR_EINVAL, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  TRY(sdr_device_count(&n));
+  if (device < 0 || device >= n) return fail(SDR_EINVAL, "device %d not in [0, %d)", device, n);
+  sdr_ctx* c = new sdr_ctx;
+  c->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(SDR_EHIP, "context creation on device %d: %s", device, hipGetErrorString(e));
+  }
+  *out = c;
+  return SDR_OK;
+}
+
+void sdr_destroy(sdr_ctx* c) {
+  if (c == nullptr) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (int s = 0; s < S_NSLOT; ++s) if (c->slot[s]) (void)hipFree(c->slot[s]);
+  for (TapSet& t : c->taps) { (void)hipFree(t.dev_f32); (void)hipFree(t.dev_f64); }
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int sdr_synchronize(sdr_ctx* c) {
+  CHECK_CTX(c);
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SDR_OK;
+}
+
+void* sdr_stream(sdr_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+// ---- device memory ---------------------------------------------------------------
+int sdr_malloc(sdr_ctx* c, int64_t bytes, void** out) {
+  CHECK_CTX(c);
+  if (out == nullptr || bytes < 0) return fail(SDR_EINVAL, "bad sdr_malloc arguments");
+  TRY(set_dev(c));
+  hipError_t e = hipMalloc(out, bytes ? (size_t)bytes : 16);
+  if (e != hipSuccess) return fail(SDR_ENOMEM, "hipMalloc(%lld): %s", (long long)bytes, hipGetErrorString(e));
+  return SDR_OK;
+}
+
+int sdr_free(sdr_ctx* c, void* p) {
+  CHECK_CTX(c);
+  if (p) HIP_TRY(hipFree(p));
+  return SDR_OK;
+}
+
+int sdr_memcpy_h2d(sdr_ctx* c, void* dst, const void* src, int64_t bytes) {
+  CHECK_CTX(c);
+  TRY(h2d(c, dst, src, (size_t)bytes));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SDR_OK;
+}
+
+int sdr_memcpy_d2h(sdr_ctx* c, void* dst, const void* src, int64_t bytes) {
+  CHECK_CTX(c);
+  TRY(d2h(c, dst, src, (size_t)bytes));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SDR_OK;
+}
+
+int sdr_memcpy_d2d(sdr_ctx* c, void* dst, const void* src, int64_t bytes) {
+  CHECK_CTX(c);
+  if (bytes) HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, c->stream));
+  return SDR_OK;
+}
+
+int sdr_memset(sdr_ctx* c, void* dst, int value, int64_t bytes) {
+  CHECK_CTX(c);
+  if (bytes) HIP_TRY(hipMemsetAsync(dst, value, (size_t)bytes, c->stream));
+  return SDR_OK;
+}
+
+// ---- events (timing on the context stream, where the kernels run) ------------------
+int sdr_event_create(sdr_ctx* c, void** ev) {
+  CHECK_CTX(c);
+  if (ev == nullptr) return fail(SDR_EINVAL, "ev is NULL");
+  TRY(set_dev(c));
+  hipEvent_t e;
+  HIP_TRY(hipEventCreate(&e));
+  *ev = (void*)e;
+  return SDR_OK;
+}
+int sdr_event_record(sdr_ctx* c, void* ev) {
+  CHECK_CTX(c);
+  HIP_TRY(hipEventRecord((hipEvent_t)ev, c->stream));
+  return SDR_OK;
+}
+int sdr_event_elapsed_ms(void* ev0, void* ev1, float* ms) {
+  if (ms == nullptr) return fail(SDR_EINVAL, "ms is NULL");
+  HIP_TRY(hipEventSynchronize((hipEvent_t)ev1));
+  HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)ev0, (hipEvent_t)ev1));
+  return SDR_OK;
+}
+int sdr_event_destroy(void* ev) {
+  if (ev) HIP_TRY(hipEventDestroy((hipEvent_t)ev));
+  return SDR_OK;
+}
+
+// ================================================================================
+// Device-pointer API (asynchronous on the context stream)
+// ================================================================================
+int sdr_rf_frontend_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t stride,
+                        int64_t hist, int nstreams, const double* b, int taps, int decim,
+                        const double* zi_i, const double* zi_q, int64_t zi_stride, double* zf_i,
+                        double* zf_q, double* prev_phase, float* demod, int64_t out_stride,
+                        float* i_ds, float* q_ds) {
+  CHECK_CTX(c);
+  if (n < 0 || nstreams < 0 || hist < 0) return fail(SDR_EINVAL, "negative size");
+  if (iq_dtype != SDR_IQ_F32 && iq_dtype != SDR_IQ_U8) return fail(SDR_EINVAL, "iq_dtype %d", iq_dtype);
+  if (decim < 1) return fail(SDR_EINVAL, "decim=%d < 1", decim);
+  if ((zi_i == nullptr) != (zi_q == nullptr)) return fail(SDR_EINVAL, "zi_i/zi_q must both be set or NULL");
+  if ((zf_i == nullptr) != (zf_q == nullptr)) return fail(SDR_EINVAL, "zf_i/zf_q must both be set or NULL");
+  if ((i_ds == nullptr) != (q_ds == nullptr)) return fail(SDR_EINVAL, "i_ds/q_ds must both be set or NULL");
+  const int64_t M = ceil_div(n, decim);
+  if (n > 0 && (iq == nullptr || demod == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  if (nstreams > 1 && (out_stride < M || stride < n)) return fail(SDR_EINVAL, "stream strides too small");
+  if (nstreams > 1 && zi_i && zi_stride < taps - 1) return fail(SDR_EINVAL, "zi_stride too small");
+  TRY(set_dev(c));
+  const TapSet* ts;
+  TRY(get_taps(c, b, taps, &ts));
+  const int u8 = iq_dtype == SDR_IQ_U8;
+  const int G = u8 ? 8 : 2;
+  float* last_phi = nullptr;
+  int* wraps = nullptr;
+  if (prev_phase != nullptr) {
+    TRY(scratch(c, S_PHI, sizeof(float) * (size_t)nstreams, (void**)&last_phi));
+    TRY(scratch(c, S_WRAP, sizeof(int) * (size_t)nstreams, (void**)&wraps));
+    HIP_TRY(hipMemsetAsync(wraps, 0, sizeof(int) * (size_t)nstreams, c->stream));
+  }
+  // zf first (reads zi), into scratch when it aliases zi
+  double* zfi = zf_i;
+  double* zfq = zf_q;
+  const bool alias = zf_i && (zf_i == zi_i || zf_q == zi_q);
+  const int64_t zs = nstreams > 1 ? zi_stride : (taps - 1);
+  if (alias) {
+    double* tmp;
+    TRY(scratch(c, S_STATE2, sizeof(double) * 2 * (size_t)zs * nstreams, (void**)&tmp));
+    zfi = tmp;
+    zfq = tmp + zs * nstreams;
+  }
+  const bool fast = (taps == 101 || taps == 151) && decim == 10 &&
+                    (nstreams <= 1 || stride % G == 0) && ((uintptr_t)iq % 16) == 0;
+  if (fast) {
+    FeLaunch a{iq, n, nstreams > 1 ? stride : ceil_div(n, G) * G, hist, nstreams,
+               ts->dev_f32, &ts->h, taps, decim, u8, zi_i, zi_q, zs, prev_phase,
+               demod, nstreams > 1 ? out_stride : M, i_ds, q_ds, last_phi, wraps};
+    HIP_TRY(sdr_launch_fe(a, c->stream));
+  } else {
+    // generic tap counts: strided FIR on I and Q, then the standalone discriminator
+    if (u8) return fail(SDR_EUNSUPPORTED, "u8 IQ needs taps 101/151 and decim 10 (got %d, %d)", taps, decim);
+    float *fi = i_ds, *fq = q_ds;
+    const int64_t os = nstreams > 1 ? out_stride : M;
+    if (fi == nullptr) {
+      float* tmp;
+      TRY(scratch(c, S_OUT4, sizeof(float) * 2 * (size_t)os * nstreams, (void**)&tmp));
+      fi = tmp;
+      fq = tmp + os * nstreams;
+    }
+    const float* x = (const float*)iq;
+    const int64_t xs = 2 * (nstreams > 1 ? stride : n);
+    FirLaunch a{x, nullptr, 1.f, 0, n, xs, 2, hist, nstreams, ts->dev_f32, &ts->h, taps, decim,
+                zi_i, zs, fi, os};
+    HIP_TRY(sdr_launch_fir(a, c->stream));
+    a.x = x + 1; a.zi = zi_q; a.y = fq;
+    HIP_TRY(sdr_launch_fir(a, c->stream));
+    HIP_TRY(sdr_launch_demod(fi, fq, M, os, nstreams, prev_phase, demod, os, last_phi, wraps, c->stream));
+  }
+  if (zf_i != nullptr)
+    HIP_TRY(sdr_launch_iq_zf(iq, u8, n, nstreams > 1 ? stride : n, nstreams, ts->dev_f64, taps,
+                             zi_i, zi_q, zs, zfi, zfq, c->stream));
+  if (alias) {
+    HIP_TRY(hipMemcpyAsync(zf_i, zfi, sizeof(double) * zs * nstreams, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(zf_q, zfq, sizeof(double) * zs * nstreams, hipMemcpyDeviceToDevice, c->stream));
+  }
+  if (prev_phase != nullptr)
+    HIP_TRY(sdr_launch_demod_state(nstreams, M, last_phi, wraps, prev_phase, c->stream));
+  return SDR_OK;
+}
+
+int sdr_fir_dev(sdr_ctx* c, const float* x, const float* mix, float gain, int pre, int64_t n,
+                int64_t x_stride, int64_t hist, int nstreams, const double* b, int taps, int decim,
+                const double* zi, int64_t zi_stride, double* zf, float* y, int64_t y_stride) {
+  CHECK_CTX(c);
+  if (n < 0 || nstreams < 0 || hist < 0) return fail(SDR_EINVAL, "negative size");
+  if (decim < 1) return fail(SDR_EINVAL, "decim=%d < 1", decim);
+  if (pre < SDR_PRE_NONE || pre > SDR_PRE_MIX) return fail(SDR_EINVAL, "pre=%d", pre);
+  if (pre == SDR_PRE_MIX && mix == nullptr) return fail(SDR_EINVAL, "PRE_MIX needs the mix operand");
+  const int64_t M = ceil_div(n, decim);
+  if (n > 0 && (x == nullptr || y == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  if (nstreams > 1 && (y_stride < M || x_stride < n)) return fail(SDR_EINVAL, "stream strides too small");
+  TRY(set_dev(c));
+  const TapSet* ts;
+  TRY(get_taps(c, b, taps, &ts));
+  const int64_t zs = nstreams > 1 ? zi_stride : (taps - 1);
+  const int64_t xs = nstreams > 1 ? x_stride : n;
+  double* zfo = zf;
+  const bool alias = zf && zf == zi;
+  if (alias) TRY(scratch(c, S_STATE2, sizeof(double) * (size_t)zs * nstreams, (void**)&zfo));
+  FirLaunch a{x, mix, gain, pre, n, xs, 1, hist, nstreams, ts->dev_f32, &ts->h, taps, decim,
+              zi, zs, y, nstreams > 1 ? y_stride : M};
+  HIP_TRY(sdr_launch_fir(a, c->stream));
+  if (zf != nullptr)
+    HIP_TRY(sdr_launch_zf(x, mix, gain, pre, n, xs, nstreams, 1, ts->dev_f64, taps, zi, zs, zfo, c->stream));
+  if (alias)
+    HIP_TRY(hipMemcpyAsync(zf, zfo, sizeof(double) * zs * nstreams, hipMemcpyDeviceToDevice, c->stream));
+  return SDR_OK;
+}
+
+int sdr_resample_dev(sdr_ctx* c, const float* x, int64_t n, const double* b, int taps, int up,
+                     int down, const double* zi, double* zf, float* y) {
+  CHECK_CTX(c);
+  if (n < 0 || up < 1 || down < 1) return fail(SDR_EINVAL, "bad resampler sizes");
+  if (n > 0 && (x == nullptr || y == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  const TapSet* ts;
+  TRY(get_taps(c, b, taps, &ts));
+  double* zfo = zf;
+  const bool alias = zf && zf == zi;
+  if (alias) TRY(scratch(c, S_STATE2, sizeof(double) * (size_t)taps, (void**)&zfo));
+  HIP_TRY(sdr_launch_resample(x, n, ts->dev_f32, taps, up, down, zi, y, c->stream));
+  if (zf != nullptr)
+    HIP_TRY(sdr_launch_zf(x, nullptr, 1.f, 0, n, n, 1, up, ts->dev_f64, taps, zi, taps - 1, zfo, c->stream));
+  if (alias)
+    HIP_TRY(hipMemcpyAsync(zf, zfo, sizeof(double) * (taps - 1), hipMemcpyDeviceToDevice, c->stream));
+  return SDR_OK;
+}
+
+int sdr_fm_demod_dev(sdr_ctx* c, const float* I, const float* Q, int64_t n, int64_t stride,
+                     int nstreams, double* prev_phase, float* out, int64_t out_stride) {
+  CHECK_CTX(c);
+  if (n < 0 || nstreams < 0) return fail(SDR_EINVAL, "negative size");
+  if (n > 0 && (I == nullptr || Q == nullptr || out == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  float* last_phi = nullptr;
+  int* wraps = nullptr;
+  if (prev_phase != nullptr) {
+    TRY(scratch(c, S_PHI, sizeof(float) * (size_t)nstreams, (void**)&last_phi));
+    TRY(scratch(c, S_WRAP, sizeof(int) * (size_t)nstreams, (void**)&wraps));
+    HIP_TRY(hipMemsetAsync(wraps, 0, sizeof(int) * (size_t)nstreams, c->stream));
+  }
+  const int64_t xs = nstreams > 1 ? stride : n;
+  HIP_TRY(sdr_launch_demod(I, Q, n, xs, nstreams, prev_phase, out, nstreams > 1 ? out_stride : n,
+                           last_phi, wraps, c->stream));
+  if (prev_phase != nullptr)
+    HIP_TRY(sdr_launch_demod_state(nstreams, n, last_phi, wraps, prev_phase, c->stream));
+  return SDR_OK;
+}
+
+int sdr_pll_dev(sdr_ctx* c, const float* in, int64_t n, int64_t in_stride, int nstreams,
+                double freq, double fs, double nco_scale, double phase_adj, double norm_bw,
+                double* state, float* nco_i, float* nco_q, int64_t out_stride) {
+  CHECK_CTX(c);
+  if (n < 0 || nstreams < 0) return fail(SDR_EINVAL, "negative size");
+  if (state == nullptr || nco_i == nullptr || (n > 0 && in == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  if (!(fs != 0.0)) return fail(SDR_EINVAL, "Fs must be non-zero");
+  TRY(set_dev(c));
+  PllCfg cfg{freq, fs, nco_scale, phase_adj, norm_bw * 2.666, norm_bw * norm_bw * 3.555};
+  double* theta;
+  double* misc;
+  const int64_t ths = n > 0 ? n : 1;
+  TRY(scratch(c, S_THETA, sizeof(double) * (size_t)ths * nstreams, (void**)&theta));
+  TRY(scratch(c, S_MISC, sizeof(double) * 2 * (size_t)nstreams, (void**)&misc));
+  HIP_TRY(sdr_launch_pll(in, n, nstreams > 1 ? in_stride : n, nstreams, cfg, state, theta, ths, misc,
+                         misc + nstreams, nco_i, nco_q, nstreams > 1 ? out_stride : n + 1, c->stream));
+  return SDR_OK;
+}
+
+int sdr_stereo_combine_dev(sdr_ctx* c, const float* mono, const float* side, int64_t n, float* left,
+                           float* right) {
+  CHECK_CTX(c);
+  if (n < 0) return fail(SDR_EINVAL, "negative size");
+  if (n > 0 && (!mono || !side || !left || !right)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  HIP_TRY(sdr_launch_combine(mono, side, n, left, right, c->stream));
+  return SDR_OK;
+}
+
+// ================================================================================
+// Host-buffer drop-in API (synchronous)
+// ================================================================================
+int sdr_rf_frontend(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, const double* b, int taps,
+                    int decim, double* zi_i, double* zi_q, double* prev_phase, float* demod,
+                    float* i_ds, float* q_ds) {
+  CHECK_CTX(c);
+  if (n < 0) return fail(SDR_EINVAL, "negative size");
+  if (iq_dtype != SDR_IQ_F32 && iq_dtype != SDR_IQ_U8) return fail(SDR_EINVAL, "iq_dtype %d", iq_dtype);
+  if (taps < 1 || taps > SDR_MAX_TAPS) return fail(SDR_EINVAL, "taps=%d outside [1, %d]", taps, SDR_MAX_TAPS);
+  if (decim < 1) return fail(SDR_EINVAL, "decim=%d < 1", decim);
+  if ((zi_i == nullptr) != (zi_q == nullptr)) return fail(SDR_EINVAL, "zi_i/zi_q must both be set or NULL");
+  if ((i_ds == nullptr) != (q_ds == nullptr)) return fail(SDR_EINVAL, "i_ds/q_ds must both be set or NULL");
+  if (n > 0 && (iq == nullptr || demod == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  const int64_t M = ceil_div(n, decim);
+  const size_t in_bytes = (size_t)n * (iq_dtype == SDR_IQ_U8 ? 2 : 8);
+  void* d_iq;
+  float* d_out;
+  double* d_st;
+  TRY(scratch(c, S_IN, in_bytes, &d_iq));
+  TRY(scratch(c, S_OUT, sizeof(float) * 3 * (size_t)(M + 4), (void**)&d_out));
+  const int Z = taps - 1;
+  TRY(scratch(c, S_STATE, sizeof(double) * (4 * (size_t)Z + 1), (void**)&d_st));
+  double *dzi = d_st, *dzq = d_st + Z, *dfi = d_st + 2 * Z, *dfq = d_st + 3 * Z, *dph = d_st + 4 * Z;
+  TRY(h2d(c, d_iq, iq, in_bytes));
+  if (zi_i) {
+    TRY(h2d(c, dzi, zi_i, sizeof(double) * Z));
+    TRY(h2d(c, dzq, zi_q, sizeof(double) * Z));
+  }
+  const double ph0 = prev_phase ? *prev_phase : 0.0;
+  TRY(h2d(c, dph, &ph0, sizeof(double)));
+  float* dI = i_ds ? d_out + (M + 4) : nullptr;
+  float* dQ = i_ds ? d_out + 2 * (M + 4) : nullptr;
+  TRY(sdr_rf_frontend_dev(c, d_iq, iq_dtype, n, n, 0, 1, b, taps, decim, zi_i ? dzi : nullptr,
+                          zi_i ? dzq : nullptr, Z, zi_i ? dfi : nullptr, zi_i ? dfq : nullptr,
+                          dph, d_out, M, dI, dQ));
+  TRY(d2h(c, demod, d_out, sizeof(float) * M));
+  if (i_ds) {
+    TRY(d2h(c, i_ds, dI, sizeof(float) * M));
+    TRY(d2h(c, q_ds, dQ, sizeof(float) * M));
+  }
+  if (zi_i) {
+    TRY(d2h(c, zi_i, dfi, sizeof(double) * Z));
+    TRY(d2h(c, zi_q, dfq, sizeof(double) * Z));
+  }
+  double ph1 = ph0;
+  TRY(d2h(c, &ph1, dph, sizeof(double)));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (prev_phase) *prev_phase = ph1;
+  return SDR_OK;
+}
+
+int sdr_lfilter(sdr_ctx* c, const float* x, const float* mix, float gain, int pre, int64_t n,
+                const double* b, int taps, int decim, double* zi_inout, float* y) {
+  CHECK_CTX(c);
+  if (n < 0) return fail(SDR_EINVAL, "negative size");
+  if (taps < 1 || taps > SDR_MAX_TAPS) return fail(SDR_EINVAL, "taps=%d outside [1, %d]", taps, SDR_MAX_TAPS);
+  if (decim < 1) return fail(SDR_EINVAL, "decim=%d < 1", decim);
+  if (pre < SDR_PRE_NONE || pre > SDR_PRE_MIX) return fail(SDR_EINVAL, "pre=%d", pre);
+  if (pre == SDR_PRE_MIX && mix == nullptr) return fail(SDR_EINVAL, "PRE_MIX needs the mix operand");
+  if (n > 0 && (x == nullptr || y == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  const int64_t M = ceil_div(n, decim);
+  float *dx, *dc = nullptr, *dy;
+  double* dz;
+  const int Z = taps - 1;
+  TRY(scratch(c, S_IN, sizeof(float) * (size_t)n, (void**)&dx));
+  if (pre == SDR_PRE_MIX) TRY(scratch(c, S_IN2, sizeof(float) * (size_t)n, (void**)&dc));
+  TRY(scratch(c, S_OUT, sizeof(float) * (size_t)M, (void**)&dy));
+  TRY(scratch(c, S_STATE, sizeof(double) * 2 * (size_t)(Z + 1), (void**)&dz));
+  TRY(h2d(c, dx, x, sizeof(float) * n));
+  if (dc) TRY(h2d(c, dc, mix, sizeof(float) * n));
+  if (zi_inout) TRY(h2d(c, dz, zi_inout, sizeof(double) * Z));
+  TRY(sdr_fir_dev(c, dx, dc, gain, pre, n, n, 0, 1, b, taps, decim, zi_inout ? dz : nullptr, Z,
+                  zi_inout ? dz + Z + 1 : nullptr, dy, M));
+  TRY(d2h(c, y, dy, sizeof(float) * M));
+  if (zi_inout) TRY(d2h(c, zi_inout, dz + Z + 1, sizeof(double) * Z));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SDR_OK;
+}
+
+int sdr_lfilter_decim(sdr_ctx* c, const float* x, int64_t n, const double* b, int taps, int decim,
+                      double* zi_inout, float* y) {
+  return sdr_lfilter(c, x, nullptr, 1.f, SDR_PRE_NONE, n, b, taps, decim, zi_inout, y);
+}
+
+int sdr_resample(sdr_ctx* c, const float* x, int64_t n, const double* b, int taps, int up, int down,
+                 double* zi_inout, float* y) {
+  CHECK_CTX(c);
+  if (n < 0 || up < 1 || down < 1) return fail(SDR_EINVAL, "bad resampler sizes");
+  if (taps < 1 || taps > SDR_MAX_TAPS) return fail(SDR_EINVAL, "taps=%d outside [1, %d]", taps, SDR_MAX_TAPS);
+  if (n > 0 && (x == nullptr || y == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  const int64_t M = ceil_div(n * up, down);
+  float *dx, *dy;
+  double* dz;
+  const int Z = taps - 1;
+  TRY(scratch(c, S_IN, sizeof(float) * (size_t)n, (void**)&dx));
+  TRY(scratch(c, S_OUT, sizeof(float) * (size_t)M, (void**)&dy));
+  TRY(scratch(c, S_STATE, sizeof(double) * 2 * (size_t)(Z + 1), (void**)&dz));
+  TRY(h2d(c, dx, x, sizeof(float) * n));
+  if (zi_inout) TRY(h2d(c, dz, zi_inout, sizeof(double) * Z));
+  TRY(sdr_resample_dev(c, dx, n, b, taps, up, down, zi_inout ? dz : nullptr,
+                       zi_inout ? dz + Z + 1 : nullptr, dy));
+  TRY(d2h(c, y, dy, sizeof(float) * M));
+  if (zi_inout) TRY(d2h(c, zi_inout, dz + Z + 1, sizeof(double) * Z));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SDR_OK;
+}
+
+int sdr_fm_demod(sdr_ctx* c, const float* I, const float* Q, int64_t n, double* prev_phase,
+                 float* out) {
+  CHECK_CTX(c);
+  if (n < 0) return fail(SDR_EINVAL, "negative size");
+  if (n > 0 && (I == nullptr || Q == nullptr || out == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  float *dI, *dO;
+  double* dp;
+  TRY(scratch(c, S_IN, sizeof(float) * 2 * (size_t)n, (void**)&dI));
+  TRY(scratch(c, S_OUT, sizeof(float) * (size_t)n, (void**)&dO));
+  TRY(scratch(c, S_STATE, sizeof(double), (void**)&dp));
+  TRY(h2d(c, dI, I, sizeof(float) * n));
+  TRY(h2d(c, dI + n, Q, sizeof(float) * n));
+  const double ph0 = prev_phase ? *prev_phase : 0.0;
+  TRY(h2d(c, dp, &ph0, sizeof(double)));
+  TRY(sdr_fm_demod_dev(c, dI, dI + n, n, n, 1, dp, dO, n));
+  TRY(d2h(c, out, dO, sizeof(float) * n));
+  double ph1 = ph0;
+  TRY(d2h(c, &ph1, dp, sizeof(double)));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (prev_phase) *prev_phase = ph1;
+  return SDR_OK;
+}
+
+int sdr_pll(sdr_ctx* c, const float* in, int64_t n, double freq, double fs, double nco_scale,
+            double phase_adj, double norm_bw, double* state6, float* nco_i, float* nco_q) {
+  CHECK_CTX(c);
+  if (n < 0) return fail(SDR_EINVAL, "negative size");
+  if (state6 == nullptr || nco_i == nullptr || (n > 0 && in == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  float *dx, *dO;
+  double* ds;
+  TRY(scratch(c, S_IN, sizeof(float) * (size_t)(n + 1), (void**)&dx));
+  TRY(scratch(c, S_OUT, sizeof(float) * 2 * (size_t)(n + 1), (void**)&dO));
+  TRY(scratch(c, S_STATE, sizeof(double) * 6, (void**)&ds));
+  TRY(h2d(c, dx, in, sizeof(float) * n));
+  TRY(h2d(c, ds, state6, sizeof(double) * 6));
+  TRY(sdr_pll_dev(c, dx, n, n, 1, freq, fs, nco_scale, phase_adj, norm_bw, ds, dO,
+                  nco_q ? dO + (n + 1) : nullptr, n + 1));
+  TRY(d2h(c, nco_i, dO, sizeof(float) * (n + 1)));
+  if (nco_q) TRY(d2h(c, nco_q, dO + (n + 1), sizeof(float) * (n + 1)));
+  TRY(d2h(c, state6, ds, sizeof(double) * 6));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SDR_OK;
+}
+
+int sdr_mono_block(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, const double* rf_b,
+                   int rf_taps, int rf_decim, double* zi_i, double* zi_q, double* prev_phase,
+                   const double* audio_b, int audio_taps, int audio_decim, double* audio_zi,
+                   float* demod_out, float* audio_out) {
+  CHECK_CTX(c);
+  if (n < 0) return fail(SDR_EINVAL, "negative size");
+  if (iq_dtype != SDR_IQ_F32 && iq_dtype != SDR_IQ_U8) return fail(SDR_EINVAL, "iq_dtype %d", iq_dtype);
+  if (rf_taps < 1 || rf_taps > SDR_MAX_TAPS || audio_taps < 1 || audio_taps > SDR_MAX_TAPS)
+    return fail(SDR_EINVAL, "taps outside [1, %d]", SDR_MAX_TAPS);
+  if (rf_decim < 1 || audio_decim < 1) return fail(SDR_EINVAL, "decimation < 1");
+  if ((zi_i == nullptr) != (zi_q == nullptr)) return fail(SDR_EINVAL, "zi_i/zi_q must both be set or NULL");
+  if (n > 0 && (iq == nullptr || audio_out == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  const int64_t M = ceil_div(n, rf_decim);
+  const int64_t A = ceil_div(M, audio_decim);
+  const size_t in_bytes = (size_t)n * (iq_dtype == SDR_IQ_U8 ? 2 : 8);
+  void* d_iq;
+  float *d_dm, *d_au;
+  double* d_st;
+  TRY(scratch(c, S_IN, in_bytes, &d_iq));
+  TRY(scratch(c, S_OUT, sizeof(float) * (size_t)(M + 4), (void**)&d_dm));
+  TRY(scratch(c, S_OUT2, sizeof(float) * (size_t)(A + 4), (void**)&d_au));
+  const int Z = rf_taps - 1, ZA = audio_taps - 1;
+  TRY(scratch(c, S_STATE, sizeof(double) * (4 * (size_t)Z + 2 * (size_t)ZA + 2), (void**)&d_st));
+  double *dzi = d_st, *dzq = d_st + Z, *dfi = d_st + 2 * Z, *dfq = d_st + 3 * Z;
+  double *dza = d_st + 4 * Z, *dfa = dza + ZA, *dph = dfa + ZA;
+  TRY(h2d(c, d_iq, iq, in_bytes));
+  if (zi_i) {
+    TRY(h2d(c, dzi, zi_i, sizeof(double) * Z));
+    TRY(h2d(c, dzq, zi_q, sizeof(double) * Z));
+  }
+  if (audio_zi) TRY(h2d(c, dza, audio_zi, sizeof(double) * ZA));
+  const double ph0 = prev_phase ? *prev_phase : 0.0;
+  TRY(h2d(c, dph, &ph0, sizeof(double)));
+  TRY(sdr_rf_frontend_dev(c, d_iq, iq_dtype, n, n, 0, 1, rf_b, rf_taps, rf_decim,
+                          zi_i ? dzi : nullptr, zi_i ? dzq : nullptr, Z, zi_i ? dfi : nullptr,
+                          zi_i ? dfq : nullptr, dph, d_dm, M, nullptr, nullptr));
+  TRY(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, audio_b, audio_taps, audio_decim,
+                  audio_zi ? dza : nullptr, ZA, audio_zi ? dfa : nullptr, d_au, A));
+  TRY(d2h(c, audio_out, d_au, sizeof(float) * A));
+  if (demod_out) TRY(d2h(c, demod_out, d_dm, sizeof(float) * M));
+  if (zi_i) {
+    TRY(d2h(c, zi_i, dfi, sizeof(double) * Z));
+    TRY(d2h(c, zi_q, dfq, sizeof(double) * Z));
+  }
+  if (audio_zi) TRY(d2h(c, audio_zi, dfa, sizeof(double) * ZA));
+  double ph1 = ph0;
+  TRY(d2h(c, &ph1, dph, sizeof(double)));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (prev_phase) *prev_phase = ph1;
+  return SDR_OK;
+}
+
+}  // extern "C"

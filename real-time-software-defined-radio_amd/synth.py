@@ -1,0 +1,50 @@
+"""Seeded synthetic FM-broadcast IQ (the reference ships no captures: data/simple_readme.txt).
+
+Composite baseband: mono L+R, 19 kHz pilot, L-R on a 38 kHz
+subcarrier, and +-1 RDS symbols at 2375 Bd on 57 kHz; frequency-modulated with
+75 kHz deviation at 2.4 MS/s; complex AWGN at 30 dB SNR.  Output is interleaved
+[I0, Q0, I1, Q1, ...] float32 (model/fmMonoBlock.py:39) or uint8
+(model/fmRDSblock.py:58, as rtl_sdr produces).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+FS = 2.4e6
+
+
+def fm_iq(n_complex: int, seed: int = 0, fs: float = FS, snr_db: float = 30.0, chunk: int = 1 << 22,
+          dtype=np.float32) -> np.ndarray:
+    """Interleaved float32 IQ of `n_complex` samples (generated in chunks to bound memory)."""
+    rng = np.random.default_rng(seed)
+    out = np.empty(2 * n_complex, dtype=np.float32)
+    sym_len = fs / 2375.0
+    nsym = int(np.ceil(n_complex / sym_len)) + 2
+    symbols = rng.choice(np.array([-1.0, 1.0]), size=nsym)
+    noise_rng = np.random.default_rng(seed + 1_000_003)
+    amp = 0.5
+    sigma = amp / np.sqrt(2.0) * 10 ** (-snr_db / 20.0)
+    phase0 = 0.0
+    for start in range(0, n_complex, chunk):
+        n = min(chunk, n_complex - start)
+        t = (start + np.arange(n, dtype=np.float64)) / fs
+        left = np.sin(2 * np.pi * 1e3 * t)
+        right = 0.8 * np.sin(2 * np.pi * 2.5e3 * t)
+        rds = symbols[((start + np.arange(n)) / sym_len).astype(np.int64)]
+        mpx = (0.45 * (left + right) / 2 + 0.1 * np.cos(2 * np.pi * 19e3 * t)
+               + 0.45 * (left - right) / 2 * np.cos(2 * np.pi * 38e3 * t)
+               + 0.05 * rds * np.cos(2 * np.pi * 57e3 * t))
+        phi = phase0 + 2 * np.pi * 75e3 * np.cumsum(mpx) / fs
+        phase0 = float(phi[-1])
+        noise = noise_rng.standard_normal((n, 2)) * sigma
+        out[2 * start:2 * (start + n):2] = (amp * np.cos(phi) + noise[:, 0]).astype(np.float32)
+        out[2 * start + 1:2 * (start + n):2] = (amp * np.sin(phi) + noise[:, 1]).astype(np.float32)
+    if np.dtype(dtype) == np.uint8:
+        return to_u8(out)
+    return out
+
+
+def to_u8(iq: np.ndarray) -> np.ndarray:
+    """round(127 * x / max|x| + 128), the rtl_sdr-style byte stream."""
+    peak = float(np.max(np.abs(iq))) or 1.0
+    return np.clip(np.rint(127.0 * iq / peak + 128.0), 0, 255).astype(np.uint8)
