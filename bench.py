@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--audio-taps", type=int, default=151)
     ap.add_argument("--iq", choices=["f32", "u8"], default="f32")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-samples", type=int, default=2_048_000, help="complex samples per CPU stream")
+    ap.add_argument("--cpu-samples", type=int, default=4_096_000, help="complex samples per CPU stream")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall time per CPU leg")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "fe_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per FE launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -95,16 +96,31 @@ def cpu_baseline(args, rf_b, au_b):
     threads = max(1, min(threads, 16, os.cpu_count() or 1))
     import rtsdr
     n = args.cpu_samples
-    iq = np.concatenate([rtsdr.synth.fm_iq(n, seed=100 + s) for s in range(threads)])
+    # one synthetic stream shared read-only by all threads (bounded memory); each thread
+    # writes its own output; repeated until ~args.cpu_seconds of wall time (~16x that of CPU work)
+    iq = rtsdr.synth.fm_iq(n, seed=100)
     A = ((n + 9) // 10 + 4) // 5
     out = np.empty(A * threads)
-    t0 = time.perf_counter()
-    lib.orc_fe_mono_streams(iq, n, n, threads, np.ascontiguousarray(rf_b), len(rf_b),
-                            np.ascontiguousarray(au_b), len(au_b), out, A, threads)
-    dt = time.perf_counter() - t0
-    res = {"value": round(n * threads / dt / 1e6, 3), "unit": "MS/s", "cores": threads, "kind": "port",
-           "sample": f"{threads} streams x {n} complex samples, FE({len(rf_b)} taps)+mono({len(au_b)} taps), "
-                     f"f64 C restatement of the Python model, -O3 OpenMP, {dt:.2f} s wall"}
+
+    def run_port():
+        lib.orc_fe_mono_streams(iq, n, 0, threads, np.ascontiguousarray(rf_b), len(rf_b),
+                                np.ascontiguousarray(au_b), len(au_b), out, A, threads)
+
+    def timed(fn):
+        t0 = time.perf_counter()
+        fn()
+        t1 = time.perf_counter() - t0
+        reps = max(1, int(np.ceil(args.cpu_seconds / max(t1, 1e-6))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return reps, time.perf_counter() - t0
+
+    reps, dt = timed(run_port)
+    res = {"value": round(n * threads * reps / dt / 1e6, 3), "unit": "MS/s", "cores": threads, "kind": "port",
+           "sample": f"{threads} threads x {reps} x {n} complex samples (one stream each), "
+                     f"FE({len(rf_b)} taps)+mono({len(au_b)} taps), f64 C restatement of the Python model "
+                     f"(oracle/fm_oracle.c, -O3 -march=x86-64-v3, OpenMP), {dt:.2f} s wall"}
     ref = os.path.join(ROOT, "oracle", "_ref", "libref_fe.so")
     if os.path.exists(ref):
         rl = ctypes.CDLL(ref)
@@ -114,14 +130,17 @@ def cpu_baseline(args, rf_b, au_b):
         blk = 153_600
         nn = (n // blk) * blk
         dm = np.empty((nn // 10) * threads, dtype=np.float32)
-        t0 = time.perf_counter()
-        rl.ref_fe_streams(iq, nn, n, threads, blk, np.ascontiguousarray(rf_b, dtype=np.float32), len(rf_b), 10,
-                          dm, nn // 10, threads)
-        dt = time.perf_counter() - t0
-        res["reference_cpp_fe"] = {"value": round(nn * threads / dt / 1e6, 3), "unit": "MS/s",
+        h32 = np.ascontiguousarray(rf_b, dtype=np.float32)
+
+        def run_ref():
+            rl.ref_fe_streams(iq, nn, 0, threads, blk, h32, len(rf_b), 10, dm, nn // 10, threads)
+
+        reps, dt = timed(run_ref)
+        res["reference_cpp_fe"] = {"value": round(nn * threads * reps / dt / 1e6, 3), "unit": "MS/s",
                                    "cores": threads, "kind": "reference",
-                                   "sample": f"{threads} streams x {nn} complex, src/ convolveWithDecimIQ + "
-                                             f"fmDemodArctan (FE only, f32, -O3), {dt:.2f} s wall"}
+                                   "sample": f"{threads} threads x {reps} x {nn} complex, src/filter.cpp "
+                                             f"convolveWithDecimIQ + src/rf_module.cpp fmDemodArctan (FE only, "
+                                             f"f32, reference -O3 flags), {dt:.2f} s wall"}
     return res
 
 

@@ -27,6 +27,8 @@
 //      reference's accumulated (unwrapped) phase state: prev_out = phi_last + 2*pi*W.
 #include "sdr_common.h"
 
+#include <algorithm>
+
 namespace {
 
 struct FeParams {
@@ -103,7 +105,111 @@ __device__ inline double unwrap_step_f64(double dd, int* w) {
   return ddmod;
 }
 
-template <int T, int D, int R, int NT, bool U8>
+// Steps 3-5 shared by the FE kernels: zi add, atan2, predecessor phase (lane 0 gets the
+// wave-reduced sums (si, sq) of output mw-1; lane l>0 shuffles from lane l-1), np.unwrap
+// wrap, stores, wrap count and last phase.  Lane l of the wave owns outputs
+// mw + R*l .. mw + R*l + R-1.
+template <int T, int D, int R>
+// If have_prev, phi_prev is the phase of output mw-1 (carried by a persistent wave from
+// its previous tile) and (si, sq) are ignored.  Returns the phase of the wave's last
+// output (lane 63's), broadcast to all lanes.  *one_store (if given) tells whether the
+// tile issued exactly one vector-memory instruction (the full-width demod store); every
+// other case (partial tile, zi/prev-phase loads, i_ds/q_ds, last_phi, wraps) ends with
+// s_waitcnt vmcnt(0), so a streaming caller can count its outstanding loads exactly.
+__device__ __forceinline__ float fe_epilogue(const FeParams& p, int s, int64_t M, int64_t mw, int lane,
+                                             float (&ai)[R], float (&aq)[R], float si, float sq,
+                                             bool have_prev = false, float phi_prev = 0.f,
+                                             bool* one_store = nullptr) {
+  const int64_t mf = mw + (int64_t)lane * R;       // first output of this lane
+  const int64_t zoff = (int64_t)s * p.zi_stride;
+  float phi[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t nn = D * (mf + r);
+    if (p.zi_i != nullptr && nn < T - 1) {
+      ai[r] += (float)p.zi_i[zoff + nn];
+      aq[r] += (float)p.zi_q[zoff + nn];
+    }
+    phi[r] = fast_atan2f(aq[r], ai[r]);
+  }
+  float phi_wprev = phi_prev;
+  if (mw > 0 && !have_prev) {
+    const int64_t nn = D * (mw - 1);
+    if (p.zi_i != nullptr && nn < T - 1) {
+      si += (float)p.zi_i[zoff + nn];
+      sq += (float)p.zi_q[zoff + nn];
+    }
+    phi_wprev = fast_atan2f(sq, si);
+  }
+  // lane l-1's last phase: DPP wave_shr:1 (a VALU move, no LDS round trip)
+  const float from_left = __int_as_float(__builtin_amdgcn_update_dpp(
+      0, __float_as_int(phi[R - 1]), 0x138 /*wave_shr:1*/, 0xf, 0xf, false));
+  float prev = (lane == 0) ? phi_wprev : from_left;
+
+  float d[R];
+  int wsum = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t m = mf + r;
+    int wk = 0;
+    if (m == 0) {
+      const double ps = p.prev_phase ? p.prev_phase[s] : 0.0;
+      d[r] = (float)unwrap_step_f64((double)phi[r] - ps, &wk);
+    } else {
+      float dd = phi[r] - prev;
+      if (dd > kPiF) { dd -= k2PiF; wk = -1; }
+      else if (dd < -kPiF) { dd += k2PiF; wk = 1; }
+      d[r] = dd;
+    }
+    if (m < M) wsum += wk;
+    prev = phi[r];
+  }
+
+  // one full-width store per lane (a wave writes 64*R contiguous floats: whole cache
+  // lines; per-float stores at an R*4-B lane stride cost partial-line writes)
+  float* out = p.demod + (int64_t)s * p.out_stride;
+  if (R == 4 && p.vec_out && mf + R <= M) {
+    *reinterpret_cast<float4*>(out + mf) = make_float4(d[0], d[1 % R], d[2 % R], d[3 % R]);
+  } else if (R == 2 && p.vec_out && mf + R <= M) {
+    *reinterpret_cast<float2*>(out + mf) = make_float2(d[0], d[1 % R]);
+  } else if (R == 3 && mf + R <= M) {
+    typedef float f3v __attribute__((ext_vector_type(3)));
+    *reinterpret_cast<f3v*>(out + mf) = f3v{d[0], d[1 % R], d[2 % R]};
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (mf + r < M) out[mf + r] = d[r];
+  }
+  if (p.i_ds != nullptr) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (mf + r < M) {
+        p.i_ds[(int64_t)s * p.out_stride + mf + r] = ai[r];
+        p.q_ds[(int64_t)s * p.out_stride + mf + r] = aq[r];
+      }
+  }
+  if (p.last_phi != nullptr) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (mf + r == M - 1) p.last_phi[s] = phi[r];
+  }
+  if (p.wraps != nullptr) {
+    wsum = wave_sum_i(wsum);
+    if (lane == 0 && wsum != 0) atomicAdd(p.wraps + s, wsum);
+  }
+  if (one_store != nullptr) {
+    const int64_t mend = mw + 64 * R;   // wave-uniform
+    const bool simple = mend <= M - 1 && D * (mw - 1) >= T - 1 && p.i_ds == nullptr && p.wraps == nullptr &&
+                        (R == 3 || p.vec_out);
+    if (!simple) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *one_store = simple;
+  }
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[R - 1]), 63));
+}
+
+// MODE (tuning builds only; the product uses 0): 1 = loads + LDS staging, no FIR;
+// 2 = LDS staging of synthetic values + FIR, no global loads.
+template <int T, int D, int R, int NT, bool U8, int MODE = 0>
 __global__ __launch_bounds__(NT) void fe_kernel(FeParams p, TapsF32 taps) {
   using L8 = IqLoad<U8>;
   constexpr int G = L8::G;
@@ -134,7 +240,9 @@ __global__ __launch_bounds__(NT) void fe_kernel(FeParams p, TapsF32 taps) {
 
   // ---- 1. stage the input span into padded LDS -------------------------------
   auto slot = [](int e) { return e + (e + DR - C0) / DR; };
-  if (n_lo >= -p.hist && n_lo + L <= p.n) {
+  if (MODE == 2) {
+    for (int e = t; e < L; e += NT) lds[slot(e)] = make_float2((float)e * 1e-4f, (float)t);
+  } else if (n_lo >= -p.hist && n_lo + L <= p.n) {
     typename L8::V v[NLOAD];
 #pragma unroll
     for (int j = 0; j < NLOAD; ++j) {
@@ -165,38 +273,26 @@ __global__ __launch_bounds__(NT) void fe_kernel(FeParams p, TapsF32 taps) {
 #pragma unroll
   for (int r = 0; r < R; ++r) { ai[r] = 0.f; aq[r] = 0.f; }
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
+  for (int i = 0; i < (MODE == 1 ? R : NI); ++i) {
     const float2 x = win[i + i / DR];
+    if (MODE == 1) { ai[i] = x.x; aq[i] = x.y; continue; }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int k = D * r + T - 1 - i;             // tap index (compile time)
       if (k >= 0 && k < T) {
-        ai[r] = fmaf(taps.h[k], x.x, ai[r]);
-        aq[r] = fmaf(taps.h[k], x.y, aq[r]);
+        const float h = taps.h[k];
+        ai[r] = fmaf(h, x.x, ai[r]);
+        aq[r] = fmaf(h, x.y, aq[r]);
       }
     }
   }
 
-  const int64_t mf = m0 + (int64_t)t * R;          // first output of this thread
-  const int64_t zoff = (int64_t)s * p.zi_stride;
-  float phi[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int64_t nn = D * (mf + r);
-    if (p.zi_i != nullptr && nn < T - 1) {
-      ai[r] += (float)p.zi_i[zoff + nn];
-      aq[r] += (float)p.zi_q[zoff + nn];
-    }
-    phi[r] = atan2f(aq[r], ai[r]);
-  }
-
-  // ---- 3. predecessor phase for lane 0 of each wave --------------------------
+  // ---- 3. predecessor sums for lane 0 of each wave (output m_w - 1) -----------
   const int lane = t & 63;
   const int w = t >> 6;
   const int64_t mw = m0 + (int64_t)w * 64 * R;
-  float phi_wprev = 0.f;
+  float si = 0.f, sq = 0.f;
   if (mw > 0) {
-    float si = 0.f, sq = 0.f;
     for (int k = lane; k < T; k += 64) {
       const int e = D * w * 64 * R + (T - 1) + DELTA - k;
       const float2 x = lds[slot(e)];
@@ -206,63 +302,181 @@ __global__ __launch_bounds__(NT) void fe_kernel(FeParams p, TapsF32 taps) {
     }
     si = wave_sum(si);
     sq = wave_sum(sq);
-    const int64_t nn = D * (mw - 1);
-    if (p.zi_i != nullptr && nn < T - 1) {
-      si += (float)p.zi_i[zoff + nn];
-      sq += (float)p.zi_q[zoff + nn];
-    }
-    phi_wprev = atan2f(sq, si);
   }
-  const float from_left = __shfl_up(phi[R - 1], 1, 64);
-  float prev = (lane == 0) ? phi_wprev : from_left;
+  fe_epilogue<T, D, R>(p, s, M, mw, lane, ai, aq, si, sq);
+}
 
-  // ---- 4. discriminator with np.unwrap semantics ------------------------------
-  float d[R];
-  int wsum = 0;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int64_t m = mf + r;
-    int wk = 0;
-    if (m == 0) {
-      const double ps = p.prev_phase ? p.prev_phase[s] : 0.0;
-      d[r] = (float)unwrap_step_f64((double)phi[r] - ps, &wk);
-    } else {
-      float dd = phi[r] - prev;
-      if (dd > kPiF) { dd -= k2PiF; wk = -1; }
-      else if (dd < -kPiF) { dd += k2PiF; wk = 1; }
-      d[r] = dd;
-    }
-    if (m < M) wsum += wk;
-    prev = phi[r];
-  }
+// Persistent streaming f32 front end: the product kernel for f32 IQ.
+//
+// One wave per workgroup and WPC resident waves per CU; each wave walks a contiguous
+// run of tiles (TO = 64*R decimated outputs each).  Tile images go HBM -> LDS through
+// an NB-deep ring filled by 16-B LDS-DMA loads (global_load_lds_dwordx4, 1 KB per
+// wave-instruction, no staging registers): tile t+1 is in flight while tile t is
+// filtered (tools/mem_probe.hip: this pattern streams at 6.2-6.4 TB/s on its own).
+// FIR: v_pk_fma_f32 on (I, Q) pairs; the taps stay in VGPR pairs {h[2j], h[2j+1]} for
+// the whole launch and each FMA broadcasts one half through op_sel, so an output costs
+// T packed FMAs and no moves.  Lane l filters samples [D R l + D + DELTA, + D(R-1)+T)
+// of the tile image; the per-lane stride D*R*8 B (240 B at R=3, 400 B at R=5) puts the
+// 16 lanes of each ds_read_b128 group on 16 distinct 16-B bank slots (conflict-free).
+// The predecessor phase of a tile is carried from the wave's previous tile (only the
+// first tile of a wave evaluates output m0-1 cooperatively).
+// The ring is dynamic LDS so the compiler's occupancy target comes from
+// amdgpu_waves_per_eu(2): a 256-register budget that keeps the taps (T/2 VGPR pairs)
+// plus a bounded window of in-flight LDS reads, instead of hoisting every read.
+template <int T, int D, int R, int NB, int MODE = 0>
+__global__ __launch_bounds__(64)
+void fe_stream_kernel(FeParams p, TapsF32 taps, int64_t total_tiles) {
+  constexpr int TO = 64 * R;
+  constexpr int G = 2;
+  constexpr int DELTA = (G - ((D + T - 1) % G)) % G;
+  constexpr int LRAW = D * TO + T + DELTA;
+  constexpr int NG = (LRAW + 127) / 128;             // LDS-DMA wave-instructions per tile
+  constexpr int L = NG * 128;
+  constexpr int LB = L + 2;                          // buffer stride (f2v); +2: last pair over-read
+  constexpr int NI = D * (R - 1) + T;
+  constexpr int TP = (T + 1) / 2;
+  static_assert(((D * R) % 2) == 0 && ((D + DELTA) % 2) == 0, "lane windows must start 16-B aligned");
+  static_assert(NG * (NB - 1) <= 63, "vmcnt range");
 
-  // ---- 5. stores ---------------------------------------------------------------
-  if (s < p.nstreams) {
-    float* out = p.demod + (int64_t)s * p.out_stride;
-    if (R == 4 && p.vec_out && mf + R <= M) {
-      *reinterpret_cast<float4*>(out + mf) = make_float4(d[0], d[1 % R], d[2 % R], d[3 % R]);
+  __shared__ __attribute__((aligned(16))) f2v lds[NB * LB];
+
+  const int lane = threadIdx.x;
+  const int64_t nw = gridDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * total_tiles / nw;
+  const int64_t t1 = ((int64_t)blockIdx.x + 1) * total_tiles / nw;
+  if (t0 >= t1) return;
+  const int64_t M = (p.n + D - 1) / D;
+
+  f2v tp[TP];
+#pragma unroll
+  for (int j = 0; j < TP; ++j) tp[j] = f2v{taps.h[2 * j], (2 * j + 1 < T) ? taps.h[2 * j + 1] : 0.f};
+#pragma unroll
+  for (int j = 0; j < TP; ++j) asm volatile("" : "+v"(tp[j]));   // keep taps in VGPRs
+
+  // (stream, first output) of tile t0, advanced incrementally
+  int s = (int)(t0 / p.tiles_per_stream);
+  int64_t m0 = (t0 - (int64_t)s * p.tiles_per_stream) * TO;
+  auto interior = [&](int ss, int64_t mm) {
+    const int64_t n_lo = D * (mm - 1) - (T - 1) - DELTA;
+    return MODE != 2 && n_lo >= -p.hist && n_lo + L <= p.n;
+  };
+  auto issue = [&](int ss, int64_t mm, int b) {
+    const int64_t n_lo = D * (mm - 1) - (T - 1) - DELTA;
+    const float* g = reinterpret_cast<const float*>(p.iq) + 2 * ((int64_t)ss * p.stride + n_lo) + 4 * lane;
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+      __builtin_amdgcn_global_load_lds(g + 256 * j,
+                                       (__attribute__((address_space(3))) void*)(lds + b * LB + 128 * j),
+                                       16, 0, 2 /* nt: streamed once, do not keep in L2 */);
+  };
+  auto advance = [&](int& ss, int64_t& mm) {
+    mm += TO;
+    if (mm >= (int64_t)p.tiles_per_stream * TO) { mm = 0; ++ss; }
+  };
+
+  bool issued = interior(s, m0);
+  if (issued) issue(s, m0, 0);
+  float carry = 0.f;
+  bool have = false;
+  bool store_pending = false;
+  int b = 0;
+  for (int64_t t = t0; t < t1; ++t) {
+    int s1 = s;
+    int64_t m1 = m0;
+    advance(s1, m1);
+    const int bn = (b + 1 == NB) ? 0 : b + 1;
+    const bool next = (t + 1 < t1) && interior(s1, m1);
+    if (next) issue(s1, m1, bn);
+    f2v* buf = lds + b * LB;
+    if (issued) {
+      // outstanding, oldest first: this tile's NG loads, the previous tile's demod store
+      // (when the epilogue reported exactly one), the next tile's NG loads
+      if (next && store_pending) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NG + 1) : "memory");
+      else if (next) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NG) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (mf + r < M) out[mf + r] = d[r];
+      const int64_t n_lo = D * (m0 - 1) - (T - 1) - DELTA;
+      const float* base = reinterpret_cast<const float*>(p.iq) + 2 * ((int64_t)s * p.stride);
+      for (int e = lane; e < L; e += 64) {
+        const int64_t nn = n_lo + e;
+        f2v x = f2v{0.f, 0.f};
+        if (MODE == 2) x = f2v{(float)e * 1e-4f, (float)lane};
+        else if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
+        buf[e] = x;
+      }
     }
-    if (p.i_ds != nullptr) {
+
+    const f2v* win = buf + (D * R * lane + D + DELTA);
+    const float4* win4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(win, 16));
+    // two accumulator pairs per output (even / odd taps): 2R independent FMA chains per wave
+    f2v acc[R], acc2[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (mf + r < M) {
-          p.i_ds[(int64_t)s * p.out_stride + mf + r] = ai[r];
-          p.q_ds[(int64_t)s * p.out_stride + mf + r] = aq[r];
+    for (int r = 0; r < R; ++r) { acc[r] = f2v{0.f, 0.f}; acc2[r] = f2v{0.f, 0.f}; }
+    if (MODE == 1 || MODE == 3) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = win[r];
+    } else {
+      // one ds_read_b128 per sample pair (the lane window starts 16-B aligned), issued by
+      // hand PF pairs ahead of use with counted lgkmcnt waits: hipcc would split the 16-B
+      // read into ds_read2_b64 (4-8-way bank conflicts at this lane stride) and read only
+      // one pair ahead (the LDS latency then stalls the wave).
+      constexpr int NP = (NI + 1) / 2;
+      constexpr int PF = 8;
+      f4v qb[NP];
+      static_for<0, (PF < NP ? PF : NP)>([&](auto I) { qb[I] = lds_read_b128<16 * I>(win4); });
+      static_for<0, NP>([&](auto I) {
+        constexpr int ip = I;
+        if constexpr (ip + PF < NP) {
+          qb[ip + PF] = lds_read_b128<16 * (ip + PF)>(win4);
+          lds_wait<PF>(qb[ip]);
+        } else {
+          lds_wait<NP - 1 - ip>(qb[ip]);
         }
-    }
-    if (p.last_phi != nullptr) {
+        const f4v q = qb[ip];
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (mf + r == M - 1) p.last_phi[s] = phi[r];
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * ip + h;
+          if (i >= NI) break;
+          const f2v x = h ? f2v{q.z, q.w} : f2v{q.x, q.y};
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int k = D * r + T - 1 - i;
+            if (k >= 0 && k < T) {
+              if (k & 1) pk_fma_bcast<true>(acc2[r], tp[k >> 1], x);
+              else pk_fma_bcast<false>(acc[r], tp[k >> 1], x);
+            }
+          }
+        }
+      });
     }
-    if (p.wraps != nullptr) {
-      wsum = wave_sum_i(wsum);
-      if (lane == 0 && wsum != 0) atomicAdd(p.wraps + s, wsum);
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] += acc2[r];
+    float ai[R], aq[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) { ai[r] = acc[r].x; aq[r] = acc[r].y; }
+
+    float si = 0.f, sq = 0.f;
+    if (MODE != 3 && m0 > 0 && !have) {
+      for (int k = lane; k < T; k += 64) {
+        const f2v x = buf[(T - 1) + DELTA - k];
+        const float h = p.taps_dev[k];
+        si = fmaf(h, x.x, si);
+        sq = fmaf(h, x.y, sq);
+      }
+      si = wave_sum(si);
+      sq = wave_sum(sq);
     }
+    if (MODE == 3) {   // tuning: no epilogue, raw store
+      *reinterpret_cast<float2*>(p.demod + (int64_t)s * p.out_stride + m0 + R * lane) = make_float2(ai[0], aq[0]);
+      store_pending = true;
+    } else {
+      carry = fe_epilogue<T, D, R>(p, s, M, m0, lane, ai, aq, si, sq, have, carry, &store_pending);
+    }
+    have = (s1 == s);          // the next tile continues this stream
+    s = s1;
+    m0 = m1;
+    issued = next;
+    b = bn;
   }
 }
 
@@ -310,9 +524,33 @@ struct FeLaunch {
   float* demod; int64_t out_stride; float* i_ds; float* q_ds; float* last_phi; int* wraps;
 };
 
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      n = prop.multiProcessorCount;
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+// Resident workgroups per CU for a kernel (the persistent grid must be fully resident
+// for its tiles to be spread evenly; any excess would run as a second, serial round).
+template <typename K>
+static int resident_per_cu(K kernel, int threads) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, threads, 0) != hipSuccess || n <= 0) n = 1;
+  return n;
+}
+
 template <int T, int D, bool U8>
 static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
-  constexpr int NT = 128, R = 4, TO = NT * R;
+  constexpr int NT = U8 ? 128 : 64;
+  constexpr int R = U8 ? 4 : 2;
+  constexpr int NB = 2;
+  constexpr int TO = NT * R;
   FeParams p;
   p.iq = a.iq; p.n = a.n; p.stride = a.stride; p.hist = a.hist; p.nstreams = a.nstreams;
   const int64_t M = (a.n + D - 1) / D;
@@ -321,11 +559,16 @@ static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
   p.prev_phase = a.prev_phase; p.demod = a.demod; p.out_stride = a.out_stride;
   p.i_ds = a.i_ds; p.q_ds = a.q_ds; p.last_phi = a.last_phi; p.wraps = a.wraps;
   p.vec_out = ((a.out_stride % 4) == 0 && ((uintptr_t)a.demod % 16) == 0) ? 1 : 0;
-  const int64_t blocks = (int64_t)p.tiles_per_stream * a.nstreams;
-  if (blocks <= 0) return hipSuccess;
-  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((fe_kernel<T, D, R, NT, U8>), dim3((unsigned)blocks), dim3(NT), 0, st,
-                     p, *a.taps);
+  const int64_t tiles = (int64_t)p.tiles_per_stream * a.nstreams;
+  if (tiles <= 0) return hipSuccess;
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  if constexpr (U8) {
+    hipLaunchKernelGGL((fe_kernel<T, D, R, NT, true>), dim3((unsigned)tiles), dim3(NT), 0, st, p, *a.taps);
+  } else {
+    static const int wpc = resident_per_cu(fe_stream_kernel<T, D, R, NB>, 64);
+    const int64_t grid = std::min<int64_t>(tiles, (int64_t)cu_count() * wpc);
+    hipLaunchKernelGGL((fe_stream_kernel<T, D, R, NB>), dim3((unsigned)grid), dim3(64), 0, st, p, *a.taps, tiles);
+  }
   return hipGetLastError();
 }
 

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define SDR_MAX_TAPS 256
 
 // Taps passed by value through the kernarg segment: with compile-time tap indices
@@ -19,6 +21,76 @@
 struct TapsF32 {
   float h[SDR_MAX_TAPS];
 };
+
+// Taps duplicated into (h, h) pairs: a v_pk_fma_f32 then takes the tap pair straight
+// from an SGPR pair and updates the (I, Q) accumulator pair in one instruction.
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+struct TapsF2 {
+  f2v h[SDR_MAX_TAPS];
+};
+
+// acc += {h, h} * x with h = the low (HI=false) or high (HI=true) half of the tap pair:
+// one v_pk_fma_f32 broadcasting a half through op_sel, so tap pairs are never duplicated
+// into extra registers.  (No hazards: VALU -> VALU.)
+template <bool HI>
+__device__ __forceinline__ void pk_fma_bcast(f2v& acc, const f2v& tap2, const f2v& x) {
+  if (HI)
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(tap2), "v"(x));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(tap2), "v"(x));
+}
+
+// ds_read_b128 issued by hand: hipcc neither splits it (into ds_read2_b64, whose 32-bank
+// mapping is conflict-prone for strided lane windows) nor counts it, so every use must be
+// preceded by lds_wait<N> naming the destination (N = LDS reads issued after it).
+template <int OFF>
+__device__ __forceinline__ f4v lds_read_b128(const void* lds_base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16-bit");
+  f4v v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)lds_base;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+  return v;
+}
+// compile-time loop: f(std::integral_constant<int, I>{}) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void lds_wait(f4v& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N));
+}
+
+// atan2 for the discriminator: |err| <= ~2.5e-7 rad (2 ulp polynomial on [0, 1] after the
+// octant reduction), ~20 VALU instead of ocml's ~40 with its inf/nan handling; exact
+// zeros go to atan2f so the IEEE signed-zero results (e.g. atan2(+0, -0) = pi) hold.
+__device__ __forceinline__ float fast_atan2f(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mn = fminf(ax, ay), mx = fmaxf(ax, ay);
+  if (!(mx > 0.f) || !(mx < INFINITY)) return atan2f(y, x);   // zeros, inf, nan
+  const float rc = __builtin_amdgcn_rcpf(mx);
+  float a = mn * rc;
+  a = fmaf(fmaf(-mx, a, mn), rc, a);                  // one Newton step: ~0.5 ulp quotient
+  const float s = a * a;
+  float r = 0.002849547192454338f;
+  r = fmaf(r, s, -0.01606736145913601f);
+  r = fmaf(r, s, 0.04268963634967804f);
+  r = fmaf(r, s, -0.0750415101647377f);
+  r = fmaf(r, s, 0.1064087525010109f);
+  r = fmaf(r, s, -0.1420363187789917f);
+  r = fmaf(r, s, 0.19992618262767792f);
+  r = fmaf(r, s, -0.3333307206630707f);
+  r = fmaf(r, s, 1.0f);
+  r *= a;
+  if (ay > ax) r = 1.57079632679489662f - r;
+  if (x < 0.f) r = 3.14159265358979324f - r;
+  return copysignf(r, y);
+}
 
 // Wave-wide sum over 64 lanes (CDNA wave64: six xor steps).
 __device__ __forceinline__ float wave_sum(float v) {

@@ -216,7 +216,8 @@ def test_u8_input_matches_float_path(sdr, gpu_ctx, oracle):
     rf_b, _ = sdr.design.mono_coeffs(151, 151)
     d8 = sdr.rf_frontend_block(u8, rf_b)[0]
     df = sdr.rf_frontend_block(f, rf_b)[0]
-    assert np.array_equal(d8, df)
+    # same inputs; the u8 and f32 kernels differ only in f32 summation order
+    assert maxabs(d8, df) < 5e-6 and rms(d8, df) < 5e-7
 
 
 # ---------------------------------------------------------------------------- full size
