@@ -5,8 +5,10 @@ One step = one pass of RF front end (101-tap IQ LPF, decimate by 10, atan2 demod
 configs[1]) + mono (151-tap audio LPF, decimate by 5; configs[2]) over a batch of
 `--blocks` x 1 024 000-complex-sample blocks of one synthetic 2.4 MS/s stream, input
 resident in HBM (block boundaries are carried-state continuations, so the batch is
-one continuous stream; SURVEY §5 "long-context").  Kernels: libsdr.so's fused FE
-kernel and tiled FIR kernel, launched through the C-ABI (no torch in the data path).
+one continuous stream; SURVEY §5 "long-context").  Kernel: libsdr.so's fused
+FE + mono kernel (sdr_fe_mono_dev: the demodulated signal never leaves the CU);
+`--path split` runs the FE kernel + FIR kernel pair instead.  Launched through the
+C-ABI (no torch in the data path).
 
 Multi-GPU (`torchrun --nproc-per-node N bench.py --gpus N`): one process per GPU,
 each rank processes its own independent stream (seed = rank): weak scaling, no
@@ -14,7 +16,7 @@ data-path collective.  torch.distributed (gloo, CPU) only provides the barrier a
 the max-over-ranks of the timed region.
 
 Prints ONE JSON line (rank 0).  `value` = complex IQ samples processed by all ranks
-per second (MS/s); `roofline` is for the FE kernel (HIP events on the libsdr stream);
+per second (MS/s); `roofline` is for the step's dominant kernel (HIP events on the libsdr stream);
 `cpu_baseline` = the C restatement of the Python model (oracle/fm_oracle.c) on the
 host cores (rank 0, N=1).
 """
@@ -46,6 +48,8 @@ def parse():
     ap.add_argument("--taps", type=int, default=101)
     ap.add_argument("--audio-taps", type=int, default=151)
     ap.add_argument("--iq", choices=["f32", "u8"], default="f32")
+    ap.add_argument("--path", choices=["fused", "split"], default="split",
+                    help="fused: one fe_mono_kernel (demod stays on chip); split: FE kernel + FIR kernel")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-samples", type=int, default=4_096_000, help="complex samples per CPU stream")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall time per CPU leg")
@@ -144,11 +148,11 @@ def cpu_baseline(args, rf_b, au_b):
     return res
 
 
-def load_traffic(path, taps, blocks):
+def load_traffic(path, taps, blocks, kpath):
     try:
         with open(path) as f:
             t = json.load(f)
-        if t.get("taps") == taps and t.get("n_complex") == blocks * BLOCK:
+        if t.get("taps") == taps and t.get("n_complex") == blocks * BLOCK and t.get("path", "split") == kpath:
             return t.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -178,6 +182,10 @@ def main():
     rfp, aup = _lib.f64p(rf_b), _lib.f64p(au_b)
     T, TA = len(rf_b), len(au_b)
 
+    def fused():
+        _lib.check(lib.sdr_fe_mono_dev(h, d_iq.ptr, dtype_code, n, n, 1, rfp, T, 10, aup, TA, 5, d_au.ptr, A),
+                   "fe_mono")
+
     def fe():
         _lib.check(lib.sdr_rf_frontend_dev(h, d_iq.ptr, dtype_code, n, n, 0, 1, rfp, T, 10, None, None, 0, None,
                                            None, None, d_dm.ptr, M, None, None), "fe")
@@ -186,32 +194,41 @@ def main():
         _lib.check(lib.sdr_fir_dev(h, d_dm.ptr, None, 1.0, 0, M, M, 0, 1, aup, TA, 5, None, 0, None, d_au.ptr, A),
                    "mono")
 
+    # the fused kernel covers f32 IQ; u8 IQ runs the FE + FIR pair inside sdr_fe_mono_dev
+    stages = [fused] if args.path == "fused" else [fe, mono]
     tm = _lib.Timer(ctx)
-    ev = [(tm.event(), tm.event(), tm.event()) for _ in range(args.steps)]
+    ev = [[tm.event() for _ in range(len(stages) + 1)] for _ in range(args.steps)]
     for _ in range(args.warmup):
-        fe()
-        mono()
+        for f in stages:
+            f()
     ctx.synchronize()
     barrier(ws)
     ctx.synchronize()
     t0 = time.perf_counter()
-    for e0, e1, e2 in ev:
-        tm.record(e0)
-        fe()
-        tm.record(e1)
-        mono()
-        tm.record(e2)
+    for e in ev:
+        tm.record(e[0])
+        for k, f in enumerate(stages):
+            f()
+            tm.record(e[k + 1])
     ctx.synchronize()
     barrier(ws)
     elapsed = max_over_ranks(ws, time.perf_counter() - t0)
-    fe_ms = [tm.elapsed_ms(a, b) for a, b, _ in ev]
-    mono_ms = [tm.elapsed_ms(b, c) for _, b, c in ev]
-    fe_avg = float(np.mean(fe_ms))
+    stage_ms = [float(np.mean([tm.elapsed_ms(e[k], e[k + 1]) for e in ev])) for k in range(len(stages))]
+    k_avg = stage_ms[0]                              # the dominant (first) kernel of the step
     bpc = 2 if args.iq == "u8" else 8
-    fe_bytes = n * bpc + M * 4                      # compulsory: IQ in + demod out
-    mono_bytes = M * 4 + A * 4
-    achieved = fe_bytes / (fe_avg * 1e-3) / 1e9
-    traffic = load_traffic(args.traffic, args.taps, args.blocks) if args.iq == "f32" else None
+    if args.path == "fused":
+        # compulsory HBM bytes of the fused kernel: IQ in + audio out
+        k_bytes = n * bpc + A * 4
+        kname = f"fe_mono_kernel<{args.taps},10,{args.audio_taps},5> (sdr_fe_mono_dev)"
+        kernels = {"fe_mono": round(k_avg, 5)}
+    else:
+        k_bytes = n * bpc + M * 4                    # IQ in + demod out
+        kname = f"fe_stream_kernel<{args.taps},10> (sdr_rf_frontend_dev)"
+        mono_bytes = M * 4 + A * 4
+        kernels = {"fe": round(k_avg, 5), "mono": round(stage_ms[1], 5),
+                   "mono_gbs": round(mono_bytes / (stage_ms[1] * 1e-3) / 1e9, 1)}
+    achieved = k_bytes / (k_avg * 1e-3) / 1e9
+    traffic = load_traffic(args.traffic, args.taps, args.blocks, args.path) if args.iq == "f32" else None
 
     result = None
     if rank == 0:
@@ -232,14 +249,13 @@ def main():
             "config": {"workload": f"RF front end ({args.taps}-tap LPF, decim 10, atan2 demod) + mono "
                                    f"({args.audio_taps}-tap LPF, decim 5): configs[1]+[2], one stream per GPU",
                        "block_complex": BLOCK, "blocks_per_step": args.blocks, "complex_per_step": n,
-                       "iq": args.iq, "parallelism": f"independent streams x{ws}"},
+                       "iq": args.iq, "path": args.path, "parallelism": f"independent streams x{ws}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": f"fe_kernel<{args.taps},10> (sdr_rf_frontend_dev)",
-                         "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": round(fe_avg, 5)},
-            "kernels_ms": {"fe": round(fe_avg, 5), "mono": round(float(np.mean(mono_ms)), 5),
-                           "mono_gbs": round(mono_bytes / (np.mean(mono_ms) * 1e-3) / 1e9, 1)},
+                         "kernel": kname, "algorithmic_bytes_per_launch": k_bytes,
+                         "avg_launch_ms": round(k_avg, 5)},
+            "kernels_ms": kernels,
         }
     if ws == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, rf_b, au_b)

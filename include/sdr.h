@@ -143,6 +143,18 @@ int sdr_rf_frontend_dev(sdr_ctx* ctx, const void* iq, int iq_dtype, int64_t n, i
                         double* zf_q, double* prev_phase, float* demod, int64_t out_stride,
                         float* i_ds, float* q_ds);
 
+/* Fused continuous-stream mono receiver: per stream,
+ *   audio = lfilter(audio_b, 1, fmDemodArctan(lfilter(rf_b, 1, I)[::rf_decim],
+ *                                             lfilter(rf_b, 1, Q)[::rf_decim]))[::audio_decim]
+ * with zero initial filter/demod state -- model/fmMonoBasic.py:70-111 (whole-signal mono
+ * path; per block: model/fmMonoBlock.py:86-105, src/fm_radio.cpp:66-84).  The demodulated
+ * stream stays on chip (f32 IQ, rf_taps 101/151 at decim 10, audio 151 taps at decim 5);
+ * other configurations run the front end into scratch HBM, then the audio filter.
+ * audio: nstreams x audio_stride floats, ceil(ceil(n/rf_decim)/audio_decim) per stream. */
+int sdr_fe_mono_dev(sdr_ctx* ctx, const void* iq, int iq_dtype, int64_t n, int64_t stride, int nstreams,
+                    const double* rf_b, int rf_taps, int rf_decim, const double* audio_b, int audio_taps,
+                    int audio_decim, float* audio, int64_t audio_stride);
+
 int sdr_fir_dev(sdr_ctx* ctx, const float* x, const float* mix, float gain, int pre, int64_t n,
                 int64_t x_stride, int64_t hist, int nstreams, const double* b, int taps, int decim,
                 const double* zi, int64_t zi_stride, double* zf, float* y, int64_t y_stride);

@@ -225,6 +225,14 @@ def rds_blocks(iq_u8, block_values=307200, taps=151, nblocks=None, demod_fn=fm_d
     return out
 
 
+def mono_basic_coeffs(iq, rf_b, au_b, rf_decim=10, audio_decim=5, demod_fn=fm_demod_arctan):
+    """model/fmMonoBasic.py:70-111 with given coefficients: returns (audio, demod)."""
+    i_f = lfilter_fir(rf_b, iq[0::2])
+    q_f = lfilter_fir(rf_b, iq[1::2])
+    demod, _ = demod_fn(i_f[::rf_decim], q_f[::rf_decim], 0.0)
+    return lfilter_fir(au_b, demod)[::audio_decim], demod
+
+
 def mono_basic(iq, rf_taps=101, audio_taps=151, demod_fn=fm_demod_arctan):
     """Single-pass model/fmMonoBasic.py:67-136: lfilter without state over the whole
     capture, [::10], demod (prev 0), audio lfilter, [::5], int16(audio/2*32767)."""

@@ -40,6 +40,8 @@ struct FirLaunch {
 struct PllCfg { double freq, fs, scale, adj, kp, ki; };
 
 hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st);
+hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
+                              int64_t audio_stride, hipStream_t st);
 hipError_t sdr_launch_iq_zf(const void* iq, int u8, int64_t n, int64_t stride, int nstreams,
                             const double* b_dev, int T, const double* zi_i, const double* zi_q,
                             int64_t zi_stride, double* zf_i, double* zf_q, hipStream_t st);
@@ -378,6 +380,44 @@ int sdr_rf_frontend_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int
   if (prev_phase != nullptr)
     HIP_TRY(sdr_launch_demod_state(nstreams, M, last_phi, wraps, prev_phase, c->stream));
   return SDR_OK;
+}
+
+int sdr_fe_mono_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t stride, int nstreams,
+                    const double* rf_b, int rf_taps, int rf_decim, const double* audio_b, int audio_taps,
+                    int audio_decim, float* audio, int64_t audio_stride) {
+  CHECK_CTX(c);
+  if (n < 0 || nstreams < 0) return fail(SDR_EINVAL, "negative size");
+  if (iq_dtype != SDR_IQ_F32 && iq_dtype != SDR_IQ_U8) return fail(SDR_EINVAL, "iq_dtype %d", iq_dtype);
+  if (rf_decim < 1 || audio_decim < 1) return fail(SDR_EINVAL, "decim < 1");
+  const int64_t M = ceil_div(n, rf_decim);
+  const int64_t A = ceil_div(M, audio_decim);
+  if (n > 0 && (iq == nullptr || audio == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  if (nstreams > 1 && (audio_stride < A || stride < n)) return fail(SDR_EINVAL, "stream strides too small");
+  TRY(set_dev(c));
+  const TapSet *rts, *ats;
+  TRY(get_taps(c, audio_b, audio_taps, &ats));
+  TRY(get_taps(c, rf_b, rf_taps, &rts));
+  TRY(get_taps(c, audio_b, audio_taps, &ats));   // again: the second lookup may have reset the cache
+  const int u8 = iq_dtype == SDR_IQ_U8;
+  const int64_t xs = nstreams > 1 ? stride : ceil_div(n, 2) * 2;
+  const int64_t as = nstreams > 1 ? audio_stride : A;
+  const bool fused = !u8 && rf_decim == 10 && (rf_taps == 101 || rf_taps == 151) && audio_taps == 151 &&
+                     audio_decim == 5 && xs % 2 == 0 && ((uintptr_t)iq % 16) == 0 &&
+                     ((uintptr_t)audio % 8) == 0 && as % 2 == 0;
+  if (fused) {
+    FeLaunch a{iq, n, xs, 0, nstreams, rts->dev_f32, &rts->h, rf_taps, rf_decim, 0, nullptr, nullptr, 0,
+               nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr};
+    HIP_TRY(sdr_launch_fe_mono(a, ats->dev_f32, audio_taps, audio_decim, audio, as, c->stream));
+    return SDR_OK;
+  }
+  // any other configuration: front end into scratch HBM, then the audio filter
+  float* dm;
+  TRY(scratch(c, S_OUT3, sizeof(float) * (size_t)(M + 4) * (nstreams > 0 ? nstreams : 1), (void**)&dm));
+  TRY(sdr_rf_frontend_dev(c, iq, iq_dtype, n, nstreams > 1 ? stride : n, 0, nstreams, rf_b, rf_taps,
+                          rf_decim, nullptr, nullptr, 0, nullptr, nullptr, nullptr, dm, M + 4, nullptr,
+                          nullptr));
+  return sdr_fir_dev(c, dm, nullptr, 1.f, SDR_PRE_NONE, M, M + 4, 0, nstreams, audio_b, audio_taps,
+                     audio_decim, nullptr, 0, nullptr, audio, as);
 }
 
 int sdr_fir_dev(sdr_ctx* c, const float* x, const float* mix, float gain, int pre, int64_t n,

@@ -119,7 +119,8 @@ template <int T, int D, int R>
 __device__ __forceinline__ float fe_epilogue(const FeParams& p, int s, int64_t M, int64_t mw, int lane,
                                              float (&ai)[R], float (&aq)[R], float si, float sq,
                                              bool have_prev = false, float phi_prev = 0.f,
-                                             bool* one_store = nullptr) {
+                                             bool* one_store = nullptr, float* dv = nullptr,
+                                             bool do_store = true) {
   const int64_t mf = mw + (int64_t)lane * R;       // first output of this lane
   const int64_t zoff = (int64_t)s * p.zi_stride;
   float phi[R];
@@ -165,10 +166,15 @@ __device__ __forceinline__ float fe_epilogue(const FeParams& p, int s, int64_t M
     prev = phi[r];
   }
 
+  if (dv != nullptr) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) dv[r] = d[r];
+  }
   // one full-width store per lane (a wave writes 64*R contiguous floats: whole cache
   // lines; per-float stores at an R*4-B lane stride cost partial-line writes)
   float* out = p.demod + (int64_t)s * p.out_stride;
-  if (R == 4 && p.vec_out && mf + R <= M) {
+  if (!do_store || p.demod == nullptr) {
+  } else if (R == 4 && p.vec_out && mf + R <= M) {
     *reinterpret_cast<float4*>(out + mf) = make_float4(d[0], d[1 % R], d[2 % R], d[3 % R]);
   } else if (R == 2 && p.vec_out && mf + R <= M) {
     *reinterpret_cast<float2*>(out + mf) = make_float2(d[0], d[1 % R]);
@@ -200,7 +206,11 @@ __device__ __forceinline__ float fe_epilogue(const FeParams& p, int s, int64_t M
   if (one_store != nullptr) {
     const int64_t mend = mw + 64 * R;   // wave-uniform
     const bool simple = mend <= M - 1 && D * (mw - 1) >= T - 1 && p.i_ds == nullptr && p.wraps == nullptr &&
-                        (R == 3 || p.vec_out);
+                        (R == 3 || p.vec_out) && do_store && p.demod != nullptr;
+    // no vector-memory instruction at all: nothing to wait for either
+    const bool none = mend <= M - 1 && D * (mw - 1) >= T - 1 && p.i_ds == nullptr && p.wraps == nullptr &&
+                      (!do_store || p.demod == nullptr);
+    if (none) { *one_store = false; return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[R - 1]), 63)); }
     if (!simple) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     *one_store = simple;
   }
@@ -306,6 +316,63 @@ __global__ __launch_bounds__(NT) void fe_kernel(FeParams p, TapsF32 taps) {
   fe_epilogue<T, D, R>(p, s, M, mw, lane, ai, aq, si, sq);
 }
 
+// Register-blocked FIR of one tile image (see fe_stream_kernel): lane l produces the R
+// decimated (I, Q) outputs of its window [D R l + D + DELTA, + D(R-1)+T).
+template <int T, int D, int R, int MODE>
+__device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v (&tp)[(T + 1) / 2],
+                                            float (&ai)[R], float (&aq)[R]) {
+  constexpr int DELTA = (2 - ((D + T - 1) % 2)) % 2;
+  constexpr int NI = D * (R - 1) + T;
+  const f2v* win = buf + (D * R * lane + D + DELTA);
+  const float4* win4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(win, 16));
+  // two accumulator pairs per output (even / odd taps): 2R independent FMA chains per wave
+  f2v acc[R], acc2[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) { acc[r] = f2v{0.f, 0.f}; acc2[r] = f2v{0.f, 0.f}; }
+  if (MODE == 1 || MODE == 3) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = win[r];
+  } else {
+    // one ds_read_b128 per sample pair (the lane window starts 16-B aligned), issued by
+    // hand PF pairs ahead of use with counted lgkmcnt waits: hipcc would split the 16-B
+    // read into ds_read2_b64 (4-8-way bank conflicts at this lane stride) and read only
+    // one pair ahead (the LDS latency then stalls the wave).
+    constexpr int NP = (NI + 1) / 2;
+    constexpr int PF = 8;
+    f4v qb[NP];
+    static_for<0, (PF < NP ? PF : NP)>([&](auto I) { qb[I] = lds_read_b128<16 * I>(win4); });
+    static_for<0, NP>([&](auto I) {
+      constexpr int ip = I;
+      if constexpr (ip + PF < NP) {
+        qb[ip + PF] = lds_read_b128<16 * (ip + PF)>(win4);
+        lds_wait<PF>(qb[ip]);
+      } else {
+        lds_wait<NP - 1 - ip>(qb[ip]);
+      }
+      const f4v q = qb[ip];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = 2 * ip + h;
+        if (i >= NI) break;
+        const f2v x = h ? f2v{q.z, q.w} : f2v{q.x, q.y};
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int k = D * r + T - 1 - i;
+          if (k >= 0 && k < T) {
+            if (k & 1) pk_fma_bcast<true>(acc2[r], tp[k >> 1], x);
+            else pk_fma_bcast<false>(acc[r], tp[k >> 1], x);
+          }
+        }
+      }
+    });
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] += acc2[r];
+#pragma unroll
+  for (int r = 0; r < R; ++r) { ai[r] = acc[r].x; aq[r] = acc[r].y; }
+
+}
+
 // Persistent streaming f32 front end: the product kernel for f32 IQ.
 //
 // One wave per workgroup and WPC resident waves per CU; each wave walks a contiguous
@@ -406,54 +473,8 @@ void fe_stream_kernel(FeParams p, TapsF32 taps, int64_t total_tiles) {
       }
     }
 
-    const f2v* win = buf + (D * R * lane + D + DELTA);
-    const float4* win4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(win, 16));
-    // two accumulator pairs per output (even / odd taps): 2R independent FMA chains per wave
-    f2v acc[R], acc2[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) { acc[r] = f2v{0.f, 0.f}; acc2[r] = f2v{0.f, 0.f}; }
-    if (MODE == 1 || MODE == 3) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = win[r];
-    } else {
-      // one ds_read_b128 per sample pair (the lane window starts 16-B aligned), issued by
-      // hand PF pairs ahead of use with counted lgkmcnt waits: hipcc would split the 16-B
-      // read into ds_read2_b64 (4-8-way bank conflicts at this lane stride) and read only
-      // one pair ahead (the LDS latency then stalls the wave).
-      constexpr int NP = (NI + 1) / 2;
-      constexpr int PF = 8;
-      f4v qb[NP];
-      static_for<0, (PF < NP ? PF : NP)>([&](auto I) { qb[I] = lds_read_b128<16 * I>(win4); });
-      static_for<0, NP>([&](auto I) {
-        constexpr int ip = I;
-        if constexpr (ip + PF < NP) {
-          qb[ip + PF] = lds_read_b128<16 * (ip + PF)>(win4);
-          lds_wait<PF>(qb[ip]);
-        } else {
-          lds_wait<NP - 1 - ip>(qb[ip]);
-        }
-        const f4v q = qb[ip];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int i = 2 * ip + h;
-          if (i >= NI) break;
-          const f2v x = h ? f2v{q.z, q.w} : f2v{q.x, q.y};
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int k = D * r + T - 1 - i;
-            if (k >= 0 && k < T) {
-              if (k & 1) pk_fma_bcast<true>(acc2[r], tp[k >> 1], x);
-              else pk_fma_bcast<false>(acc[r], tp[k >> 1], x);
-            }
-          }
-        }
-      });
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] += acc2[r];
     float ai[R], aq[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) { ai[r] = acc[r].x; aq[r] = acc[r].y; }
+    fe_fir_tile<T, D, R, MODE>(buf, lane, tp, ai, aq);
 
     float si = 0.f, sq = 0.f;
     if (MODE != 3 && m0 > 0 && !have) {
@@ -475,6 +496,196 @@ void fe_stream_kernel(FeParams p, TapsF32 taps, int64_t total_tiles) {
     have = (s1 == s);          // the next tile continues this stream
     s = s1;
     m0 = m1;
+    issued = next;
+    b = bn;
+  }
+}
+
+// Fused RF front end + mono audio filter (FE kernel above + lfilter(audio, demod)[::DA]),
+// the device-resident continuous-stream form of model/fmMonoBlock.py:86-105: the demod
+// stream never leaves the CU.  Each wave owns a run of audio blocks; an audio block is
+// TPB FE tiles = TPB*64*R demod samples = 64*RA audio outputs.  Demod values go to a
+// wave-private LDS history (HA = TA-1 (+pad) samples of the previous block + the
+// current block); after the block's last tile, lane l computes audio outputs
+// RA*l .. RA*l+RA-1 from its window of the history (register-blocked like the FE FIR).
+// A wave whose first block is not a stream start first runs WU warm-up tiles to fill
+// the TA-1-sample history (their demod is not stored).  Zero pre-history at each
+// stream start (lfilter without zi), so this serves device streams, not the block API.
+template <int T, int D, int R, int NB, int TA, int DA, int MODE = 0>
+__global__ __launch_bounds__(64)
+void fe_mono_kernel(FeParams p, TapsF32 taps, const float* __restrict__ ataps, float* audio,
+                    int64_t audio_stride, int64_t total_blocks) {
+  constexpr int TO = 64 * R;                         // demod outputs per FE tile
+  constexpr int RA = 2;                              // audio outputs per lane per block
+  constexpr int BO = 64 * RA;                        // audio outputs per block
+  constexpr int BD = BO * DA;                        // demod samples per block
+  static_assert(BD % TO == 0, "audio block must be whole FE tiles");
+  constexpr int TPB = BD / TO;                       // FE tiles per audio block
+  constexpr int HA = ((TA - 1) + 3) / 4 * 4 + 2;     // history slots before the block (even, covers TA-1)
+  constexpr int WU = (TA - 1 + TO - 1) / TO;         // warm-up tiles
+  constexpr int G = 2;
+  constexpr int DELTA = (G - ((D + T - 1) % G)) % G;
+  constexpr int LRAW = D * TO + T + DELTA;
+  constexpr int NG = (LRAW + 127) / 128;
+  constexpr int L = NG * 128;
+  constexpr int LB = L + 2;
+  constexpr int TP = (T + 1) / 2;
+  constexpr int NW = DA * (RA - 1) + TA;             // audio window per lane
+  constexpr int NWP = (NW + 1) / 2 * 2;
+  static_assert(NG * (NB - 1) + 1 <= 63, "vmcnt range");
+  static_assert(((HA - (TA - 1)) % 2) == 0 && (DA * RA) % 2 == 0, "audio windows must start 8-B aligned");
+
+  __shared__ __attribute__((aligned(16))) f2v lds[NB * LB];
+  __shared__ __attribute__((aligned(16))) float dh[HA + BD + 4];
+  __shared__ __attribute__((aligned(16))) f2v ptab[NWP];
+
+  const int lane = threadIdx.x;
+  const int64_t nw = gridDim.x;
+  const int64_t b0 = (int64_t)blockIdx.x * total_blocks / nw;
+  const int64_t b1 = ((int64_t)blockIdx.x + 1) * total_blocks / nw;
+  if (b0 >= b1) return;
+  const int64_t M = (p.n + D - 1) / D;
+  const int64_t A = (M + DA - 1) / DA;               // lfilter(...)[::DA] length
+  const int64_t AB = (M + BD - 1) / BD;              // audio blocks per stream
+
+  f2v tp[TP];
+#pragma unroll
+  for (int j = 0; j < TP; ++j) tp[j] = f2v{taps.h[2 * j], (2 * j + 1 < T) ? taps.h[2 * j + 1] : 0.f};
+#pragma unroll
+  for (int j = 0; j < TP; ++j) asm volatile("" : "+v"(tp[j]));
+
+  // tile sequence: (stream s, audio block q, tile i within the block, i < 0: warm-up)
+  int s = (int)(b0 / AB);
+  int64_t q = b0 - (int64_t)s * AB;
+  int i = (q > 0) ? -WU : 0;
+  const int64_t U = (b1 - b0) * TPB + ((q > 0) ? WU : 0);
+  auto m0_of = [&](int64_t qq, int ii) { return (qq * TPB + ii) * (int64_t)TO; };
+  auto advance = [&](int& ss, int64_t& qq, int& ii) {
+    if (++ii == TPB) { ii = 0; if (++qq == AB) { qq = 0; ++ss; } }
+  };
+  auto interior = [&](int64_t mm) {
+    const int64_t n_lo = D * (mm - 1) - (T - 1) - DELTA;
+    return MODE != 2 && n_lo >= -p.hist && n_lo + L <= p.n;
+  };
+  auto issue = [&](int ss, int64_t mm, int b) {
+    const int64_t n_lo = D * (mm - 1) - (T - 1) - DELTA;
+    const float* g = reinterpret_cast<const float*>(p.iq) + 2 * ((int64_t)ss * p.stride + n_lo) + 4 * lane;
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+      __builtin_amdgcn_global_load_lds(g + 256 * j,
+                                       (__attribute__((address_space(3))) void*)(lds + b * LB + 128 * j),
+                                       16, 0, 2 /* nt */);
+  };
+
+  if (q == 0)
+    for (int e = lane; e < HA; e += 64) dh[e] = 0.f;   // stream start: zero pre-history
+  if (lane < 4) dh[HA + BD + lane] = 0.f;             // never-written tail (read as padding only)
+  for (int w = lane; w < NWP; w += 64) {
+    const int k0 = (TA - 1) - w, k1 = (TA - 1) + DA - w;
+    ptab[w] = f2v{(w < NW && k0 >= 0 && k0 < TA) ? ataps[k0] : 0.f,
+                  (w < NW && k1 >= 0 && k1 < TA) ? ataps[k1] : 0.f};
+  }
+  bool issued = interior(m0_of(q, i));
+  if (issued) issue(s, m0_of(q, i), 0);
+  float carry = 0.f;
+  bool have = false;
+  bool store_pending = false;
+  int b = 0;
+  for (int64_t u = 0; u < U; ++u) {
+    const int64_t m0 = m0_of(q, i);
+    int s1 = s, i1 = i;
+    int64_t q1 = q;
+    advance(s1, q1, i1);
+    const int64_t m1 = m0_of(q1, i1);
+    const int bn = (b + 1 == NB) ? 0 : b + 1;
+    const bool next = (u + 1 < U) && interior(m1);
+    if (next) issue(s1, m1, bn);
+    f2v* buf = lds + b * LB;
+    if (issued) {
+      if (next && store_pending) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NG + 1) : "memory");
+      else if (next) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NG) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      const int64_t n_lo = D * (m0 - 1) - (T - 1) - DELTA;
+      const float* base = reinterpret_cast<const float*>(p.iq) + 2 * ((int64_t)s * p.stride);
+      for (int e = lane; e < L; e += 64) {
+        const int64_t nn = n_lo + e;
+        f2v x = f2v{0.f, 0.f};
+        if (MODE == 2) x = f2v{(float)e * 1e-4f, (float)lane};
+        else if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
+        buf[e] = x;
+      }
+    }
+
+    float ai[R], aq[R];
+    fe_fir_tile<T, D, R, MODE>(buf, lane, tp, ai, aq);
+    float si = 0.f, sq = 0.f;
+    if (m0 > 0 && !have) {
+      for (int k = lane; k < T; k += 64) {
+        const f2v x = buf[(T - 1) + DELTA - k];
+        const float h = p.taps_dev[k];
+        si = fmaf(h, x.x, si);
+        sq = fmaf(h, x.y, sq);
+      }
+      si = wave_sum(si);
+      sq = wave_sum(sq);
+    }
+    float d[R];
+    bool sp = false;
+    carry = fe_epilogue<T, D, R>(p, s, M, m0, lane, ai, aq, si, sq, have, carry, &sp, d, i >= 0);
+    // demod -> history: sample m0 + R*lane + r sits at dh[HA + i*TO + R*lane + r]
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int rel = i * TO + R * lane + r;
+      if (rel >= -HA) dh[HA + rel] = d[r];
+    }
+
+    bool ast = false;
+    if (i == TPB - 1) {
+      asm volatile("" ::: "memory");   // history writes of other lanes precede the window reads
+      // audio outputs j = q*BO + RA*lane + ra:  a[j] = sum_k g[k] d[DA*j - k]
+      // lane window: dh[HA + DA*RA*lane - (TA-1) + w], w = 0 .. NW-1; per sample one
+      // v_pk_fma_f32 updates both outputs with the tap pair {g[TA-1-w], g[TA-1+DA-w]}
+      // (a uniform-address LDS read: broadcast, no bank conflicts)
+      const float* aw = dh + (HA - (TA - 1) + DA * RA * lane);
+      f2v acc[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+      static_for<0, NWP / 2>([&](auto I) {
+        constexpr int w = 2 * I;
+        const f2v x2 = *reinterpret_cast<const f2v*>(aw + w);
+        const f4v pp = *reinterpret_cast<const f4v*>(ptab + w);
+        pk_fma_bcast_x<false>(acc[(I & 1) * 2], f2v{pp.x, pp.y}, x2);
+        pk_fma_bcast_x<true>(acc[(I & 1) * 2 + 1], f2v{pp.z, pp.w}, x2);
+      });
+      const float a0 = (acc[0].x + acc[1].x) + (acc[2].x + acc[3].x);
+      const float a1 = (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y);
+      const int64_t j = q * BO + RA * lane;
+      float* ao = audio + (int64_t)s * audio_stride + j;
+      if (j + RA <= A) {
+        *reinterpret_cast<float2*>(ao) = make_float2(a0, a1);
+        ast = true;
+      } else {
+        if (j < A) ao[0] = a0;
+        if (j + 1 < A) ao[1] = a1;
+      }
+      // carry the last HA demod samples into the history slots of the next block
+      // (every lane has finished its window reads: LDS ops of one wave complete in order)
+      asm volatile("" ::: "memory");
+      if (q1 == 0)
+        for (int e = lane; e < HA; e += 64) dh[e] = 0.f;   // next block starts a new stream
+      else
+        for (int e = lane; e < HA; e += 64) dh[e] = dh[BD + e];
+      asm volatile("" ::: "memory");
+    }
+    // exactly-one-store accounting for the next wait (see fe_stream_kernel)
+    const bool full_audio = (i == TPB - 1) && (q * BO + BO <= A);
+    if (i == TPB - 1 && !full_audio) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int nst = (sp ? 1 : 0) + (full_audio ? 1 : 0);
+    if (nst == 2) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // keep at most one outstanding
+    store_pending = nst >= 1;
+    (void)ast;
+
+    have = (s1 == s);
+    s = s1; q = q1; i = i1;
     issued = next;
     b = bn;
   }
@@ -580,6 +791,37 @@ hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st) {
   switch (a.T) {
     case 101: return a.u8 ? launch_fe_t<101, 10, true>(a, st) : launch_fe_t<101, 10, false>(a, st);
     case 151: return a.u8 ? launch_fe_t<151, 10, true>(a, st) : launch_fe_t<151, 10, false>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int T, int TA>
+static hipError_t launch_fe_mono_t(const FeLaunch& a, const float* ataps, float* audio,
+                                   int64_t audio_stride, hipStream_t st) {
+  constexpr int D = 10, R = 2, NB = 2, DA = 5;
+  constexpr int BD = 64 * 2 * DA;                  // demod samples per audio block
+  FeParams p{};
+  p.iq = a.iq; p.n = a.n; p.stride = a.stride; p.hist = 0; p.nstreams = a.nstreams;
+  p.taps_dev = a.taps_dev;
+  const int64_t M = (a.n + D - 1) / D;
+  const int64_t blocks = (M + BD - 1) / BD * a.nstreams;
+  if (blocks <= 0) return hipSuccess;
+  static const int wpc = resident_per_cu(fe_mono_kernel<T, D, R, NB, TA, DA>, 64);
+  const int64_t grid = std::min<int64_t>(blocks, (int64_t)cu_count() * wpc);
+  hipLaunchKernelGGL((fe_mono_kernel<T, D, R, NB, TA, DA>), dim3((unsigned)grid), dim3(64), 0, st, p,
+                     *a.taps, ataps, audio, audio_stride, blocks);
+  return hipGetLastError();
+}
+
+// Fused FE + mono audio filter over whole streams (zero initial state).  Supported: f32 IQ,
+// RF taps 101/151 at decim 10, audio taps 151 at decim 5 (model/fmMonoBlock.py:24-31);
+// anything else returns hipErrorInvalidValue and the C-ABI runs the two-kernel path.
+hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
+                              int64_t audio_stride, hipStream_t st) {
+  if (a.D != 10 || a.u8 || TA != 151 || DA != 5) return hipErrorInvalidValue;
+  switch (a.T) {
+    case 101: return launch_fe_mono_t<101, 151>(a, ataps, audio, audio_stride, st);
+    case 151: return launch_fe_mono_t<151, 151>(a, ataps, audio, audio_stride, st);
     default: return hipErrorInvalidValue;
   }
 }

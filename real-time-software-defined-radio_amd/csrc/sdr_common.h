@@ -41,6 +41,17 @@ __device__ __forceinline__ void pk_fma_bcast(f2v& acc, const f2v& tap2, const f2
     asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(tap2), "v"(x));
 }
 
+// acc += tap2 * {x, x} with x = the low (HI=false) or high (HI=true) half of x2: the
+// mirror of pk_fma_bcast, broadcasting the sample instead of the tap (two filters, or two
+// outputs of one filter, per sample).
+template <bool HI>
+__device__ __forceinline__ void pk_fma_bcast_x(f2v& acc, const f2v& tap2, const f2v& x2) {
+  if (HI)
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(tap2), "v"(x2));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(tap2), "v"(x2));
+}
+
 // ds_read_b128 issued by hand: hipcc neither splits it (into ds_read2_b64, whose 32-bank
 // mapping is conflict-prone for strided lane windows) nor counts it, so every use must be
 // preceded by lds_wait<N> naming the destination (N = LDS reads issued after it).

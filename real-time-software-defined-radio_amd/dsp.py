@@ -15,6 +15,8 @@ plus the fused forms the hot path is built from:
     rf_frontend_block(iq, rf_coeff, zi_i, zi_q, prev_phase, rf_decim=10)
     mono_block(iq, rf_coeff, audio_coeff, state)
     resample(x, b, zi, up, down)               model/fmRDSblock.py:184-199
+    fm_mono_streams(iq, rf_coeff, audio_coeff) model/fmMonoBasic.py:70-111 over one or
+                                               more whole streams, demod kept on chip
 
 Arrays come back as float64 (the reference's dtype) so downstream np.concatenate /
 wavfile code is unchanged; the kernels compute in f32 (state in f64), see DESIGN.md.
@@ -259,3 +261,36 @@ def mono_block(iq, rf_coeff, audio_coeff, state: MonoState, rf_decim=10, audio_d
     state.phase = float(ph[0])
     audio = audio.astype(np.float64)
     return (audio, demod.astype(np.float64)) if return_demod else audio
+
+
+def fm_mono_streams(iq, rf_coeff, audio_coeff, rf_decim=10, audio_decim=5, ctx=None):
+    """Whole-capture mono receiver of model/fmMonoBasic.py:70-111 (lfilter without state,
+    [::rf_decim], fmDemodArctan from phase 0, audio lfilter, [::audio_decim]) for each row
+    of `iq` (1-D: one stream; 2-D: streams x interleaved samples), in one fused kernel
+    (sdr_fe_mono_dev): the demodulated signal never leaves the CU.  Returns float64 audio
+    of shape (ceil(ceil(n / rf_decim) / audio_decim),) or (streams, that)."""
+    b = _taps(rf_coeff)
+    ab = _taps(audio_coeff)
+    iq = np.asarray(iq)
+    one = iq.ndim == 1
+    iq2 = iq[None, :] if one else iq
+    if iq2.ndim != 2 or iq2.shape[1] % 2:
+        raise ValueError("iq must be [I0, Q0, ...] rows of even length")
+    rows = [_iq_args(r) for r in iq2]
+    dt = rows[0][1]
+    data = np.ascontiguousarray(np.stack([r[0] for r in rows])) if rows else iq2
+    S, n = data.shape[0], data.shape[1] // 2
+    c = _ctx(ctx)
+    m = (n + rf_decim - 1) // rf_decim
+    a = (m + audio_decim - 1) // audio_decim
+    astride = a + (a & 1)
+    d_iq = _lib.DeviceBuffer.from_array(c, data)
+    d_au = _lib.DeviceBuffer(c, 4 * max(astride * S, 4))
+    try:
+        check(c.lib.sdr_fe_mono_dev(c.handle, d_iq.ptr, dt, n, n, S, f64p(b), len(b), int(rf_decim), f64p(ab),
+                                    len(ab), int(audio_decim), d_au.ptr, astride), "sdr_fe_mono_dev")
+        out = d_au.download(astride * S).reshape(S, astride)[:, :a].astype(np.float64)
+    finally:
+        d_iq.free()
+        d_au.free()
+    return out[0] if one else out
