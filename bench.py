@@ -149,11 +149,13 @@ def cpu_baseline(args, rf_b, au_b):
 
 
 def load_traffic(path, taps, blocks, kpath):
+    """HBM bytes per launch of the dominant kernel, from tools/pmc_traffic.py's PMC summary."""
     try:
         with open(path) as f:
             t = json.load(f)
-        if t.get("taps") == taps and t.get("n_complex") == blocks * BLOCK and t.get("path", "split") == kpath:
-            return t.get("hbm_bytes_per_launch")
+        for e in t.get("entries", []):
+            if e.get("taps") == taps and e.get("n_complex") == blocks * BLOCK and e.get("path") == kpath:
+                return e.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     return None

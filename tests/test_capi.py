@@ -113,3 +113,12 @@ def test_synthetic_iq_is_deterministic_and_bounded(sdr):
     z = a[0::2] + 1j * a[1::2]
     step = np.abs(np.angle(z[10::10] * np.conj(z[:-10:10])))
     assert np.percentile(step, 99) < np.pi
+
+
+def test_product_never_imports_oracle():
+    """The shipped package must not import, load or execute anything under oracle/."""
+    import pathlib
+    pkg = pathlib.Path(__file__).resolve().parents[1] / "real-time-software-defined-radio_amd"
+    for f in list(pkg.rglob("*.py")) + list(pkg.rglob("*.hip")) + list(pkg.rglob("*.h")) + [pkg / "csrc" / "Makefile"]:
+        text = f.read_text()
+        assert "oracle" not in text.replace("never imports oracle", ""), f
