@@ -212,6 +212,7 @@ def main():
         for k, f in enumerate(stages):
             f()
             tm.record(e[k + 1])
+    t_enq = time.perf_counter() - t0                 # host enqueue time (async launches)
     ctx.synchronize()
     barrier(ws)
     elapsed = max_over_ranks(ws, time.perf_counter() - t0)
@@ -258,6 +259,7 @@ def main():
                          "kernel": kname, "algorithmic_bytes_per_launch": k_bytes,
                          "avg_launch_ms": round(k_avg, 5)},
             "kernels_ms": kernels,
+            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
         }
     if ws == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, rf_b, au_b)

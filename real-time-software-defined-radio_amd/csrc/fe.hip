@@ -343,11 +343,14 @@ __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v 
     static_for<0, (PF < NP ? PF : NP)>([&](auto I) { qb[I] = lds_read_b128<16 * I>(win4); });
     static_for<0, NP>([&](auto I) {
       constexpr int ip = I;
+      // the wait is an operand-free volatile asm ordered with the (volatile) FMAs; an asm
+      // "defining" qb[ip] right before its first reader costs an s_nop per step (hipcc's
+      // gfx950 dst-forwarding hazard rule, applied conservatively to inline asm)
       if constexpr (ip + PF < NP) {
         qb[ip + PF] = lds_read_b128<16 * (ip + PF)>(win4);
-        lds_wait<PF>(qb[ip]);
+        lds_wait_ordered<PF>();
       } else {
-        lds_wait<NP - 1 - ip>(qb[ip]);
+        lds_wait_ordered<NP - 1 - ip>();
       }
       const f4v q = qb[ip];
 #pragma unroll
@@ -501,52 +504,71 @@ void fe_stream_kernel(FeParams p, TapsF32 taps, int64_t total_tiles) {
   }
 }
 
-// Fused RF front end + mono audio filter (FE kernel above + lfilter(audio, demod)[::DA]),
-// the device-resident continuous-stream form of model/fmMonoBlock.py:86-105: the demod
-// stream never leaves the CU.  Each wave owns a run of audio blocks; an audio block is
-// TPB FE tiles = TPB*64*R demod samples = 64*RA audio outputs.  Demod values go to a
-// wave-private LDS history (HA = TA-1 (+pad) samples of the previous block + the
-// current block); after the block's last tile, lane l computes audio outputs
-// RA*l .. RA*l+RA-1 from its window of the history (register-blocked like the FE FIR).
-// A wave whose first block is not a stream start first runs WU warm-up tiles to fill
-// the TA-1-sample history (their demod is not stored).  Zero pre-history at each
-// stream start (lfilter without zi), so this serves device streams, not the block API.
-template <int T, int D, int R, int NB, int TA, int DA, int MODE = 0>
-__global__ __launch_bounds__(64)
-void fe_mono_kernel(FeParams p, TapsF32 taps, const float* __restrict__ ataps, float* audio,
-                    int64_t audio_stride, int64_t total_blocks) {
-  constexpr int TO = 64 * R;                         // demod outputs per FE tile
-  constexpr int RA = 2;                              // audio outputs per lane per block
-  constexpr int BO = 64 * RA;                        // audio outputs per block
-  constexpr int BD = BO * DA;                        // demod samples per block
-  static_assert(BD % TO == 0, "audio block must be whole FE tiles");
-  constexpr int TPB = BD / TO;                       // FE tiles per audio block
-  constexpr int HA = ((TA - 1) + 3) / 4 * 4 + 2;     // history slots before the block (even, covers TA-1)
-  constexpr int WU = (TA - 1 + TO - 1) / TO;         // warm-up tiles
-  constexpr int G = 2;
-  constexpr int DELTA = (G - ((D + T - 1) % G)) % G;
-  constexpr int LRAW = D * TO + T + DELTA;
-  constexpr int NG = (LRAW + 127) / 128;
-  constexpr int L = NG * 128;
-  constexpr int LB = L + 2;
-  constexpr int TP = (T + 1) / 2;
-  constexpr int NW = DA * (RA - 1) + TA;             // audio window per lane
-  constexpr int NWP = (NW + 1) / 2 * 2;
-  static_assert(NG * (NB - 1) + 1 <= 63, "vmcnt range");
-  static_assert(((HA - (TA - 1)) % 2) == 0 && (DA * RA) % 2 == 0, "audio windows must start 8-B aligned");
+// ---------------------------------------------------------------------------------
+// fe_ring_kernel: the product f32 front end (R = 3 outputs per lane, TO = 192 per tile).
+//
+// Differences from fe_stream_kernel (r01 profile: 178 SALU + 338 VALU per 128-output
+// tile, 2-way LDS bank conflicts at the R=2 lane stride, 7 waves/CU spread 2-2-2-1 over
+// the SIMDs, 1.087x the algorithmic HBM reads):
+//  * R = 3: the lane stride (30 samples = 15 x 16 B, odd) puts every ds_read_b128 lane
+//    group on 16 distinct bank quads -> conflict-free, and 20 LDS reads per output
+//    instead of 28;
+//  * halo reuse: consecutive tiles of a wave overlap by NCH-15 chunks; only the 15 new
+//    1-KiB chunks are DMA'd and the halo is copied LDS->LDS (HBM bytes = algorithmic);
+//  * LDS-DMA in the saddr form with immediate chunk offsets (glds16), exact vmcnt
+//    accounting through a running issue counter, 32-bit per-tile index math;
+//  * a fast epilogue for interior tiles (atan2, DPP predecessor, wrap, one 12-B store per
+//    lane, wrap counts kept per lane and reduced once per stream segment); head/tail
+//    tiles, zi, i_ds/q_ds and last_phi go through the general fe_epilogue;
+//  * 4 resident waves per CU = one per SIMD (LDS: 2 x 16 KiB ring per wave).
+// ---------------------------------------------------------------------------------
+struct RingArgs {
+  int64_t total;       // work units: tiles (FE), or audio blocks (FUSED), over all streams
+  int per_wave;        // units per wave (contiguous run)
+  int tps;             // tiles per stream in the tile sequence
+  int ab;              // FUSED: audio blocks per stream
+  float* audio;        // FUSED: per stream ceil(M/DA) audio samples, audio_stride apart
+  int64_t audio_stride;
+  const float* ataps;  // FUSED: TA audio taps (device)
+};
 
-  __shared__ __attribute__((aligned(16))) f2v lds[NB * LB];
-  __shared__ __attribute__((aligned(16))) float dh[HA + BD + 4];
-  __shared__ __attribute__((aligned(16))) f2v ptab[NWP];
+// FUSED = the continuous-stream mono receiver (sdr_fe_mono_dev): an audio block is DA
+// tiles = 960 demod samples = 192 audio outputs (RA = 3 per lane).  Demod values go to
+// a wave-private LDS history instead of HBM; after a block's last tile lane l computes
+// audio outputs 3l..3l+2 of the block:  a[j] = sum_k g[k] d[5j - k].  A wave whose run
+// starts mid-stream first runs one warm-up tile (192 >= TA-1 demod samples of history).
+template <int T, bool FUSED = false, int MODE = 0>
+__global__ __launch_bounds__(64)
+void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
+  constexpr int D = 10, R = 3, TO = 64 * R;
+  constexpr int NEWC = D * TO / 128;                 // 15 new 1-KiB chunks per tile
+  constexpr int NCH = (D * TO + T + 1 + 127) / 128;  // chunks per tile image
+  constexpr int HCH = NCH - NEWC;                    // halo chunks shared with the next tile
+  constexpr int L = NCH * 128;                       // image length (complex samples)
+  constexpr int TP = (T + 1) / 2;
+  static_assert((T & 1) == 1 && HCH >= 1 && HCH <= 2, "odd tap counts 101..235");
+  static_assert(D * TO % 128 == 0, "tiles advance by whole chunks");
+  // audio (FUSED): TA = 151 taps, DA = 5
+  constexpr int TA = 151, DA = 5, RA = R;
+  constexpr int TPB = DA;                            // tiles per audio block
+  constexpr int BD = TO * TPB;                       // 960 demod samples per block
+  constexpr int BO = 64 * RA;                        // 192 audio outputs per block
+  constexpr int HA = 152;                            // history slots (>= TA-1)
+  constexpr int NW = DA * (RA - 1) + TA;             // 161-sample audio window per lane
+  static_assert(BD == DA * BO, "block bookkeeping");
+
+  // slot stride >= 20 KiB: at most 4 resident waves per CU (one per SIMD; a 5th wave would
+  // double one SIMD's load and set the pace of the whole launch)
+  constexpr int LS = FUSED ? L : (L > 2560 ? L : 2560);
+  __shared__ __attribute__((aligned(16))) f2v ring[2][LS];
+  __shared__ __attribute__((aligned(16))) float dh[FUSED ? HA + BD + 4 : 1];
+  __shared__ __attribute__((aligned(16))) f4v ptab[FUSED ? NW + 1 : 1];
 
   const int lane = threadIdx.x;
-  const int64_t nw = gridDim.x;
-  const int64_t b0 = (int64_t)blockIdx.x * total_blocks / nw;
-  const int64_t b1 = ((int64_t)blockIdx.x + 1) * total_blocks / nw;
-  if (b0 >= b1) return;
+  const int64_t u0 = (int64_t)blockIdx.x * a.per_wave;
+  if (u0 >= a.total) return;
+  const int nunits = (int)min<int64_t>(a.per_wave, a.total - u0);
   const int64_t M = (p.n + D - 1) / D;
-  const int64_t A = (M + DA - 1) / DA;               // lfilter(...)[::DA] length
-  const int64_t AB = (M + BD - 1) / BD;              // audio blocks per stream
 
   f2v tp[TP];
 #pragma unroll
@@ -554,140 +576,252 @@ void fe_mono_kernel(FeParams p, TapsF32 taps, const float* __restrict__ ataps, f
 #pragma unroll
   for (int j = 0; j < TP; ++j) asm volatile("" : "+v"(tp[j]));
 
-  // tile sequence: (stream s, audio block q, tile i within the block, i < 0: warm-up)
-  int s = (int)(b0 / AB);
-  int64_t q = b0 - (int64_t)s * AB;
-  int i = (q > 0) ? -WU : 0;
-  const int64_t U = (b1 - b0) * TPB + ((q > 0) ? WU : 0);
-  auto m0_of = [&](int64_t qq, int ii) { return (qq * TPB + ii) * (int64_t)TO; };
-  auto advance = [&](int& ss, int64_t& qq, int& ii) {
-    if (++ii == TPB) { ii = 0; if (++qq == AB) { qq = 0; ++ss; } }
-  };
-  auto interior = [&](int64_t mm) {
-    const int64_t n_lo = D * (mm - 1) - (T - 1) - DELTA;
-    return MODE != 2 && n_lo >= -p.hist && n_lo + L <= p.n;
-  };
-  auto issue = [&](int ss, int64_t mm, int b) {
-    const int64_t n_lo = D * (mm - 1) - (T - 1) - DELTA;
-    const float* g = reinterpret_cast<const float*>(p.iq) + 2 * ((int64_t)ss * p.stride + n_lo) + 4 * lane;
-#pragma unroll
-    for (int j = 0; j < NG; ++j)
-      __builtin_amdgcn_global_load_lds(g + 256 * j,
-                                       (__attribute__((address_space(3))) void*)(lds + b * LB + 128 * j),
-                                       16, 0, 2 /* nt */);
+  const unsigned voff = 16u * lane;
+  const float* iqf = reinterpret_cast<const float*>(p.iq);
+  // tile (s, i): outputs m0 = TO*i ..; image = samples [n_lo, n_lo + L) of stream s,
+  // n_lo = D*(m0-1) - (T-1) (output m0-1's window first, for the predecessor)
+  auto n_lo_of = [&](int i) { return (int64_t)(D * TO) * i - D - (T - 1); };
+  auto interior = [&](int64_t nl) { return MODE != 2 && nl >= -p.hist && nl + L <= p.n; };
+  // issue chunks [0 or HCH, NCH) of tile image nl (stream s) into ring slot b
+  auto issue = [&](int s, int64_t nl, int b, bool full) {
+    const char* g = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s * p.stride + nl));
+    const unsigned lb = lds_addr_of(&ring[b][0]);
+    auto run = [&](auto C0) {
+      constexpr int c0 = decltype(C0)::value;
+      static_for<0, (NCH - c0 + 3) / 4>([&](auto Q) {
+        constexpr int c = c0 + 4 * Q;
+        constexpr int n = (NCH - c) < 4 ? (NCH - c) : 4;
+        glds16x<n>(voff, g + 1024 * c, lb + 1024 * c);
+      });
+    };
+    if (full) run(std::integral_constant<int, 0>{});
+    else run(std::integral_constant<int, HCH>{});
   };
 
-  if (q == 0)
-    for (int e = lane; e < HA; e += 64) dh[e] = 0.f;   // stream start: zero pre-history
-  if (lane < 4) dh[HA + BD + lane] = 0.f;             // never-written tail (read as padding only)
-  for (int w = lane; w < NWP; w += 64) {
-    const int k0 = (TA - 1) - w, k1 = (TA - 1) + DA - w;
-    ptab[w] = f2v{(w < NW && k0 >= 0 && k0 < TA) ? ataps[k0] : 0.f,
-                  (w < NW && k1 >= 0 && k1 < TA) ? ataps[k1] : 0.f};
+  // tile sequence of this wave
+  int s, i, U;
+  if constexpr (FUSED) {
+    s = (int)(u0 / a.ab);
+    const int q0 = (int)(u0 - (int64_t)s * a.ab);
+    i = TPB * q0 - (q0 > 0 ? 1 : 0);
+    U = nunits * TPB + (q0 > 0 ? 1 : 0);
+    if (q0 == 0)
+      for (int e = lane; e < HA; e += 64) dh[e] = 0.f;          // stream start: zero history
+    for (int e = lane; e < 4; e += 64) dh[HA + BD + e] = 0.f;
+    for (int w = lane; w < NW + 1; w += 64) {               // entry NW: zero (pairs over-read)
+      const int k0 = (TA - 1) - w, k1 = k0 + DA, k2 = k0 + 2 * DA;
+      ptab[w] = f4v{(k0 >= 0 && k0 < TA) ? a.ataps[k0] : 0.f, (k1 >= 0 && k1 < TA) ? a.ataps[k1] : 0.f,
+                    (k2 >= 0 && k2 < TA) ? a.ataps[k2] : 0.f, 0.f};
+    }
+  } else {
+    s = (int)(u0 / a.tps);
+    i = (int)(u0 - (int64_t)s * a.tps);
+    U = nunits;
   }
-  bool issued = interior(m0_of(q, i));
-  if (issued) issue(s, m0_of(q, i), 0);
+  int64_t nl = n_lo_of(i);
+  // kinds: 0 none, 1 guarded (built with plain loads at compute time), 2 DMA full, 3 DMA halo
+  int kind = interior(nl) ? 2 : 1;
+  int issued = 0, mark = 0;
+  if (kind == 2) { issue(s, nl, 0, true); issued += NCH; mark = issued; }
   float carry = 0.f;
   bool have = false;
-  bool store_pending = false;
+  int wacc = 0;
   int b = 0;
-  for (int64_t u = 0; u < U; ++u) {
-    const int64_t m0 = m0_of(q, i);
-    int s1 = s, i1 = i;
-    int64_t q1 = q;
-    advance(s1, q1, i1);
-    const int64_t m1 = m0_of(q1, i1);
-    const int bn = (b + 1 == NB) ? 0 : b + 1;
-    const bool next = (u + 1 < U) && interior(m1);
-    if (next) issue(s1, m1, bn);
-    f2v* buf = lds + b * LB;
-    if (issued) {
-      if (next && store_pending) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NG + 1) : "memory");
-      else if (next) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NG) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // MODE 6 (tuning): per-phase s_memtime accounting -> p.q_ds as uint64[grid][8]
+  uint64_t tph[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t tlast = 0;
+  auto stamp = [&](int k) {
+    if constexpr (MODE == 6) {
+      uint64_t t;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+      if (k >= 0) tph[k] += t - tlast;
+      tlast = t;
+    }
+  };
+  stamp(-1);
+  for (int u = 0; u < U; ++u) {
+    // ---- next tile: position, kind, issue ----
+    int s1 = s, i1 = i + 1;
+    if (i1 == a.tps) { i1 = 0; ++s1; }
+    const int64_t nl1 = (s1 == s) ? nl + D * TO : n_lo_of(0);
+    int kind1 = 0, mark1 = 0;
+    if (u + 1 < U) {
+      if (s1 == s && MODE != 2 && MODE != 5 && nl1 + L <= p.n && nl1 + HCH * 128 >= -p.hist) kind1 = 3;
+      else kind1 = interior(nl1) ? 2 : 1;
+      if (kind1 >= 2) {
+        issue(s1, nl1, b ^ 1, kind1 == 2);
+        issued += (kind1 == 2) ? NCH : NEWC;
+        mark1 = issued;
+      }
+    }
+    f2v* buf = &ring[b][0];
+    const int64_t m0 = (int64_t)TO * i;
+    stamp(0);
+    // ---- this tile's image ----
+    if (kind >= 2) {
+      const int nw = issued - mark;                  // VMEM ops issued after this tile's loads
+      if (nw == NEWC) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC) : "memory");
+      else if (nw == NEWC + 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC + 1) : "memory");
+      else wait_vm_chain(nw);
     } else {
-      const int64_t n_lo = D * (m0 - 1) - (T - 1) - DELTA;
-      const float* base = reinterpret_cast<const float*>(p.iq) + 2 * ((int64_t)s * p.stride);
+      const float* base = iqf + 2 * ((int64_t)s * p.stride);
       for (int e = lane; e < L; e += 64) {
-        const int64_t nn = n_lo + e;
+        const int64_t nn = nl + e;
         f2v x = f2v{0.f, 0.f};
         if (MODE == 2) x = f2v{(float)e * 1e-4f, (float)lane};
         else if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
         buf[e] = x;
       }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      issued = 0; mark1 = 0;
+    }
+    stamp(1);
+    // halo of the next tile: read now, written after the FIR (all reads then returned)
+    f4v h0, h1;
+    if (kind1 == 3) {
+      h0 = lds_read_b128<0>(buf + NEWC * 128 + 2 * lane);
+      if constexpr (HCH == 2) h1 = lds_read_b128<0>(buf + (NEWC + 1) * 128 + 2 * lane);
     }
 
     float ai[R], aq[R];
-    fe_fir_tile<T, D, R, MODE>(buf, lane, tp, ai, aq);
-    float si = 0.f, sq = 0.f;
-    if (m0 > 0 && !have) {
-      for (int k = lane; k < T; k += 64) {
-        const f2v x = buf[(T - 1) + DELTA - k];
-        const float h = p.taps_dev[k];
-        si = fmaf(h, x.x, si);
-        sq = fmaf(h, x.y, sq);
-      }
-      si = wave_sum(si);
-      sq = wave_sum(sq);
+    fe_fir_tile<T, D, R, (MODE == 1 || MODE >= 4) ? 1 : 0>(buf, lane, tp, ai, aq);
+
+    if (kind1 == 3) {
+      lds_wait<0>(h0);
+      f2v* nb = &ring[b ^ 1][0];
+      lds_write_b128(nb + 2 * lane, h0);
+      if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(nb + 128 + 2 * lane, h1); }
     }
+
+    stamp(2);
+    // ---- epilogue ----
     float d[R];
-    bool sp = false;
-    carry = fe_epilogue<T, D, R>(p, s, M, m0, lane, ai, aq, si, sq, have, carry, &sp, d, i >= 0);
-    // demod -> history: sample m0 + R*lane + r sits at dh[HA + i*TO + R*lane + r]
+    const bool fast = i >= 1 && m0 + TO < M && p.i_ds == nullptr && have;
+    if (MODE >= 4) {          // tuning: memory pipeline only
+      carry += ai[0] + aq[0];
+      d[0] = d[1] = d[2] = carry;
+    } else if (fast) {
+      float phi[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int rel = i * TO + R * lane + r;
-      if (rel >= -HA) dh[HA + rel] = d[r];
-    }
-
-    bool ast = false;
-    if (i == TPB - 1) {
-      asm volatile("" ::: "memory");   // history writes of other lanes precede the window reads
-      // audio outputs j = q*BO + RA*lane + ra:  a[j] = sum_k g[k] d[DA*j - k]
-      // lane window: dh[HA + DA*RA*lane - (TA-1) + w], w = 0 .. NW-1; per sample one
-      // v_pk_fma_f32 updates both outputs with the tap pair {g[TA-1-w], g[TA-1+DA-w]}
-      // (a uniform-address LDS read: broadcast, no bank conflicts)
-      const float* aw = dh + (HA - (TA - 1) + DA * RA * lane);
-      f2v acc[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
-      static_for<0, NWP / 2>([&](auto I) {
-        constexpr int w = 2 * I;
-        const f2v x2 = *reinterpret_cast<const f2v*>(aw + w);
-        const f4v pp = *reinterpret_cast<const f4v*>(ptab + w);
-        pk_fma_bcast_x<false>(acc[(I & 1) * 2], f2v{pp.x, pp.y}, x2);
-        pk_fma_bcast_x<true>(acc[(I & 1) * 2 + 1], f2v{pp.z, pp.w}, x2);
-      });
-      const float a0 = (acc[0].x + acc[1].x) + (acc[2].x + acc[3].x);
-      const float a1 = (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y);
-      const int64_t j = q * BO + RA * lane;
-      float* ao = audio + (int64_t)s * audio_stride + j;
-      if (j + RA <= A) {
-        *reinterpret_cast<float2*>(ao) = make_float2(a0, a1);
-        ast = true;
-      } else {
-        if (j < A) ao[0] = a0;
-        if (j + 1 < A) ao[1] = a1;
+      for (int r = 0; r < R; ++r) phi[r] = fast_atan2f(aq[r], ai[r]);
+      const float from_left = __int_as_float(__builtin_amdgcn_update_dpp(
+          0, __float_as_int(phi[R - 1]), 0x138 /*wave_shr:1*/, 0xf, 0xf, false));
+      float prev = (lane == 0) ? carry : from_left;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float dd = phi[r] - prev;
+        if (dd > kPiF) { dd -= k2PiF; wacc -= 1; }
+        else if (dd < -kPiF) { dd += k2PiF; wacc += 1; }
+        d[r] = dd;
+        prev = phi[r];
       }
-      // carry the last HA demod samples into the history slots of the next block
-      // (every lane has finished its window reads: LDS ops of one wave complete in order)
-      asm volatile("" ::: "memory");
-      if (q1 == 0)
-        for (int e = lane; e < HA; e += 64) dh[e] = 0.f;   // next block starts a new stream
-      else
-        for (int e = lane; e < HA; e += 64) dh[e] = dh[BD + e];
-      asm volatile("" ::: "memory");
+      if constexpr (!FUSED) {
+        typedef float f3v __attribute__((ext_vector_type(3)));
+        *reinterpret_cast<f3v*>(p.demod + (int64_t)s * p.out_stride + m0 + R * lane) = f3v{d[0], d[1], d[2]};
+        issued += 1;
+      }
+      carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[R - 1]), 63));
+    } else {
+      float si = 0.f, sq = 0.f;
+      if (m0 > 0 && !have) {
+        for (int k = lane; k < T; k += 64) {
+          const f2v x = buf[(T - 1) - k];
+          const float h = p.taps_dev[k];
+          si = fmaf(h, x.x, si);
+          sq = fmaf(h, x.y, sq);
+        }
+        si = wave_sum(si);
+        sq = wave_sum(sq);
+      }
+      bool one = false;
+      carry = fe_epilogue<T, D, R>(p, s, M, m0, lane, ai, aq, si, sq, have, carry, &one, d, !FUSED);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      issued = 0; mark1 = 0;
     }
-    // exactly-one-store accounting for the next wait (see fe_stream_kernel)
-    const bool full_audio = (i == TPB - 1) && (q * BO + BO <= A);
-    if (i == TPB - 1 && !full_audio) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int nst = (sp ? 1 : 0) + (full_audio ? 1 : 0);
-    if (nst == 2) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // keep at most one outstanding
-    store_pending = nst >= 1;
-    (void)ast;
 
+    stamp(3);
+    if constexpr (FUSED && MODE < 4) {
+      // demod -> history: sample m0 + 3 lane + r of block q sits at dh[HA + rel]
+      const int ib = i - TPB * (i / TPB);            // tile within its audio block (warm-up: 4)
+      const bool warm = (i + 1) % TPB == 0 && u == 0 && U % TPB == 1;
+      const int rel0 = (warm ? -TO : ib * TO) + R * lane;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (rel0 + r >= -HA) dh[HA + rel0 + r] = d[r];
+      if (!warm && ib == TPB - 1) {
+        asm volatile("" ::: "memory");
+        const int64_t q = i / TPB;
+        // lane window: dh[HA - (TA-1) + 15 lane + w], w = 0 .. NW-1
+        const float* aw = dh + (HA - (TA - 1) + DA * RA * lane);
+        // hand-pipelined like the FIR: per step k (samples 2k, 2k+1) one ds_read2_b32 of the
+        // lane's samples + two broadcast ds_read_b128 of tap triples, APF steps ahead
+        f2v acc01a = f2v{0.f, 0.f}, acc01b = f2v{0.f, 0.f};
+        float a2a = 0.f, a2b = 0.f;
+        constexpr int NS = (NW + 1) / 2, APF = 5;   // 3*APF <= 15 (lgkmcnt field)
+        f2v xq[NS];
+        f4v ta[NS], tb[NS];
+        auto rd = [&](auto K) {
+          constexpr int k = K;
+          xq[k] = lds_read2_b32<2 * k, 2 * k + 1>(aw);
+          ta[k] = lds_read_b128<32 * k>(ptab);
+          tb[k] = lds_read_b128<32 * k + 16>(ptab);
+        };
+        static_for<0, APF>(rd);
+        static_for<0, NS>([&](auto K) {
+          constexpr int k = K;
+          if constexpr (k + APF < NS) {
+            rd(std::integral_constant<int, k + APF>{});
+            lds_wait_ordered<3 * APF>();
+          } else {
+            lds_wait_ordered<3 * (NS - 1 - k)>();
+          }
+          pk_fma_bcast_x_ordered<false>(acc01a, f2v{ta[k].x, ta[k].y}, xq[k]);
+          pk_fma_bcast_x_ordered<true>(acc01b, f2v{tb[k].x, tb[k].y}, xq[k]);
+          fmac_ordered(a2a, ta[k].z, xq[k].x);
+          fmac_ordered(a2b, tb[k].z, xq[k].y);
+        });
+        const float o0 = acc01a.x + acc01b.x, o1 = acc01a.y + acc01b.y, o2 = a2a + a2b;
+        const int64_t A = (M + DA - 1) / DA;
+        const int64_t j = q * BO + RA * lane;
+        float* ao = a.audio + (int64_t)s * a.audio_stride + j;
+        if (q * BO + BO <= A) {
+          typedef float f3v __attribute__((ext_vector_type(3)));
+          *reinterpret_cast<f3v*>(ao) = f3v{o0, o1, o2};
+          issued += 1;
+        } else {
+          if (j < A) ao[0] = o0;
+          if (j + 1 < A) ao[1] = o1;
+          if (j + 2 < A) ao[2] = o2;
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          issued = 0; mark1 = 0;
+        }
+        asm volatile("" ::: "memory");
+        if (s1 != s)
+          for (int e = lane; e < HA; e += 64) dh[e] = 0.f;     // next block starts a new stream
+        else
+          for (int e = lane; e < HA; e += 64) dh[e] = dh[BD + e];
+        asm volatile("" ::: "memory");
+      }
+    }
+
+    stamp(4);
+    // ---- advance ----
+    if ((s1 != s || u + 1 == U) && p.wraps != nullptr) {
+      const int w = wave_sum_i(wacc);
+      if (lane == 0 && w != 0) atomicAdd(p.wraps + s, w);
+      wacc = 0;
+    }
     have = (s1 == s);
-    s = s1; q = q1; i = i1;
-    issued = next;
-    b = bn;
+    s = s1; i = i1; nl = nl1;
+    kind = kind1; mark = mark1;
+    b ^= 1;
+  }
+  if constexpr (MODE == 6) {
+    if (lane == 0) {
+      uint64_t* o = reinterpret_cast<uint64_t*>(p.q_ds) + 8 * blockIdx.x;
+      for (int k = 0; k < 5; ++k) o[k] = tph[k];
+      o[5] = U;
+    }
   }
 }
 
@@ -776,9 +910,17 @@ static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
   if constexpr (U8) {
     hipLaunchKernelGGL((fe_kernel<T, D, R, NT, true>), dim3((unsigned)tiles), dim3(NT), 0, st, p, *a.taps);
   } else {
-    static const int wpc = resident_per_cu(fe_stream_kernel<T, D, R, NB>, 64);
-    const int64_t grid = std::min<int64_t>(tiles, (int64_t)cu_count() * wpc);
-    hipLaunchKernelGGL((fe_stream_kernel<T, D, R, NB>), dim3((unsigned)grid), dim3(64), 0, st, p, *a.taps, tiles);
+    // fe_ring_kernel: 192 outputs per tile, one resident wave per SIMD
+    constexpr int TO3 = 192;
+    RingArgs ra{};
+    ra.tps = (int)((M + TO3 - 1) / TO3);
+    ra.total = (int64_t)ra.tps * a.nstreams;
+    static const int wpc = resident_per_cu(fe_ring_kernel<T>, 64);
+    const int64_t slots = (int64_t)cu_count() * std::min(wpc, 4);
+    ra.per_wave = (int)((ra.total + slots - 1) / slots);
+    const int64_t grid = (ra.total + ra.per_wave - 1) / ra.per_wave;
+    p.tiles_per_stream = ra.tps;
+    hipLaunchKernelGGL((fe_ring_kernel<T>), dim3((unsigned)grid), dim3(64), 0, st, p, *a.taps, ra);
   }
   return hipGetLastError();
 }
@@ -795,34 +937,39 @@ hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st) {
   }
 }
 
-template <int T, int TA>
+template <int T>
 static hipError_t launch_fe_mono_t(const FeLaunch& a, const float* ataps, float* audio,
                                    int64_t audio_stride, hipStream_t st) {
-  constexpr int D = 10, R = 2, NB = 2, DA = 5;
-  constexpr int BD = 64 * 2 * DA;                  // demod samples per audio block
+  constexpr int D = 10, BD = 960;                  // demod samples per audio block
   FeParams p{};
   p.iq = a.iq; p.n = a.n; p.stride = a.stride; p.hist = 0; p.nstreams = a.nstreams;
   p.taps_dev = a.taps_dev;
   const int64_t M = (a.n + D - 1) / D;
-  const int64_t blocks = (M + BD - 1) / BD * a.nstreams;
-  if (blocks <= 0) return hipSuccess;
-  static const int wpc = resident_per_cu(fe_mono_kernel<T, D, R, NB, TA, DA>, 64);
-  const int64_t grid = std::min<int64_t>(blocks, (int64_t)cu_count() * wpc);
-  hipLaunchKernelGGL((fe_mono_kernel<T, D, R, NB, TA, DA>), dim3((unsigned)grid), dim3(64), 0, st, p,
-                     *a.taps, ataps, audio, audio_stride, blocks);
+  RingArgs ra{};
+  ra.ab = (int)((M + BD - 1) / BD);
+  ra.tps = 5 * ra.ab;
+  ra.total = (int64_t)ra.ab * a.nstreams;
+  if (ra.total <= 0) return hipSuccess;
+  if (ra.total > 0x7fffffff / 5) return hipErrorInvalidValue;
+  ra.audio = audio; ra.audio_stride = audio_stride; ra.ataps = ataps;
+  static const int wpc = resident_per_cu(fe_ring_kernel<T, true>, 64);
+  const int64_t slots = (int64_t)cu_count() * std::min(wpc, 4);
+  ra.per_wave = (int)((ra.total + slots - 1) / slots);
+  const int64_t grid = (ra.total + ra.per_wave - 1) / ra.per_wave;
+  p.tiles_per_stream = ra.tps;
+  hipLaunchKernelGGL((fe_ring_kernel<T, true>), dim3((unsigned)grid), dim3(64), 0, st, p, *a.taps, ra);
   return hipGetLastError();
 }
 
 // Fused FE + mono audio filter over whole streams (zero initial state).  Supported: f32 IQ,
-// RF taps 101/151 at decim 10, audio taps 151 at decim 5 (model/fmMonoBlock.py:24-31);
-// anything else returns hipErrorInvalidValue and the C-ABI runs the two-kernel path.
+// RF taps 101 at decim 10, audio taps 151 at decim 5 (model/fmMonoBlock.py:24-31, BASELINE
+// configs); anything else returns hipErrorInvalidValue and the C-ABI runs the two-kernel path.
 hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
                               int64_t audio_stride, hipStream_t st) {
   if (a.D != 10 || a.u8 || TA != 151 || DA != 5) return hipErrorInvalidValue;
   switch (a.T) {
-    case 101: return launch_fe_mono_t<101, 151>(a, ataps, audio, audio_stride, st);
-    case 151: return launch_fe_mono_t<151, 151>(a, ataps, audio, audio_stride, st);
-    default: return hipErrorInvalidValue;
+    case 101: return launch_fe_mono_t<101>(a, ataps, audio, audio_stride, st);
+    default: return hipErrorInvalidValue;   // 151 RF taps: 3 waves/CU by LDS -> two-kernel path
   }
 }
 

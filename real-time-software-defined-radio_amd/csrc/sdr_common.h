@@ -36,14 +36,16 @@ struct TapsF2 {
 template <bool HI>
 __device__ __forceinline__ void pk_fma_bcast(f2v& acc, const f2v& tap2, const f2v& x) {
   if (HI)
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(tap2), "v"(x));
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(tap2), "v"(x));
   else
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(tap2), "v"(x));
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(tap2), "v"(x));
 }
 
 // acc += tap2 * {x, x} with x = the low (HI=false) or high (HI=true) half of x2: the
 // mirror of pk_fma_bcast, broadcasting the sample instead of the tap (two filters, or two
 // outputs of one filter, per sample).
+// Not volatile: its operands come from compiler-visible loads, so the compiler orders and
+// waits for them itself (a volatile asm would pin every load of the loop in place).
 template <bool HI>
 __device__ __forceinline__ void pk_fma_bcast_x(f2v& acc, const f2v& tap2, const f2v& x2) {
   if (HI)
@@ -63,6 +65,77 @@ __device__ __forceinline__ f4v lds_read_b128(const void* lds_base) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
   return v;
 }
+// ds_read2_b32 issued by hand: two dwords at dword offsets O0, O1 (< 256) from base.
+template <int O0, int O1>
+__device__ __forceinline__ f2v lds_read2_b32(const void* lds_base) {
+  static_assert(O0 >= 0 && O0 < 256 && O1 >= 0 && O1 < 256, "8-bit dword offsets");
+  f2v v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)lds_base;
+  asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(v) : "v"(a), "i"(O0), "i"(O1));
+  return v;
+}
+
+// ordered (volatile) scalar FMA for hand-pipelined loops: acc += a * b
+__device__ __forceinline__ void fmac_ordered(float& acc, float a, float b) {
+  asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "v"(a), "v"(b));
+}
+// ordered variant of pk_fma_bcast_x (for operands from hand-issued LDS reads)
+template <bool HI>
+__device__ __forceinline__ void pk_fma_bcast_x_ordered(f2v& acc, const f2v& tap2, const f2v& x2) {
+  if (HI)
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(tap2), "v"(x2));
+  else
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(tap2), "v"(x2));
+}
+
+// ds_write_b128 issued by hand (ordered with the hand-issued reads above).
+__device__ __forceinline__ void lds_write_b128(void* lds_base, const f4v& v) {
+  const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds_base;
+  asm volatile("ds_write_b128 %0, %1" : : "v"(a), "v"(v) : "memory");
+}
+
+// N consecutive 1-KiB chunks by 16-B-per-lane LDS-DMA in the saddr form: wave-uniform
+// global base in an SGPR pair + per-lane 32-bit byte offset; the immediate offset is
+// applied to BOTH the global and the LDS address (M0 = LDS byte address), so up to four
+// chunks share one M0 / base setup.  Non-temporal (nt): streamed once.
+// hipcc's builtin form materialises a 64-bit VGPR address and an SGPR pair per chunk.
+template <int N>
+__device__ __forceinline__ void glds16x(unsigned voff, const void* sbase, unsigned lds_addr) {
+  static_assert(N >= 1 && N <= 4, "1..4 chunks per M0 setup (13-bit immediate)");
+  // s_nop: M0 written by SALU needs one wait state before an LDS-DMA reads it
+  if constexpr (N == 1)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 offset:0 nt"
+                 :: "v"(voff), "s"(sbase), "s"(lds_addr) : "memory", "m0");
+  else if constexpr (N == 2)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 offset:0 nt\n\t"
+                 "global_load_lds_dwordx4 %0, %1 offset:1024 nt"
+                 :: "v"(voff), "s"(sbase), "s"(lds_addr) : "memory", "m0");
+  else if constexpr (N == 3)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 offset:0 nt\n\t"
+                 "global_load_lds_dwordx4 %0, %1 offset:1024 nt\n\tglobal_load_lds_dwordx4 %0, %1 offset:2048 nt"
+                 :: "v"(voff), "s"(sbase), "s"(lds_addr) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 offset:0 nt\n\t"
+                 "global_load_lds_dwordx4 %0, %1 offset:1024 nt\n\tglobal_load_lds_dwordx4 %0, %1 offset:2048 nt\n\t"
+                 "global_load_lds_dwordx4 %0, %1 offset:3072 nt"
+                 :: "v"(voff), "s"(sbase), "s"(lds_addr) : "memory", "m0");
+}
+__device__ __forceinline__ unsigned lds_addr_of(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (clamped to [0, 24]; waiting for more
+// than needed is always safe).  The steady-state counts are tested first.
+template <int I = 24>
+__device__ __forceinline__ void wait_vm_chain(int n) {
+  if constexpr (I == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (n >= I) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(I) : "memory");
+    else wait_vm_chain<I - 1>(n);
+  }
+}
+
 // compile-time loop: f(std::integral_constant<int, I>{}) for I in [B, E)
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -70,6 +143,14 @@ __device__ __forceinline__ void static_for(F&& f) {
     f(std::integral_constant<int, B>{});
     static_for<B + 1, E>(f);
   }
+}
+
+// Counted LDS wait without register operands: ordering with the consumers comes from
+// every consumer being a volatile asm (pk_fma_bcast*), so no asm "defines" the loaded
+// registers right before their first reader (which would cost an s_nop, see fe.hip).
+template <int N>
+__device__ __forceinline__ void lds_wait_ordered() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(N));
 }
 
 template <int N>

@@ -77,6 +77,58 @@ float time_fs(FeParams p, const TapsF32& taps, hipStream_t st, int iters, int wa
   return ms / iters;
 }
 
+template <int MODE>
+float time_ring(FeParams p, const TapsF32& taps, hipStream_t st, int iters, int waves_per_cu) {
+  const int64_t M = (p.n + 9) / 10;
+  RingArgs ra;
+  ra.tps = (int)((M + 191) / 192);
+  ra.total = (int64_t)ra.tps * p.nstreams;
+  const int64_t slots = 256LL * waves_per_cu;
+  ra.per_wave = (int)((ra.total + slots - 1) / slots);
+  const int grid = (int)((ra.total + ra.per_wave - 1) / ra.per_wave);
+  p.tiles_per_stream = ra.tps;
+  p.vec_out = 1;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i)
+    hipLaunchKernelGGL((fe_ring_kernel<101, false, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
+  CK(hipEventRecord(a, st));
+  for (int i = 0; i < iters; ++i)
+    hipLaunchKernelGGL((fe_ring_kernel<101, false, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
+  CK(hipEventRecord(b, st));
+  CK(hipEventSynchronize(b));
+  CK(hipGetLastError());
+  float ms; CK(hipEventElapsedTime(&ms, a, b));
+  return ms / iters;
+}
+
+template <int MODE>
+float time_ring_fused(FeParams p, const TapsF32& taps, const float* ataps, float* audio, hipStream_t st, int iters) {
+  const int64_t M = (p.n + 9) / 10;
+  RingArgs ra{};
+  ra.ab = (int)((M + 959) / 960);
+  ra.tps = 5 * ra.ab;
+  ra.total = (int64_t)ra.ab * p.nstreams;
+  ra.audio = audio; ra.audio_stride = (M + 4) / 5; ra.ataps = ataps;
+  const int64_t slots = 256LL * 4;
+  ra.per_wave = (int)((ra.total + slots - 1) / slots);
+  const int grid = (int)((ra.total + ra.per_wave - 1) / ra.per_wave);
+  p.tiles_per_stream = ra.tps;
+  p.demod = nullptr;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i)
+    hipLaunchKernelGGL((fe_ring_kernel<101, true, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
+  CK(hipEventRecord(a, st));
+  for (int i = 0; i < iters; ++i)
+    hipLaunchKernelGGL((fe_ring_kernel<101, true, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
+  CK(hipEventRecord(b, st));
+  CK(hipEventSynchronize(b));
+  CK(hipGetLastError());
+  float ms; CK(hipEventElapsedTime(&ms, a, b));
+  return ms / iters;
+}
+
 int main(int argc, char** argv) {
   const int64_t n = 64LL * 1024000;  // complex samples
   const int64_t M = n / 10;
@@ -129,6 +181,26 @@ int main(int argc, char** argv) {
     float t3 = time_fs<R, NB, 3>(p, taps, st, it, W); \
     printf("strm R=%d NB=%d w/cu=%d: full %8.2f us (%7.1f GB/s)  mem-only %8.2f us  compute-only %8.2f us  mem-no-epilogue %8.2f us\n", R, NB, W, t0 * 1e3, bytes / t0 / 1e6, t1 * 1e3, t2 * 1e3, t3 * 1e3); }
   RUNS(3, 2, 4, "s324") RUNS(2, 2, 7, "s227") RUNS(2, 2, 6, "s226") RUNS(3, 3, 3, "s333") RUNS(2, 3, 5, "s235") RUNS(1, 2, 12, "s1212")
+#define RUNR(W, tag) if (want(tag)) { \
+    float t0 = time_ring<0>(p, taps, st, it, W), t1 = time_ring<1>(p, taps, st, it, W), t2 = time_ring<2>(p, taps, st, it, W); \
+    printf("ring R=3 NB=2 w/cu=%d: full %8.2f us (%7.1f GB/s)  mem-only %8.2f us  compute-only %8.2f us\n", W, t0 * 1e3, bytes / t0 / 1e6, t1 * 1e3, t2 * 1e3); }
+  RUNR(4, "r4") RUNR(3, "r3") RUNR(2, "r2")
+  if (want("fused")) {
+    float* aud; CK(hipMalloc(&aud, (M / 5 + 64) * 4));
+    float t0 = time_ring_fused<0>(p, taps, tdev, aud, st, it), t1 = time_ring_fused<1>(p, taps, tdev, aud, st, it);
+    float t4 = time_ring_fused<4>(p, taps, tdev, aud, st, it), t5 = time_ring_fused<5>(p, taps, tdev, aud, st, it);
+    const double fb = n * 8.0 + (M / 5) * 4.0;
+    printf("ring fused FE+mono: full %8.2f us (%7.1f GB/s)  no-FIR %8.2f us  DMA+halo only %8.2f us  DMA(16 chunks) only %8.2f us\n",
+           t0 * 1e3, fb / t0 / 1e6, t1 * 1e3, t4 * 1e3, t5 * 1e3);
+    uint64_t* dbg; CK(hipMalloc(&dbg, 8 * 8 * 4096));
+    p.q_ds = reinterpret_cast<float*>(dbg);
+    float t6 = time_ring_fused<6>(p, taps, tdev, aud, st, 1);
+    std::vector<uint64_t> hd(8 * 4096); CK(hipMemcpy(hd.data(), dbg, 8 * 8 * 4096, hipMemcpyDeviceToHost));
+    double acc[6] = {0, 0, 0, 0, 0, 0}; int nw = 0;
+    for (int w = 0; w < 1024; ++w) { if (!hd[8 * w + 5]) continue; ++nw; for (int k = 0; k < 6; ++k) acc[k] += (double)hd[8 * w + k]; }
+    printf("instrumented %8.2f us; per wave-tile cycles: issue %.0f  wait/build %.0f  halo+FIR %.0f  epilogue %.0f  audio %.0f  (tiles/wave %.1f)\n",
+           t6 * 1e3, acc[0] / acc[5], acc[1] / acc[5], acc[2] / acc[5], acc[3] / acc[5], acc[4] / acc[5], acc[5] / nw);
+  }
   CK(hipDeviceSynchronize());
   return 0;
 }

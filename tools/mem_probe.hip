@@ -61,7 +61,7 @@ __global__ __launch_bounds__(64) void ring_glds(const float* __restrict__ in, in
   float acc8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int64_t u = 0; u < NB - 1 && u < mine; ++u) issue(u);
   for (int64_t u = 0; u < mine; ++u) {
-    constexpr int S = WR == 2 ? 2 : WR == 3 ? 1 : WR == 4 ? 2 : (WR >= 6 && WR <= 8) ? 1 : 0;   // stores per tile (exact)
+    constexpr int S = WR == 2 ? 2 : (WR == 3 || WR == 9) ? 1 : WR == 4 ? 2 : (WR >= 6 && WR <= 8) ? 1 : 0;   // stores per tile (exact)
     if (u + NB - 1 < mine) {
       issue(u + NB - 1);
       if (u > 0 && S > 0 && WR != 5) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL * (NB - 1) + S) : "memory");
@@ -73,6 +73,8 @@ __global__ __launch_bounds__(64) void ring_glds(const float* __restrict__ in, in
     if (WR == 2) {
 #pragma unroll
       for (int w = 0; w < WR; ++w) out[(tile(u) * 64 + lane) * WR + w] = acc;
+    } else if (WR == 9) {          // one float2 store per lane, always to the wave's own 512 B (L2-resident)
+      reinterpret_cast<float2*>(out)[blockIdx.x * 64 + lane] = make_float2(acc, acc + 1.f);
     } else if (WR == 3) {          // one float2 store per lane
       reinterpret_cast<float2*>(out)[tile(u) * 64 + lane] = make_float2(acc, acc + 1.f);
     } else if (WR == 4) {          // one nontemporal float2 store per lane
@@ -139,5 +141,7 @@ int main(int argc, char** argv) {
   RING3(11, 2, 7, true, 2560, 0, 2) RING3(11, 2, 7, true, 2560, 3, 2)
   RING3(11, 2, 7, true, 2560, 6, 2) RING3(11, 2, 7, true, 2560, 7, 2) RING3(11, 2, 7, true, 2560, 8, 2)
   RING3(11, 2, 7, false, 2560, 6, 2) RING3(11, 2, 7, true, 2560, 6, 0)
+  RING3(16, 2, 4, true, 3840, 0, 2) RING3(16, 2, 4, true, 3840, 3, 2) RING3(16, 2, 4, true, 3840, 9, 2)
+  RING3(16, 2, 4, true, 3840, 5, 2) RING3(11, 2, 7, true, 2560, 9, 2) RING3(11, 2, 7, true, 2560, 5, 2)
   return 0;
 }
