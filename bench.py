@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--taps", type=int, default=101)
     ap.add_argument("--audio-taps", type=int, default=151)
     ap.add_argument("--iq", choices=["f32", "u8"], default="f32")
-    ap.add_argument("--path", choices=["fused", "split"], default="split",
+    ap.add_argument("--path", choices=["fused", "split"], default="fused",
                     help="fused: one fe_mono_kernel (demod stays on chip); split: FE kernel + FIR kernel")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-samples", type=int, default=4_096_000, help="complex samples per CPU stream")
@@ -199,7 +199,11 @@ def main():
     # the fused kernel covers f32 IQ; u8 IQ runs the FE + FIR pair inside sdr_fe_mono_dev
     stages = [fused] if args.path == "fused" else [fe, mono]
     tm = _lib.Timer(ctx)
-    ev = [[tm.event() for _ in range(len(stages) + 1)] for _ in range(args.steps)]
+    # fused: one kernel per step -> one event pair around the whole timed region (per-step
+    # events would add ~10 us of event processing between launches); split: events
+    # between the two kernels of every step to separate them
+    per_step = len(stages) > 1
+    ev = [[tm.event() for _ in range(len(stages) + 1)] for _ in range(args.steps if per_step else 1)]
     for _ in range(args.warmup):
         for f in stages:
             f()
@@ -207,26 +211,35 @@ def main():
     barrier(ws)
     ctx.synchronize()
     t0 = time.perf_counter()
-    for e in ev:
-        tm.record(e[0])
-        for k, f in enumerate(stages):
-            f()
-            tm.record(e[k + 1])
+    if per_step:
+        for e in ev:
+            tm.record(e[0])
+            for k, f in enumerate(stages):
+                f()
+                tm.record(e[k + 1])
+    else:
+        tm.record(ev[0][0])
+        for _ in range(args.steps):
+            stages[0]()
+        tm.record(ev[0][1])
     t_enq = time.perf_counter() - t0                 # host enqueue time (async launches)
     ctx.synchronize()
     barrier(ws)
     elapsed = max_over_ranks(ws, time.perf_counter() - t0)
-    stage_ms = [float(np.mean([tm.elapsed_ms(e[k], e[k + 1]) for e in ev])) for k in range(len(stages))]
+    if per_step:
+        stage_ms = [float(np.mean([tm.elapsed_ms(e[k], e[k + 1]) for e in ev])) for k in range(len(stages))]
+    else:
+        stage_ms = [tm.elapsed_ms(ev[0][0], ev[0][1]) / args.steps]
     k_avg = stage_ms[0]                              # the dominant (first) kernel of the step
     bpc = 2 if args.iq == "u8" else 8
     if args.path == "fused":
         # compulsory HBM bytes of the fused kernel: IQ in + audio out
         k_bytes = n * bpc + A * 4
-        kname = f"fe_mono_kernel<{args.taps},10,{args.audio_taps},5> (sdr_fe_mono_dev)"
+        kname = f"fe_ring_kernel<{args.taps},fused> (sdr_fe_mono_dev: FE {args.taps} taps + audio {args.audio_taps} taps)"
         kernels = {"fe_mono": round(k_avg, 5)}
     else:
         k_bytes = n * bpc + M * 4                    # IQ in + demod out
-        kname = f"fe_stream_kernel<{args.taps},10> (sdr_rf_frontend_dev)"
+        kname = f"fe_ring_kernel<{args.taps}> (sdr_rf_frontend_dev)"
         mono_bytes = M * 4 + A * 4
         kernels = {"fe": round(k_avg, 5), "mono": round(stage_ms[1], 5),
                    "mono_gbs": round(mono_bytes / (stage_ms[1] * 1e-3) / 1e9, 1)}

@@ -28,6 +28,8 @@
 #include "sdr_common.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 namespace {
 
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(NT) void fe_kernel(FeParams p, TapsF32 taps) {
 
 // Register-blocked FIR of one tile image (see fe_stream_kernel): lane l produces the R
 // decimated (I, Q) outputs of its window [D R l + D + DELTA, + D(R-1)+T).
-template <int T, int D, int R, int MODE>
+template <int T, int D, int R, int MODE, int PF = 8>
 __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v (&tp)[(T + 1) / 2],
                                             float (&ai)[R], float (&aq)[R]) {
   constexpr int DELTA = (2 - ((D + T - 1) % 2)) % 2;
@@ -326,31 +328,33 @@ __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v 
   const f2v* win = buf + (D * R * lane + D + DELTA);
   const float4* win4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(win, 16));
   // two accumulator pairs per output (even / odd taps): 2R independent FMA chains per wave
-  f2v acc[R], acc2[R];
+  // (R == 1: two more, by tap index mod 4, so a lone wave is not latency-bound)
+  constexpr int NA = (R == 1) ? 2 : 1;
+  f2v acc[R * NA], acc2[R * NA];
 #pragma unroll
-  for (int r = 0; r < R; ++r) { acc[r] = f2v{0.f, 0.f}; acc2[r] = f2v{0.f, 0.f}; }
+  for (int r = 0; r < R * NA; ++r) { acc[r] = f2v{0.f, 0.f}; acc2[r] = f2v{0.f, 0.f}; }
   if (MODE == 1 || MODE == 3) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = win[r];
+    for (int r = 0; r < R; ++r) acc[r * NA] = win[r];
   } else {
     // one ds_read_b128 per sample pair (the lane window starts 16-B aligned), issued by
     // hand PF pairs ahead of use with counted lgkmcnt waits: hipcc would split the 16-B
     // read into ds_read2_b64 (4-8-way bank conflicts at this lane stride) and read only
     // one pair ahead (the LDS latency then stalls the wave).
     constexpr int NP = (NI + 1) / 2;
-    constexpr int PF = 8;
+    static_assert(PF >= 1 && PF <= 15, "lgkmcnt field");
     f4v qb[NP];
     static_for<0, (PF < NP ? PF : NP)>([&](auto I) { qb[I] = lds_read_b128<16 * I>(win4); });
     static_for<0, NP>([&](auto I) {
       constexpr int ip = I;
-      // the wait is an operand-free volatile asm ordered with the (volatile) FMAs; an asm
-      // "defining" qb[ip] right before its first reader costs an s_nop per step (hipcc's
-      // gfx950 dst-forwarding hazard rule, applied conservatively to inline asm)
+      // the wait "redefines" qb[ip] ("+v"): the register allocator may then not copy or
+      // spill the in-flight value before the data has arrived (it costs one s_nop per
+      // step: hipcc's gfx950 dst-forwarding hazard rule, applied conservatively to asm)
       if constexpr (ip + PF < NP) {
         qb[ip + PF] = lds_read_b128<16 * (ip + PF)>(win4);
-        lds_wait_ordered<PF>();
+        lds_wait<PF>(qb[ip]);
       } else {
-        lds_wait_ordered<NP - 1 - ip>();
+        lds_wait<NP - 1 - ip>(qb[ip]);
       }
       const f4v q = qb[ip];
 #pragma unroll
@@ -362,17 +366,21 @@ __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v 
         for (int r = 0; r < R; ++r) {
           const int k = D * r + T - 1 - i;
           if (k >= 0 && k < T) {
-            if (k & 1) pk_fma_bcast<true>(acc2[r], tp[k >> 1], x);
-            else pk_fma_bcast<false>(acc[r], tp[k >> 1], x);
+            const int a = (NA == 2) ? r * NA + ((k >> 1) & 1) : r;
+            if (k & 1) pk_fma_bcast<true>(acc2[a], tp[k >> 1], x);
+            else pk_fma_bcast<false>(acc[a], tp[k >> 1], x);
           }
         }
       }
     });
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] += acc2[r];
-#pragma unroll
-  for (int r = 0; r < R; ++r) { ai[r] = acc[r].x; aq[r] = acc[r].y; }
+  for (int r = 0; r < R; ++r) {
+    f2v t = acc[r * NA] + acc2[r * NA];
+    if constexpr (NA == 2) t += acc[r * NA + 1] + acc2[r * NA + 1];
+    ai[r] = t.x;
+    aq[r] = t.y;
+  }
 
 }
 
@@ -522,6 +530,9 @@ void fe_stream_kernel(FeParams p, TapsF32 taps, int64_t total_tiles) {
 //    tiles, zi, i_ds/q_ds and last_phi go through the general fe_epilogue;
 //  * 4 resident waves per CU = one per SIMD (LDS: 2 x 16 KiB ring per wave).
 // ---------------------------------------------------------------------------------
+#ifndef RING_PF
+#define RING_PF 12
+#endif
 struct RingArgs {
   int64_t total;       // work units: tiles (FE), or audio blocks (FUSED), over all streams
   int per_wave;        // units per wave (contiguous run)
@@ -638,117 +649,17 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
       tlast = t;
     }
   };
-  stamp(-1);
-  for (int u = 0; u < U; ++u) {
-    // ---- next tile: position, kind, issue ----
-    int s1 = s, i1 = i + 1;
-    if (i1 == a.tps) { i1 = 0; ++s1; }
-    const int64_t nl1 = (s1 == s) ? nl + D * TO : n_lo_of(0);
-    int kind1 = 0, mark1 = 0;
-    if (u + 1 < U) {
-      if (s1 == s && MODE != 2 && MODE != 5 && nl1 + L <= p.n && nl1 + HCH * 128 >= -p.hist) kind1 = 3;
-      else kind1 = interior(nl1) ? 2 : 1;
-      if (kind1 >= 2) {
-        issue(s1, nl1, b ^ 1, kind1 == 2);
-        issued += (kind1 == 2) ? NCH : NEWC;
-        mark1 = issued;
-      }
-    }
-    f2v* buf = &ring[b][0];
-    const int64_t m0 = (int64_t)TO * i;
-    stamp(0);
-    // ---- this tile's image ----
-    if (kind >= 2) {
-      const int nw = issued - mark;                  // VMEM ops issued after this tile's loads
-      if (nw == NEWC) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC) : "memory");
-      else if (nw == NEWC + 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC + 1) : "memory");
-      else wait_vm_chain(nw);
-    } else {
-      const float* base = iqf + 2 * ((int64_t)s * p.stride);
-      for (int e = lane; e < L; e += 64) {
-        const int64_t nn = nl + e;
-        f2v x = f2v{0.f, 0.f};
-        if (MODE == 2) x = f2v{(float)e * 1e-4f, (float)lane};
-        else if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
-        buf[e] = x;
-      }
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      issued = 0; mark1 = 0;
-    }
-    stamp(1);
-    // halo of the next tile: read now, written after the FIR (all reads then returned)
-    f4v h0, h1;
-    if (kind1 == 3) {
-      h0 = lds_read_b128<0>(buf + NEWC * 128 + 2 * lane);
-      if constexpr (HCH == 2) h1 = lds_read_b128<0>(buf + (NEWC + 1) * 128 + 2 * lane);
-    }
-
-    float ai[R], aq[R];
-    fe_fir_tile<T, D, R, (MODE == 1 || MODE >= 4) ? 1 : 0>(buf, lane, tp, ai, aq);
-
-    if (kind1 == 3) {
-      lds_wait<0>(h0);
-      f2v* nb = &ring[b ^ 1][0];
-      lds_write_b128(nb + 2 * lane, h0);
-      if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(nb + 128 + 2 * lane, h1); }
-    }
-
-    stamp(2);
-    // ---- epilogue ----
-    float d[R];
-    const bool fast = i >= 1 && m0 + TO < M && p.i_ds == nullptr && have;
-    if (MODE >= 4) {          // tuning: memory pipeline only
-      carry += ai[0] + aq[0];
-      d[0] = d[1] = d[2] = carry;
-    } else if (fast) {
-      float phi[R];
+  // FUSED: demod values of tile (i) -> history; after the block's last tile, the block's
+  // audio outputs (lane l: 3l..3l+2) and the history shift.  `next_same`: the following
+  // tile continues this stream.
+  auto fused_tail = [&](int i, bool warm, const float (&d)[R], bool next_same) -> bool {
+    bool drained = false;
+    const int ib = i - TPB * (i / TPB);            // tile within its audio block (warm-up: 4)
+    const int rel0 = (warm ? -TO : ib * TO) + R * lane;
 #pragma unroll
-      for (int r = 0; r < R; ++r) phi[r] = fast_atan2f(aq[r], ai[r]);
-      const float from_left = __int_as_float(__builtin_amdgcn_update_dpp(
-          0, __float_as_int(phi[R - 1]), 0x138 /*wave_shr:1*/, 0xf, 0xf, false));
-      float prev = (lane == 0) ? carry : from_left;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        float dd = phi[r] - prev;
-        if (dd > kPiF) { dd -= k2PiF; wacc -= 1; }
-        else if (dd < -kPiF) { dd += k2PiF; wacc += 1; }
-        d[r] = dd;
-        prev = phi[r];
-      }
-      if constexpr (!FUSED) {
-        typedef float f3v __attribute__((ext_vector_type(3)));
-        *reinterpret_cast<f3v*>(p.demod + (int64_t)s * p.out_stride + m0 + R * lane) = f3v{d[0], d[1], d[2]};
-        issued += 1;
-      }
-      carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[R - 1]), 63));
-    } else {
-      float si = 0.f, sq = 0.f;
-      if (m0 > 0 && !have) {
-        for (int k = lane; k < T; k += 64) {
-          const f2v x = buf[(T - 1) - k];
-          const float h = p.taps_dev[k];
-          si = fmaf(h, x.x, si);
-          sq = fmaf(h, x.y, sq);
-        }
-        si = wave_sum(si);
-        sq = wave_sum(sq);
-      }
-      bool one = false;
-      carry = fe_epilogue<T, D, R>(p, s, M, m0, lane, ai, aq, si, sq, have, carry, &one, d, !FUSED);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      issued = 0; mark1 = 0;
-    }
-
-    stamp(3);
-    if constexpr (FUSED && MODE < 4) {
-      // demod -> history: sample m0 + 3 lane + r of block q sits at dh[HA + rel]
-      const int ib = i - TPB * (i / TPB);            // tile within its audio block (warm-up: 4)
-      const bool warm = (i + 1) % TPB == 0 && u == 0 && U % TPB == 1;
-      const int rel0 = (warm ? -TO : ib * TO) + R * lane;
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (rel0 + r >= -HA) dh[HA + rel0 + r] = d[r];
-      if (!warm && ib == TPB - 1) {
+    for (int r = 0; r < R; ++r)
+      if (rel0 + r >= -HA) dh[HA + rel0 + r] = d[r];
+    if (!warm && ib == TPB - 1) {
         asm volatile("" ::: "memory");
         const int64_t q = i / TPB;
         // lane window: dh[HA - (TA-1) + 15 lane + w], w = 0 .. NW-1
@@ -771,9 +682,9 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
           constexpr int k = K;
           if constexpr (k + APF < NS) {
             rd(std::integral_constant<int, k + APF>{});
-            lds_wait_ordered<3 * APF>();
+            lds_wait3<3 * APF>(xq[k], ta[k], tb[k]);
           } else {
-            lds_wait_ordered<3 * (NS - 1 - k)>();
+            lds_wait3<3 * (NS - 1 - k)>(xq[k], ta[k], tb[k]);
           }
           pk_fma_bcast_x_ordered<false>(acc01a, f2v{ta[k].x, ta[k].y}, xq[k]);
           pk_fma_bcast_x_ordered<true>(acc01b, f2v{tb[k].x, tb[k].y}, xq[k]);
@@ -793,15 +704,185 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
           if (j + 1 < A) ao[1] = o1;
           if (j + 2 < A) ao[2] = o2;
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          issued = 0; mark1 = 0;
+          issued = 0;
+          drained = true;
         }
         asm volatile("" ::: "memory");
-        if (s1 != s)
+        if (!next_same)
           for (int e = lane; e < HA; e += 64) dh[e] = 0.f;     // next block starts a new stream
         else
           for (int e = lane; e < HA; e += 64) dh[e] = dh[BD + e];
         asm volatile("" ::: "memory");
+    }
+    return drained;
+  };
+  // fast epilogue of an interior tile: phases, predecessor (DPP / carry), np.unwrap wrap
+  auto fast_epi = [&](const float (&ai)[R], const float (&aq)[R], float (&d)[R]) {
+    float phi[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) phi[r] = fast_atan2f(aq[r], ai[r]);
+    const float from_left = __int_as_float(__builtin_amdgcn_update_dpp(
+        0, __float_as_int(phi[R - 1]), 0x138 /*wave_shr:1*/, 0xf, 0xf, false));
+    float prev = (lane == 0) ? carry : from_left;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float dd = phi[r] - prev;
+      if (dd > kPiF) { dd -= k2PiF; wacc -= 1; }
+      else if (dd < -kPiF) { dd += k2PiF; wacc += 1; }
+      d[r] = dd;
+      prev = phi[r];
+    }
+    carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[R - 1]), 63));
+  };
+  auto wait_tile = [&](int nw) {                   // VMEM ops issued after the tile's loads
+    if (nw == NEWC) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC) : "memory");
+    else if (nw == NEWC + 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC + 1) : "memory");
+    else wait_vm_chain(nw);
+  };
+  // tile-index limits of the steady (fast) path, per stream: image interior (DMA) and
+  // fast epilogue (full tile strictly before the last output)
+  const int64_t j_int = (p.n + D + (T - 1) - L) / (D * TO);
+  const int64_t j_fast = M >= TO + 1 ? (M - TO - 1) / TO : -1;
+  stamp(-1);
+  for (int u = 0; u < U; ++u) {
+    if constexpr (MODE == 0) {
+      // ---- steady run: consecutive interior tiles of one stream, fixed VMEM pattern ----
+      if (kind >= 2 && have && i >= 1 && p.i_ds == nullptr) {
+        int64_t K = min<int64_t>(U - 1 - u, a.tps - 1 - i);
+        K = min<int64_t>(K, j_int - i);
+        K = min<int64_t>(K, j_fast - i + 1);
+        if (K > 0) {
+          const char* gn = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s * p.stride + nl + D * TO)) + 1024 * HCH;
+          float* outp = FUSED ? nullptr : p.demod + (int64_t)s * p.out_stride + (int64_t)TO * i + R * lane;
+          for (int k = 0; k < (int)K; ++k) {
+            // issue the next tile's new chunks into the other slot
+            {
+              const unsigned lb = lds_addr_of(&ring[b ^ 1][0]) + 1024 * HCH;
+              static_for<0, (NEWC + 3) / 4>([&](auto Q) {
+                constexpr int c = 4 * Q;
+                constexpr int n = (NEWC - c) < 4 ? (NEWC - c) : 4;
+                glds16x<n>(voff, gn + 1024 * c, lb + 1024 * c);
+              });
+              gn += D * TO * 8;
+            }
+            issued += NEWC;
+            const int mark1 = issued;
+            wait_tile(issued - mark);
+            f2v* buf = &ring[b][0];
+            f4v h0 = lds_read_b128<0>(buf + NEWC * 128 + 2 * lane), h1;
+            if constexpr (HCH == 2) h1 = lds_read_b128<0>(buf + (NEWC + 1) * 128 + 2 * lane);
+            float ai[R], aq[R];
+            fe_fir_tile<T, D, R, 0, (T > 127 ? 8 : RING_PF)>(buf, lane, tp, ai, aq);
+            lds_wait<0>(h0);
+            lds_write_b128(&ring[b ^ 1][0] + 2 * lane, h0);
+            if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(&ring[b ^ 1][0] + 128 + 2 * lane, h1); }
+            float d[R];
+            fast_epi(ai, aq, d);
+            if constexpr (!FUSED) {
+              typedef float f3v __attribute__((ext_vector_type(3)));
+              *reinterpret_cast<f3v*>(outp) = f3v{d[0], d[1], d[2]};
+              outp += TO;
+              issued += 1;
+            } else {
+              if (fused_tail(i, false, d, true)) { mark = 0; b ^= 1; ++i; nl += D * TO; continue; }
+            }
+            mark = mark1;
+            b ^= 1;
+            ++i;
+            nl += D * TO;
+          }
+          u += (int)K;
+          kind = 3;
+          // (tile u now has its halo DMA issued; have stays true, s unchanged)
+        }
       }
+    }
+    // ---- next tile: position, kind, issue ----
+    int s1 = s, i1 = i + 1;
+    if (i1 == a.tps) { i1 = 0; ++s1; }
+    const int64_t nl1 = (s1 == s) ? nl + D * TO : n_lo_of(0);
+    int kind1 = 0, mark1 = 0;
+    if (u + 1 < U) {
+      if (s1 == s && MODE != 2 && MODE != 5 && nl1 + L <= p.n && nl1 + HCH * 128 >= -p.hist) kind1 = 3;
+      else kind1 = interior(nl1) ? 2 : 1;
+      if (kind1 >= 2) {
+        issue(s1, nl1, b ^ 1, kind1 == 2);
+        issued += (kind1 == 2) ? NCH : NEWC;
+        mark1 = issued;
+      }
+    }
+    f2v* buf = &ring[b][0];
+    const int64_t m0 = (int64_t)TO * i;
+    stamp(0);
+    // ---- this tile's image ----
+    if (kind >= 2) {
+      wait_tile(issued - mark);
+    } else {
+      const float* base = iqf + 2 * ((int64_t)s * p.stride);
+      for (int e = lane; e < L; e += 64) {
+        const int64_t nn = nl + e;
+        f2v x = f2v{0.f, 0.f};
+        if (MODE == 2) x = f2v{(float)e * 1e-4f, (float)lane};
+        else if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
+        buf[e] = x;
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      issued = 0; mark1 = 0;
+    }
+    stamp(1);
+    // halo of the next tile: read now, written after the FIR (all reads then returned)
+    f4v h0, h1;
+    if (kind1 == 3) {
+      h0 = lds_read_b128<0>(buf + NEWC * 128 + 2 * lane);
+      if constexpr (HCH == 2) h1 = lds_read_b128<0>(buf + (NEWC + 1) * 128 + 2 * lane);
+    }
+
+    float ai[R], aq[R];
+    fe_fir_tile<T, D, R, (MODE == 1 || MODE == 4 || MODE == 5) ? 1 : 0, (T > 127 ? 8 : RING_PF)>(buf, lane, tp, ai, aq);
+
+    if (kind1 == 3) {
+      lds_wait<0>(h0);
+      f2v* nb = &ring[b ^ 1][0];
+      lds_write_b128(nb + 2 * lane, h0);
+      if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(nb + 128 + 2 * lane, h1); }
+    }
+
+    stamp(2);
+    // ---- epilogue ----
+    float d[R];
+    const bool fast = i >= 1 && m0 + TO < M && p.i_ds == nullptr && have;
+    if (MODE == 4 || MODE == 5) {          // tuning: memory pipeline only
+      carry += ai[0] + aq[0];
+      d[0] = d[1] = d[2] = carry;
+    } else if (fast) {
+      fast_epi(ai, aq, d);
+      if constexpr (!FUSED) {
+        typedef float f3v __attribute__((ext_vector_type(3)));
+        *reinterpret_cast<f3v*>(p.demod + (int64_t)s * p.out_stride + m0 + R * lane) = f3v{d[0], d[1], d[2]};
+        issued += 1;
+      }
+    } else {
+      float si = 0.f, sq = 0.f;
+      if (m0 > 0 && !have) {
+        for (int k = lane; k < T; k += 64) {
+          const f2v x = buf[(T - 1) - k];
+          const float h = p.taps_dev[k];
+          si = fmaf(h, x.x, si);
+          sq = fmaf(h, x.y, sq);
+        }
+        si = wave_sum(si);
+        sq = wave_sum(sq);
+      }
+      bool one = false;
+      carry = fe_epilogue<T, D, R>(p, s, M, m0, lane, ai, aq, si, sq, have, carry, &one, d, !FUSED);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      issued = 0; mark1 = 0;
+    }
+
+    stamp(3);
+    if constexpr (FUSED && (MODE < 4 || MODE == 6)) {
+      const bool warm = (i + 1) % TPB == 0 && u == 0 && U % TPB == 1;
+      if (fused_tail(i, warm, d, s1 == s)) mark1 = 0;
     }
 
     stamp(4);
@@ -822,6 +903,286 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
       for (int k = 0; k < 5; ++k) o[k] = tph[k];
       o[5] = U;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// fe_circ_kernel: sub-tile FE with a circular per-wave chunk ring (deep prefetch).
+//
+// r01 measurements of fe_ring_kernel (one wave per SIMD, 2-slot ring): the per-tile
+// compute (~2.2-3 us) is about the loaded memory latency of the next tile (~2.2 us), so
+// a wave with ONE tile in flight exposes part of its compute.  Here a wave walks
+// sub-tiles of 64 outputs (R = 1, lane l -> output m0 + l, lane stride 10 samples =
+// 5 x 16 B: conflict-free ds_read_b128) through a circular ring of C = 30 one-KiB chunks
+// (+ HCH mirror chunks): sub-tile g occupies chunks [5g, 5g + NCH) at ring positions
+// 5g mod C .. (a sub-tile starting at position C-5 reads its last HCH chunks from the
+// mirror positions C..C+HCH-1).  Consecutive sub-tiles share their halo chunks in place
+// (no copies), and P = 4 sub-tiles (20 KiB) stay in flight behind the one being
+// filtered, so the latency is covered by 4 sub-tiles of compute.
+//   * new chunks of sub-tile g: [5g + NCH - 5, 5g + NCH) at position (5g mod C) + k
+//     (k = NCH-5..NCH-1; >= C means the mirror position);
+//   * a sub-tile starting at position 0 also gets its first HCH chunks DMA'd to
+//     positions [0, HCH) (the previous sub-tile holds them at the mirror positions);
+//   * the first sub-tile of a run, and one after a stream change, load all NCH chunks;
+//     head/tail sub-tiles (outside [-hist, n)) are built with plain loads instead.
+// FUSED: audio block = 5 sub-tiles = 320 demod samples = 64 audio outputs (one per
+// lane); a run starting mid-stream runs 3 warm-up sub-tiles (192 >= 150 samples).
+// ---------------------------------------------------------------------------------
+template <int T, bool FUSED = false, int MODE = 0>
+__global__ __launch_bounds__(64)
+void fe_circ_kernel(FeParams p, TapsF32 taps, RingArgs a) {
+  constexpr int D = 10, TO = 64;
+  constexpr int NCH = (D * TO + T + 1 + 127) / 128;  // chunks per sub-tile image (6 at T=101)
+  constexpr int HCH = NCH - 5;                       // halo chunks shared with the next sub-tile
+  constexpr int C = 30;                              // ring positions (6 sub-tile starts)
+  constexpr int P = 4;                               // sub-tiles in flight ahead
+  constexpr int L = NCH * 128;
+  constexpr int TP = (T + 1) / 2;
+  static_assert((T & 1) == 1 && HCH >= 1 && HCH <= 2, "odd tap counts 101..235");
+  static_assert(5 * P + NCH <= C, "ring must hold the computing sub-tile and P ahead");
+  constexpr int TA = 151, DA = 5;
+  constexpr int BD = TO * DA;                        // 320 demod samples per audio block
+  constexpr int HA = 152;                            // history slots (>= TA-1)
+  constexpr int NPA = (TA + 1) / 2;                  // 76 audio sample pairs per lane
+  constexpr int WU = (TA - 1 + TO - 1) / TO;         // 3 warm-up sub-tiles
+
+  constexpr int RING = C + HCH;                      // chunks incl. mirrors
+  constexpr int RINGP = FUSED ? RING * 128 : (RING * 128 > 5120 ? RING * 128 : 5120);  // >= 40 KiB: 4 waves/CU
+  __shared__ __attribute__((aligned(16))) f2v ring[RINGP];
+  __shared__ __attribute__((aligned(16))) float dh[FUSED ? HA + BD + 8 : 1];
+  __shared__ __attribute__((aligned(16))) f2v ptab[FUSED ? NPA + 1 : 1];
+
+  const int lane = threadIdx.x;
+  const int64_t u0 = (int64_t)blockIdx.x * a.per_wave;
+  if (u0 >= a.total) return;
+  const int nunits = (int)min<int64_t>(a.per_wave, a.total - u0);
+  const int64_t M = (p.n + D - 1) / D;
+
+  f2v tp[TP];
+#pragma unroll
+  for (int j = 0; j < TP; ++j) tp[j] = f2v{taps.h[2 * j], (2 * j + 1 < T) ? taps.h[2 * j + 1] : 0.f};
+#pragma unroll
+  for (int j = 0; j < TP; ++j) asm volatile("" : "+v"(tp[j]));
+
+  const unsigned voff = 16u * lane;
+  const float* iqf = reinterpret_cast<const float*>(p.iq);
+  const unsigned ring_lds = lds_addr_of(&ring[0]);
+  auto n_lo_of = [&](int i) { return (int64_t)(D * TO) * i - D - (T - 1); };
+
+  // sub-tile sequence of this wave: (stream s, index i in stream), U sub-tiles
+  int s0, i0, U;
+  if constexpr (FUSED) {
+    s0 = (int)(u0 / a.ab);
+    const int q0 = (int)(u0 - (int64_t)s0 * a.ab);
+    i0 = DA * q0 - (q0 > 0 ? WU : 0);
+    U = nunits * DA + (q0 > 0 ? WU : 0);
+    if (q0 == 0)
+      for (int e = lane; e < HA; e += 64) dh[e] = 0.f;
+    for (int e = lane; e < 8; e += 64) dh[HA + BD + e] = 0.f;
+    for (int k = lane; k <= NPA; k += 64) {
+      const int k0 = (TA - 1) - 2 * k, k1 = k0 - 1;
+      ptab[k] = f2v{(k0 >= 0 && k < NPA) ? a.ataps[k0] : 0.f, (k1 >= 0 && k < NPA) ? a.ataps[k1] : 0.f};
+    }
+  } else {
+    s0 = (int)(u0 / a.tps);
+    i0 = (int)(u0 - (int64_t)s0 * a.tps);
+    U = nunits;
+  }
+
+  // issue state (sub-tile sequence number v relative to the run; g = absolute chunk
+  // base 5*v counted from the run start; ring position of sub-tile v = (5 v) mod C)
+  int is = s0, ii = i0;          // stream / index of the next sub-tile to issue
+  int64_t inl = n_lo_of(i0);
+  int issued = 0;
+  int mk[P + 1];                 // issue marks of sub-tiles v .. v+P (rotating)
+  int kd[P + 1];                 // kinds: 0 none, 1 guarded, 2 DMA (image complete after wait)
+#pragma unroll
+  for (int k = 0; k <= P; ++k) { mk[k] = 0; kd[k] = 0; }
+  bool prev_valid = false;       // previous issued sub-tile was in the same stream
+  auto issue_next = [&](int v, int slot) {
+    // v: sequence number of the sub-tile being issued; slot: index into mk/kd
+    const int pos = (5 * v) % C;
+    const bool full = !prev_valid;
+    const int64_t lo = full ? inl : inl + 128 * (NCH - 5);
+    const bool dma = MODE != 2 && inl >= -p.hist && inl + L <= p.n;
+    (void)lo;
+    if (dma) {
+      const char* g = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)is * p.stride + inl));
+      auto chunk = [&](int k, int at) {       // chunk k of this image -> ring position `at`
+        glds16x<1>(voff, g + 1024 * k, ring_lds + 1024u * at);
+      };
+      if (full) {
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) chunk(k, pos + k);
+        issued += NCH;
+      } else {
+#pragma unroll
+        for (int k = NCH - 5; k < NCH; ++k) chunk(k, pos + k);
+        issued += 5;
+      }
+      if (pos == 0 && !full) {                // halo chunks also at [0, HCH)
+#pragma unroll
+        for (int k = 0; k < HCH; ++k) chunk(k, k);
+        issued += HCH;
+      }
+      kd[slot] = 2;
+    } else {
+      kd[slot] = 1;
+    }
+    mk[slot] = issued;
+    prev_valid = true;
+    // advance the issue pointer
+    if (++ii == a.tps) { ii = 0; ++is; inl = n_lo_of(0); prev_valid = false; }
+    else inl += D * TO;
+  };
+  // prologue: issue sub-tiles 0 .. P-1 of the run
+#pragma unroll
+  for (int k = 0; k < P; ++k)
+    if (k < U) issue_next(k, k);
+
+  int s = s0, i = i0;
+  int64_t nl = n_lo_of(i0);
+  float carry = 0.f;
+  bool have = false;
+  int wacc = 0;
+  for (int v = 0; v < U; ++v) {
+    // ---- issue sub-tile v + P ----
+    if (v + P < U) issue_next(v + P, P);
+    else { kd[P] = 0; mk[P] = issued; }
+    const int pos = (5 * v) % C;
+    f2v* img = ring + 128 * pos;
+    const int64_t m0 = (int64_t)TO * i;
+    // ---- wait / build this sub-tile's image ----
+    if (kd[0] == 2) {
+      const int nw = issued - mk[0];
+      if (nw == 5 * P) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(5 * P) : "memory");
+      else if (nw == 5 * P + 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(5 * P + 1) : "memory");
+      else wait_vm_chain(nw);
+    } else {
+      const float* base = iqf + 2 * ((int64_t)s * p.stride);
+      for (int e = lane; e < L; e += 64) {
+        const int64_t nn = nl + e;
+        f2v x = f2v{0.f, 0.f};
+        if (MODE == 2) x = f2v{(float)e * 1e-4f, (float)lane};
+        else if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
+        img[e] = x;
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      issued = 0;
+#pragma unroll
+      for (int k = 0; k <= P; ++k) mk[k] = 0;
+    }
+
+    float ai[1], aq[1];
+    fe_fir_tile<T, D, 1, (MODE == 1 || MODE >= 4) ? 1 : 0>(img, lane, tp, ai, aq);
+
+    // ---- epilogue ----
+    float d[1];
+    const bool fast = i >= 1 && m0 + TO < M && p.i_ds == nullptr && have;
+    if (MODE >= 4) {
+      carry += ai[0] + aq[0];
+      d[0] = carry;
+    } else if (fast) {
+      const float phi = fast_atan2f(aq[0], ai[0]);
+      const float from_left = __int_as_float(__builtin_amdgcn_update_dpp(
+          0, __float_as_int(phi), 0x138 /*wave_shr:1*/, 0xf, 0xf, false));
+      const float prev = (lane == 0) ? carry : from_left;
+      float dd = phi - prev;
+      if (dd > kPiF) { dd -= k2PiF; wacc -= 1; }
+      else if (dd < -kPiF) { dd += k2PiF; wacc += 1; }
+      d[0] = dd;
+      if constexpr (!FUSED) {
+        p.demod[(int64_t)s * p.out_stride + m0 + lane] = dd;
+        issued += 1;
+      }
+      carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi), 63));
+    } else {
+      float si = 0.f, sq = 0.f;
+      if (m0 > 0 && !have) {
+        for (int k = lane; k < T; k += 64) {
+          const f2v x = img[(T - 1) - k];
+          const float h = p.taps_dev[k];
+          si = fmaf(h, x.x, si);
+          sq = fmaf(h, x.y, sq);
+        }
+        si = wave_sum(si);
+        sq = wave_sum(sq);
+      }
+      bool one = false;
+      carry = fe_epilogue<T, D, 1>(p, s, M, m0, lane, ai, aq, si, sq, have, carry, &one, d, !FUSED);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      issued = 0;
+#pragma unroll
+      for (int k = 0; k <= P; ++k) mk[k] = 0;
+    }
+
+    // next sub-tile in compute order
+    int s1 = s, i1 = i + 1;
+    if (i1 == a.tps) { i1 = 0; ++s1; }
+
+    if constexpr (FUSED && MODE < 4) {
+      const int ib = i % DA;                         // sub-tile within its audio block
+      const bool warm = v < U % DA;                  // leading warm-up sub-tiles of the run
+      const int rel = (warm ? (ib - DA) : ib) * TO + lane;
+      if (rel >= -HA) dh[HA + rel] = d[0];
+      if (!warm && ib == DA - 1) {
+        asm volatile("" ::: "memory");
+        const int64_t q = i / DA;
+        // lane window: dh[HA - (TA-1) + 5 lane + w], w = 0 .. 2*NPA-1 (pairs)
+        const float* aw = dh + (HA - (TA - 1) + DA * lane);
+        f2v acc0 = f2v{0.f, 0.f}, acc1 = f2v{0.f, 0.f};
+        constexpr int APF = 5;                       // steps read ahead (1.5 reads per step)
+        f2v xq[NPA];
+        f4v tq[(NPA + 1) / 2];
+        auto rd = [&](auto K) {
+          constexpr int k = K;
+          xq[k] = lds_read2_b32<2 * k, 2 * k + 1>(aw);
+          if constexpr ((k & 1) == 0) tq[k / 2] = lds_read_b128<8 * k>(ptab);   // entries k, k+1
+        };
+        // reads per step: 1 (odd k) or 2 (even k); counted waits by cumulative totals
+        constexpr auto nreads = [](int k) { return k + (k + 1) / 2; };   // reads issued for steps 0..k-1
+        static_for<0, APF>(rd);
+        static_for<0, NPA>([&](auto K) {
+          constexpr int k = K;
+          if constexpr (k + APF < NPA) rd(std::integral_constant<int, k + APF>{});
+          constexpr int issued_r = nreads(k + APF < NPA ? k + APF + 1 : NPA);
+          constexpr int needed_r = nreads(k + 1);
+          constexpr int pend = issued_r - needed_r;
+          lds_wait2<(pend > 15 ? 15 : pend)>(xq[k], tq[k / 2]);
+          const f2v t2 = (k & 1) ? f2v{tq[k / 2].z, tq[k / 2].w} : f2v{tq[k / 2].x, tq[k / 2].y};
+          if constexpr (k & 1) pk_fma_ordered(acc1, t2, xq[k]);
+          else pk_fma_ordered(acc0, t2, xq[k]);
+        });
+        const float out = (acc0.x + acc0.y) + (acc1.x + acc1.y);
+        const int64_t A = (M + DA - 1) / DA;
+        const int64_t j = q * TO + lane;
+        if (j < A) a.audio[(int64_t)s * a.audio_stride + j] = out;
+        if (q * TO + TO <= A) issued += 1;
+        else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          issued = 0;
+#pragma unroll
+          for (int k = 0; k <= P; ++k) mk[k] = 0;
+        }
+        asm volatile("" ::: "memory");
+        if (s1 != s)
+          for (int e = lane; e < HA; e += 64) dh[e] = 0.f;
+        else
+          for (int e = lane; e < HA; e += 64) dh[e] = dh[BD + e];
+        asm volatile("" ::: "memory");
+      }
+    }
+
+    if ((s1 != s || v + 1 == U) && p.wraps != nullptr) {
+      const int w = wave_sum_i(wacc);
+      if (lane == 0 && w != 0) atomicAdd(p.wraps + s, w);
+      wacc = 0;
+    }
+    have = (s1 == s);
+    nl = (s1 == s) ? nl + D * TO : n_lo_of(i1);
+    s = s1; i = i1;
+#pragma unroll
+    for (int k = 0; k < P; ++k) { mk[k] = mk[k + 1]; kd[k] = kd[k + 1]; }
   }
 }
 
@@ -890,6 +1251,16 @@ static int resident_per_cu(K kernel, int threads) {
   return n;
 }
 
+// f32 front-end kernel family: "ring" (fe_ring_kernel, default) or "circ" (fe_circ_kernel),
+// chosen once per process by SDR_FE_KERNEL (A/B measurement; both are parity-tested).
+static bool use_circ() {
+  static const bool c = [] {
+    const char* e = getenv("SDR_FE_KERNEL");
+    return e && strcmp(e, "circ") == 0;
+  }();
+  return c;
+}
+
 template <int T, int D, bool U8>
 static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
   constexpr int NT = U8 ? 128 : 64;
@@ -910,6 +1281,18 @@ static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
   if constexpr (U8) {
     hipLaunchKernelGGL((fe_kernel<T, D, R, NT, true>), dim3((unsigned)tiles), dim3(NT), 0, st, p, *a.taps);
   } else {
+    if (use_circ()) {
+      RingArgs ra{};
+      ra.tps = (int)((M + 63) / 64);
+      ra.total = (int64_t)ra.tps * a.nstreams;
+      static const int wpc = resident_per_cu(fe_circ_kernel<T>, 64);
+      const int64_t slots = (int64_t)cu_count() * std::min(wpc, 4);
+      ra.per_wave = (int)((ra.total + slots - 1) / slots);
+      const int64_t grid = (ra.total + ra.per_wave - 1) / ra.per_wave;
+      p.tiles_per_stream = ra.tps;
+      hipLaunchKernelGGL((fe_circ_kernel<T>), dim3((unsigned)grid), dim3(64), 0, st, p, *a.taps, ra);
+      return hipGetLastError();
+    }
     // fe_ring_kernel: 192 outputs per tile, one resident wave per SIMD
     constexpr int TO3 = 192;
     RingArgs ra{};
@@ -952,6 +1335,18 @@ static hipError_t launch_fe_mono_t(const FeLaunch& a, const float* ataps, float*
   if (ra.total <= 0) return hipSuccess;
   if (ra.total > 0x7fffffff / 5) return hipErrorInvalidValue;
   ra.audio = audio; ra.audio_stride = audio_stride; ra.ataps = ataps;
+  if (use_circ()) {
+    ra.ab = (int)((M + 319) / 320);
+    ra.tps = 5 * ra.ab;
+    ra.total = (int64_t)ra.ab * a.nstreams;
+    static const int wpc = resident_per_cu(fe_circ_kernel<T, true>, 64);
+    const int64_t slots = (int64_t)cu_count() * std::min(wpc, 4);
+    ra.per_wave = (int)((ra.total + slots - 1) / slots);
+    const int64_t grid = (ra.total + ra.per_wave - 1) / ra.per_wave;
+    p.tiles_per_stream = ra.tps;
+    hipLaunchKernelGGL((fe_circ_kernel<T, true>), dim3((unsigned)grid), dim3(64), 0, st, p, *a.taps, ra);
+    return hipGetLastError();
+  }
   static const int wpc = resident_per_cu(fe_ring_kernel<T, true>, 64);
   const int64_t slots = (int64_t)cu_count() * std::min(wpc, 4);
   ra.per_wave = (int)((ra.total + slots - 1) / slots);

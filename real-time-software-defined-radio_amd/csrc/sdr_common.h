@@ -88,6 +88,11 @@ __device__ __forceinline__ void pk_fma_bcast_x_ordered(f2v& acc, const f2v& tap2
     asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(tap2), "v"(x2));
 }
 
+// ordered elementwise packed FMA: acc += a * b (both halves)
+__device__ __forceinline__ void pk_fma_ordered(f2v& acc, const f2v& a, const f2v& b) {
+  asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+
 // ds_write_b128 issued by hand (ordered with the hand-issued reads above).
 __device__ __forceinline__ void lds_write_b128(void* lds_base, const f4v& v) {
   const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds_base;
@@ -145,12 +150,21 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// Counted LDS wait without register operands: ordering with the consumers comes from
-// every consumer being a volatile asm (pk_fma_bcast*), so no asm "defines" the loaded
-// registers right before their first reader (which would cost an s_nop, see fe.hip).
+// Counted LDS wait without register operands.  Only safe where the register allocator
+// cannot copy the in-flight destination before the wait; the kernels use the "+v" forms
+// below (lds_wait, lds_wait2, lds_wait3), which make that impossible.
 template <int N>
 __device__ __forceinline__ void lds_wait_ordered() {
   asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(N));
+}
+
+template <int N>
+__device__ __forceinline__ void lds_wait3(f2v& a, f4v& b, f4v& c) {
+  asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void lds_wait2(f2v& a, f4v& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
 }
 
 template <int N>
@@ -159,15 +173,17 @@ __device__ __forceinline__ void lds_wait(f4v& v) {
 }
 
 // atan2 for the discriminator: |err| <= ~2.5e-7 rad (2 ulp polynomial on [0, 1] after the
-// octant reduction), ~20 VALU instead of ocml's ~40 with its inf/nan handling; exact
-// zeros go to atan2f so the IEEE signed-zero results (e.g. atan2(+0, -0) = pi) hold.
+// octant reduction), branch-free: ~30 VALU and no divergent call into ocml's atan2f.  The
+// IEEE special cases are selected, not branched to: atan2(+-0, +-0), infinities (the
+// quotient of two infinities is taken as 1), and NaN inputs (NaN out).
 __device__ __forceinline__ float fast_atan2f(float y, float x) {
   const float ax = fabsf(x), ay = fabsf(y);
   const float mn = fminf(ax, ay), mx = fmaxf(ax, ay);
-  if (!(mx > 0.f) || !(mx < INFINITY)) return atan2f(y, x);   // zeros, inf, nan
-  const float rc = __builtin_amdgcn_rcpf(mx);
+  const float mxs = fmaxf(mx, 1e-30f);                // zeros: finite quotient 0, selected below
+  const float rc = __builtin_amdgcn_rcpf(mxs);
   float a = mn * rc;
-  a = fmaf(fmaf(-mx, a, mn), rc, a);                  // one Newton step: ~0.5 ulp quotient
+  a = fmaf(fmaf(-mxs, a, mn), rc, a);                 // one Newton step: ~0.5 ulp quotient
+  a = (mx == INFINITY) ? ((mn == INFINITY) ? 1.f : 0.f) : a;
   const float s = a * a;
   float r = 0.002849547192454338f;
   r = fmaf(r, s, -0.01606736145913601f);
@@ -179,9 +195,13 @@ __device__ __forceinline__ float fast_atan2f(float y, float x) {
   r = fmaf(r, s, -0.3333307206630707f);
   r = fmaf(r, s, 1.0f);
   r *= a;
-  if (ay > ax) r = 1.57079632679489662f - r;
-  if (x < 0.f) r = 3.14159265358979324f - r;
-  return copysignf(r, y);
+  r = (ay > ax) ? 1.57079632679489662f - r : r;
+  r = (x < 0.f) ? 3.14159265358979324f - r : r;
+  asm volatile("" : "+v"(r));                          // keep the selects below branch-free
+  // both zero: +0 -> 0, -0 -> pi (IEEE atan2 sign rules; copysign below gives +-)
+  r = (mx == 0.f) ? (__builtin_signbitf(x) ? 3.14159265358979324f : 0.f) : r;
+  r = copysignf(r, y);
+  return (x != x || y != y) ? __builtin_nanf("") : r;
 }
 
 // Wave-wide sum over 64 lanes (CDNA wave64: six xor steps).

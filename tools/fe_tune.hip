@@ -129,6 +129,32 @@ float time_ring_fused(FeParams p, const TapsF32& taps, const float* ataps, float
   return ms / iters;
 }
 
+template <bool FUSED, int MODE>
+float time_circ(FeParams p, const TapsF32& taps, const float* ataps, float* audio, hipStream_t st, int iters) {
+  const int64_t M = (p.n + 9) / 10;
+  RingArgs ra{};
+  if (FUSED) { ra.ab = (int)((M + 319) / 320); ra.tps = 5 * ra.ab; ra.total = (int64_t)ra.ab * p.nstreams; }
+  else { ra.tps = (int)((M + 63) / 64); ra.total = (int64_t)ra.tps * p.nstreams; }
+  ra.audio = audio; ra.audio_stride = (M + 4) / 5; ra.ataps = ataps;
+  const int64_t slots = 256LL * 4;
+  ra.per_wave = (int)((ra.total + slots - 1) / slots);
+  const int grid = (int)((ra.total + ra.per_wave - 1) / ra.per_wave);
+  p.tiles_per_stream = ra.tps;
+  if (FUSED) p.demod = nullptr;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i)
+    hipLaunchKernelGGL((fe_circ_kernel<101, FUSED, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
+  CK(hipEventRecord(a, st));
+  for (int i = 0; i < iters; ++i)
+    hipLaunchKernelGGL((fe_circ_kernel<101, FUSED, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
+  CK(hipEventRecord(b, st));
+  CK(hipEventSynchronize(b));
+  CK(hipGetLastError());
+  float ms; CK(hipEventElapsedTime(&ms, a, b));
+  return ms / iters;
+}
+
 int main(int argc, char** argv) {
   const int64_t n = 64LL * 1024000;  // complex samples
   const int64_t M = n / 10;
@@ -185,6 +211,16 @@ int main(int argc, char** argv) {
     float t0 = time_ring<0>(p, taps, st, it, W), t1 = time_ring<1>(p, taps, st, it, W), t2 = time_ring<2>(p, taps, st, it, W); \
     printf("ring R=3 NB=2 w/cu=%d: full %8.2f us (%7.1f GB/s)  mem-only %8.2f us  compute-only %8.2f us\n", W, t0 * 1e3, bytes / t0 / 1e6, t1 * 1e3, t2 * 1e3); }
   RUNR(4, "r4") RUNR(3, "r3") RUNR(2, "r2")
+  if (want("circ")) {
+    float* aud; CK(hipMalloc(&aud, (M / 5 + 64) * 4));
+    float f0 = time_circ<false, 0>(p, taps, tdev, aud, st, it), f1 = time_circ<false, 1>(p, taps, tdev, aud, st, it);
+    float f4 = time_circ<false, 4>(p, taps, tdev, aud, st, it);
+    printf("circ FE   : full %8.2f us (%7.1f GB/s)  no-FIR %8.2f us  DMA only %8.2f us\n", f0 * 1e3, bytes / f0 / 1e6, f1 * 1e3, f4 * 1e3);
+    float g0 = time_circ<true, 0>(p, taps, tdev, aud, st, it), g1 = time_circ<true, 1>(p, taps, tdev, aud, st, it);
+    float g4 = time_circ<true, 4>(p, taps, tdev, aud, st, it);
+    const double fb = n * 8.0 + (M / 5) * 4.0;
+    printf("circ fused: full %8.2f us (%7.1f GB/s)  no-FIR %8.2f us  DMA only %8.2f us\n", g0 * 1e3, fb / g0 / 1e6, g1 * 1e3, g4 * 1e3);
+  }
   if (want("fused")) {
     float* aud; CK(hipMalloc(&aud, (M / 5 + 64) * 4));
     float t0 = time_ring_fused<0>(p, taps, tdev, aud, st, it), t1 = time_ring_fused<1>(p, taps, tdev, aud, st, it);

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(64) void wave_glds(const float* __restrict__ in, fl
 // persistent: each wave streams tiles of NL KB round-robin through an NB-deep LDS ring
 // CONTIG: each wave takes a contiguous run of tiles (else round robin); STEP < NL*256:
 // tiles overlap (halo re-read); WR: each tile also writes WR floats per lane
-template <int NL, int NB, bool CONTIG = false, int STEP = NL * 256, int WR = 0, int AUX = 0>
+template <int NL, int NB, bool CONTIG = false, int STEP = NL * 256, int WR = 0, int AUX = 0, int DELAY = 0>
 __global__ __launch_bounds__(64) void ring_glds(const float* __restrict__ in, int64_t ntiles, float* out) {
   __shared__ __attribute__((aligned(16))) float lds[NB * NL * 256];
   const int lane = threadIdx.x;
@@ -70,6 +70,14 @@ __global__ __launch_bounds__(64) void ring_glds(const float* __restrict__ in, in
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     acc += lds[(u % NB) * NL * 256 + lane * 4];
+    if (DELAY > 0) {                 // synthetic per-tile compute: DELAY independent-ish FMAs
+      float x0 = acc, x1 = acc + 1.f, x2 = acc + 2.f, x3 = acc + 3.f;
+      for (int k = 0; k < DELAY; ++k) {
+        asm volatile("v_fma_f32 %0, %0, %0, %0\n\tv_fma_f32 %1, %1, %1, %1\n\tv_fma_f32 %2, %2, %2, %2\n\tv_fma_f32 %3, %3, %3, %3"
+                     : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+      }
+      acc += x0 + x1 + x2 + x3;
+    }
     if (WR == 2) {
 #pragma unroll
       for (int w = 0; w < WR; ++w) out[(tile(u) * 64 + lane) * WR + w] = acc;
@@ -143,5 +151,10 @@ int main(int argc, char** argv) {
   RING3(11, 2, 7, false, 2560, 6, 2) RING3(11, 2, 7, true, 2560, 6, 0)
   RING3(16, 2, 4, true, 3840, 0, 2) RING3(16, 2, 4, true, 3840, 3, 2) RING3(16, 2, 4, true, 3840, 9, 2)
   RING3(16, 2, 4, true, 3840, 5, 2) RING3(11, 2, 7, true, 2560, 9, 2) RING3(11, 2, 7, true, 2560, 5, 2)
+#define RINGD(NL, NB, W, STEP, DL) timeit("ring_glds NL=" #NL " NB=" #NB " w/cu=" #W " step=" #STEP " aux=2 delay=" #DL "x4 fma", [&] { \
+    hipLaunchKernelGGL((ring_glds<NL, NB, true, STEP, 0, 2, DL>), dim3(256 * W), dim3(64), 0, st, in, (bytes - NL * 1024) / (STEP * 4), out); });
+  RINGD(16, 2, 4, 3840, 0) RINGD(16, 2, 4, 3840, 100) RINGD(16, 2, 4, 3840, 200) RINGD(16, 2, 4, 3840, 400) RINGD(16, 2, 4, 3840, 800)
+  RINGD(16, 3, 3, 3840, 0) RINGD(16, 3, 3, 3840, 200) RINGD(16, 3, 3, 3840, 400)
+  RINGD(6, 3, 8, 1280, 0) RINGD(6, 3, 8, 1280, 67) RINGD(6, 3, 8, 1280, 133) RINGD(6, 2, 8, 1280, 67) RINGD(6, 2, 8, 1280, 133)
   return 0;
 }
