@@ -320,7 +320,7 @@ __global__ __launch_bounds__(NT) void fe_kernel(FeParams p, TapsF32 taps) {
 
 // Register-blocked FIR of one tile image (see fe_stream_kernel): lane l produces the R
 // decimated (I, Q) outputs of its window [D R l + D + DELTA, + D(R-1)+T).
-template <int T, int D, int R, int MODE, int PF = 8>
+template <int T, int D, int R, int MODE, int PF = 8, bool SAFEW = true>
 __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v (&tp)[(T + 1) / 2],
                                             float (&ai)[R], float (&aq)[R]) {
   constexpr int DELTA = (2 - ((D + T - 1) % 2)) % 2;
@@ -345,17 +345,16 @@ __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v 
     static_assert(PF >= 1 && PF <= 15, "lgkmcnt field");
     f4v qb[NP];
     static_for<0, (PF < NP ? PF : NP)>([&](auto I) { qb[I] = lds_read_b128<16 * I>(win4); });
+    if constexpr (SAFEW) lds_wait<PF - 1 < NP - 1 ? PF - 1 : NP - 1>(qb[0]);
+    else lds_wait_ordered<PF - 1 < NP - 1 ? PF - 1 : NP - 1>();
     static_for<0, NP>([&](auto I) {
       constexpr int ip = I;
       // the wait "redefines" qb[ip] ("+v"): the register allocator may then not copy or
       // spill the in-flight value before the data has arrived (it costs one s_nop per
       // step: hipcc's gfx950 dst-forwarding hazard rule, applied conservatively to asm)
-      if constexpr (ip + PF < NP) {
-        qb[ip + PF] = lds_read_b128<16 * (ip + PF)>(win4);
-        lds_wait<PF>(qb[ip]);
-      } else {
-        lds_wait<NP - 1 - ip>(qb[ip]);
-      }
+      // the read PF pairs ahead; qb[ip] itself was waited for one step earlier, so the
+      // step's FMAs separate each wait from the first reader of its register
+      if constexpr (ip + PF < NP) qb[ip + PF] = lds_read_b128<16 * (ip + PF)>(win4);
       const f4v q = qb[ip];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -367,10 +366,23 @@ __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v 
           const int k = D * r + T - 1 - i;
           if (k >= 0 && k < T) {
             const int a = (NA == 2) ? r * NA + ((k >> 1) & 1) : r;
+            // hand-written v_pk_fma_f32 with an op_sel tap broadcast.  (The compiler's own
+            // packed FMA folds the broadcast too, but then reschedules the whole loop into
+            // ~370 registers with AGPR spills; as inline asm each step costs one s_nop.)
             if (k & 1) pk_fma_bcast<true>(acc2[a], tp[k >> 1], x);
             else pk_fma_bcast<false>(acc[a], tp[k >> 1], x);
           }
         }
+      }
+      // wait for the next step's pair: reads issued so far = min(ip + PF + 1, NP).
+      // SAFEW: "+v" form (the allocator cannot copy the in-flight register; costs an s_nop
+      // per step, see sdr_common.h); else an operand-free wait, valid because every reader
+      // is a volatile asm and the kernel's register use leaves the allocator no reason to
+      // copy (r01: T=101 at 231 VGPRs; the parity tests check each compiled kernel).
+      if constexpr (ip + 1 < NP) {
+        constexpr int issued_r = (ip + PF + 1 < NP) ? ip + PF + 1 : NP;
+        if constexpr (SAFEW) lds_wait<issued_r - (ip + 2)>(qb[ip + 1]);
+        else lds_wait_ordered<issued_r - (ip + 2)>();
       }
     });
   }
@@ -382,6 +394,114 @@ __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v 
     aq[r] = t.y;
   }
 
+}
+
+// FE FIR of one R=3 tile (as fe_fir_tile) with the previous audio block's 3-output-per-
+// lane audio FIR interleaved step by step (fe_ring_kernel<FUSED>, steady path): the audio
+// reads (lane samples by ds_read2_b32, tap triples by broadcast ds_read_b128) are latency-
+// bound on their own, the FE FIR is VALU-bound; interleaved, each covers the other.
+// One static schedule: macro-step t runs FE step t and audio steps [NS*t/NP, NS*(t+1)/NP);
+// reads are issued PF (FE) / APF (audio) steps ahead and every wait counts the reads
+// issued after the one it needs (all compile-time; lgkmcnt <= 15 is asserted).
+namespace fa {
+template <int NP, int NS, int PF, int APF>
+struct Sched {
+  static constexpr int ab(int t) { return (NS * t) / NP; }               // first audio step of t
+  static constexpr int pro() { return (PF < NP ? PF : NP) + 3 * (APF < NS ? APF : NS); }
+  static constexpr int issued_at(int t) {                                 // reads issued in t
+    int n = (t + PF < NP) ? 1 : 0;
+    for (int k = ab(t); k < ab(t + 1); ++k) n += (k + APF < NS) ? 3 : 0;
+    return n;
+  }
+  static constexpr int cum(int t) {                                       // after t's issue phase
+    int n = pro();
+    for (int u = 0; u <= t; ++u) n += issued_at(u);
+    return n;
+  }
+  static constexpr int pos_fir(int ip) { return ip < PF ? ip : cum(ip - PF - 1); }
+  static constexpr int pos_aud(int k) {
+    if (k < APF) return (PF < NP ? PF : NP) + 3 * k;
+    const int ki = k - APF;                                               // issued with step ki
+    int t = 0;
+    while (!(ki >= ab(t) && ki < ab(t + 1))) ++t;
+    int n = cum(t - 1) + ((t + PF < NP) ? 1 : 0);
+    for (int kk = ab(t); kk < ki; ++kk) n += (kk + APF < NS) ? 3 : 0;
+    return n;
+  }
+  static constexpr int wait_fir(int t) { return cum(t) - (pos_fir(t) + 1); }
+  static constexpr int wait_aud(int t, int k) { return cum(t) - (pos_aud(k) + 3); }
+};
+template <int v> struct CW { static_assert(v >= 0 && v <= 15, "lgkmcnt field"); static constexpr int value = v; };
+}  // namespace fa
+
+template <int T, int PF, int APF>
+__device__ __forceinline__ void fir_audio_tile(const f2v* buf, int lane, const f2v (&tp)[(T + 1) / 2],
+                                               float (&ai)[3], float (&aq)[3], const float* aw,
+                                               const f4v* ptab, float& o0, float& o1, float& o2) {
+  constexpr int D = 10, R = 3;
+  constexpr int NI = D * (R - 1) + T;
+  constexpr int NP = (NI + 1) / 2;                   // FE steps (sample pairs)
+  constexpr int NS = 81;                             // audio steps (161-sample window in pairs)
+  using S = fa::Sched<NP, NS, PF, APF>;
+  const f2v* win = buf + (D * R * lane + D);
+  const float4* win4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(win, 16));
+  f2v acc[R], acc2[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) { acc[r] = f2v{0.f, 0.f}; acc2[r] = f2v{0.f, 0.f}; }
+  f2v a01a = f2v{0.f, 0.f}, a01b = f2v{0.f, 0.f};
+  float a2a = 0.f, a2b = 0.f;
+  f4v qb[NP];
+  f2v xq[NS];
+  f4v ta[NS], tb[NS];
+  auto rd_aud = [&](auto K) {
+    constexpr int k = K;
+    xq[k] = lds_read2_b32<2 * k, 2 * k + 1>(aw);
+    ta[k] = lds_read_b128<32 * k>(ptab);
+    tb[k] = lds_read_b128<32 * k + 16>(ptab);
+  };
+  static_for<0, (PF < NP ? PF : NP)>([&](auto I) { qb[I] = lds_read_b128<16 * I>(win4); });
+  static_for<0, (APF < NS ? APF : NS)>(rd_aud);
+  static_for<0, NP>([&](auto I) {
+    constexpr int t = I;
+    if constexpr (t + PF < NP) qb[t + PF] = lds_read_b128<16 * (t + PF)>(win4);
+    static_for<S::ab(t), S::ab(t + 1)>([&](auto K) {
+      constexpr int k = K;
+      if constexpr (k + APF < NS) rd_aud(std::integral_constant<int, k + APF>{});
+    });
+    lds_wait<fa::CW<S::wait_fir(t)>::value>(qb[t]);
+    const f4v q = qb[t];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = 2 * t + h;
+      if (i >= NI) break;
+      const f2v x = h ? f2v{q.z, q.w} : f2v{q.x, q.y};
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int k = D * r + T - 1 - i;
+        if (k >= 0 && k < T) {
+          if (k & 1) pk_fma_bcast<true>(acc2[r], tp[k >> 1], x);
+          else pk_fma_bcast<false>(acc[r], tp[k >> 1], x);
+        }
+      }
+    }
+    static_for<S::ab(t), S::ab(t + 1)>([&](auto K) {
+      constexpr int k = K;
+      lds_wait3<fa::CW<S::wait_aud(t, k)>::value>(xq[k], ta[k], tb[k]);
+      pk_fma_bcast_x_ordered<false>(a01a, f2v{ta[k].x, ta[k].y}, xq[k]);
+      pk_fma_bcast_x_ordered<true>(a01b, f2v{tb[k].x, tb[k].y}, xq[k]);
+      fmac_ordered(a2a, ta[k].z, xq[k].x);
+      fmac_ordered(a2b, tb[k].z, xq[k].y);
+    });
+  });
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const f2v t = acc[r] + acc2[r];
+    ai[r] = t.x;
+    aq[r] = t.y;
+  }
+  o0 = a01a.x + a01b.x;
+  o1 = a01a.y + a01b.y;
+  o2 = a2a + a2b;
 }
 
 // Persistent streaming f32 front end: the product kernel for f32 IQ.
@@ -652,68 +772,84 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   // FUSED: demod values of tile (i) -> history; after the block's last tile, the block's
   // audio outputs (lane l: 3l..3l+2) and the history shift.  `next_same`: the following
   // tile continues this stream.
-  auto fused_tail = [&](int i, bool warm, const float (&d)[R], bool next_same) -> bool {
-    bool drained = false;
+  // FUSED audio pieces: the block's outputs (lane l: 3l..3l+2) from the history, their
+  // store (returns true if it drained vmcnt), and the history shift / reset
+  const float* aw_lane = dh + (HA - (TA - 1) + DA * RA * lane);   // lane window in dh
+  auto audio_compute = [&](float& o0, float& o1, float& o2) {
+    asm volatile("" ::: "memory");
+    // hand-pipelined like the FIR: per step k (samples 2k, 2k+1) one ds_read2_b32 of the
+    // lane's samples + two broadcast ds_read_b128 of tap triples, APF steps ahead
+    f2v acc01a = f2v{0.f, 0.f}, acc01b = f2v{0.f, 0.f};
+    float a2a = 0.f, a2b = 0.f;
+    constexpr int NS = (NW + 1) / 2, APF = 5;   // 3*APF <= 15 (lgkmcnt field)
+    f2v xq[NS];
+    f4v ta[NS], tb[NS];
+    auto rd = [&](auto K) {
+      constexpr int k = K;
+      xq[k] = lds_read2_b32<2 * k, 2 * k + 1>(aw_lane);
+      ta[k] = lds_read_b128<32 * k>(ptab);
+      tb[k] = lds_read_b128<32 * k + 16>(ptab);
+    };
+    static_for<0, APF>(rd);
+    static_for<0, NS>([&](auto K) {
+      constexpr int k = K;
+      if constexpr (k + APF < NS) {
+        rd(std::integral_constant<int, k + APF>{});
+        lds_wait3<3 * APF>(xq[k], ta[k], tb[k]);
+      } else {
+        lds_wait3<3 * (NS - 1 - k)>(xq[k], ta[k], tb[k]);
+      }
+      pk_fma_bcast_x_ordered<false>(acc01a, f2v{ta[k].x, ta[k].y}, xq[k]);
+      pk_fma_bcast_x_ordered<true>(acc01b, f2v{tb[k].x, tb[k].y}, xq[k]);
+      fmac_ordered(a2a, ta[k].z, xq[k].x);
+      fmac_ordered(a2b, tb[k].z, xq[k].y);
+    });
+    o0 = acc01a.x + acc01b.x;
+    o1 = acc01a.y + acc01b.y;
+    o2 = a2a + a2b;
+  };
+  auto audio_store = [&](int64_t q, float o0, float o1, float o2) -> bool {
+    const int64_t A = (M + DA - 1) / DA;
+    const int64_t j = q * BO + RA * lane;
+    float* ao = a.audio + (int64_t)s * a.audio_stride + j;
+    if (q * BO + BO <= A) {
+      typedef float f3v __attribute__((ext_vector_type(3)));
+      *reinterpret_cast<f3v*>(ao) = f3v{o0, o1, o2};
+      issued += 1;
+      return false;
+    }
+    if (j < A) ao[0] = o0;
+    if (j + 1 < A) ao[1] = o1;
+    if (j + 2 < A) ao[2] = o2;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    issued = 0;
+    return true;
+  };
+  auto dh_shift = [&](bool next_same) {
+    asm volatile("" ::: "memory");
+    if (!next_same)
+      for (int e = lane; e < HA; e += 64) dh[e] = 0.f;     // next block starts a new stream
+    else
+      for (int e = lane; e < HA; e += 64) dh[e] = dh[BD + e];
+    asm volatile("" ::: "memory");
+  };
+  auto dh_write = [&](int i, bool warm, const float (&d)[R]) {
     const int ib = i - TPB * (i / TPB);            // tile within its audio block (warm-up: 4)
     const int rel0 = (warm ? -TO : ib * TO) + R * lane;
 #pragma unroll
     for (int r = 0; r < R; ++r)
       if (rel0 + r >= -HA) dh[HA + rel0 + r] = d[r];
-    if (!warm && ib == TPB - 1) {
-        asm volatile("" ::: "memory");
-        const int64_t q = i / TPB;
-        // lane window: dh[HA - (TA-1) + 15 lane + w], w = 0 .. NW-1
-        const float* aw = dh + (HA - (TA - 1) + DA * RA * lane);
-        // hand-pipelined like the FIR: per step k (samples 2k, 2k+1) one ds_read2_b32 of the
-        // lane's samples + two broadcast ds_read_b128 of tap triples, APF steps ahead
-        f2v acc01a = f2v{0.f, 0.f}, acc01b = f2v{0.f, 0.f};
-        float a2a = 0.f, a2b = 0.f;
-        constexpr int NS = (NW + 1) / 2, APF = 5;   // 3*APF <= 15 (lgkmcnt field)
-        f2v xq[NS];
-        f4v ta[NS], tb[NS];
-        auto rd = [&](auto K) {
-          constexpr int k = K;
-          xq[k] = lds_read2_b32<2 * k, 2 * k + 1>(aw);
-          ta[k] = lds_read_b128<32 * k>(ptab);
-          tb[k] = lds_read_b128<32 * k + 16>(ptab);
-        };
-        static_for<0, APF>(rd);
-        static_for<0, NS>([&](auto K) {
-          constexpr int k = K;
-          if constexpr (k + APF < NS) {
-            rd(std::integral_constant<int, k + APF>{});
-            lds_wait3<3 * APF>(xq[k], ta[k], tb[k]);
-          } else {
-            lds_wait3<3 * (NS - 1 - k)>(xq[k], ta[k], tb[k]);
-          }
-          pk_fma_bcast_x_ordered<false>(acc01a, f2v{ta[k].x, ta[k].y}, xq[k]);
-          pk_fma_bcast_x_ordered<true>(acc01b, f2v{tb[k].x, tb[k].y}, xq[k]);
-          fmac_ordered(a2a, ta[k].z, xq[k].x);
-          fmac_ordered(a2b, tb[k].z, xq[k].y);
-        });
-        const float o0 = acc01a.x + acc01b.x, o1 = acc01a.y + acc01b.y, o2 = a2a + a2b;
-        const int64_t A = (M + DA - 1) / DA;
-        const int64_t j = q * BO + RA * lane;
-        float* ao = a.audio + (int64_t)s * a.audio_stride + j;
-        if (q * BO + BO <= A) {
-          typedef float f3v __attribute__((ext_vector_type(3)));
-          *reinterpret_cast<f3v*>(ao) = f3v{o0, o1, o2};
-          issued += 1;
-        } else {
-          if (j < A) ao[0] = o0;
-          if (j + 1 < A) ao[1] = o1;
-          if (j + 2 < A) ao[2] = o2;
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          issued = 0;
-          drained = true;
-        }
-        asm volatile("" ::: "memory");
-        if (!next_same)
-          for (int e = lane; e < HA; e += 64) dh[e] = 0.f;     // next block starts a new stream
-        else
-          for (int e = lane; e < HA; e += 64) dh[e] = dh[BD + e];
-        asm volatile("" ::: "memory");
-    }
+  };
+  // FUSED (general path): demod values of tile i -> history; after the block's last tile,
+  // the block's audio outputs and the history shift.  Returns true if vmcnt was drained.
+  auto fused_tail = [&](int i, bool warm, const float (&d)[R], bool next_same) -> bool {
+    dh_write(i, warm, d);
+    const int ib = i - TPB * (i / TPB);
+    if (warm || ib != TPB - 1) return false;
+    float o0, o1, o2;
+    audio_compute(o0, o1, o2);
+    const bool drained = audio_store(i / TPB, o0, o1, o2);
+    dh_shift(next_same);
     return drained;
   };
   // fast epilogue of an interior tile: phases, predecessor (DPP / carry), np.unwrap wrap
@@ -745,7 +881,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   const int64_t j_fast = M >= TO + 1 ? (M - TO - 1) / TO : -1;
   stamp(-1);
   for (int u = 0; u < U; ++u) {
-    if constexpr (MODE == 0) {
+    if constexpr (MODE == 0 || MODE == 6) {
       // ---- steady run: consecutive interior tiles of one stream, fixed VMEM pattern ----
       if (kind >= 2 && have && i >= 1 && p.i_ds == nullptr) {
         int64_t K = min<int64_t>(U - 1 - u, a.tps - 1 - i);
@@ -754,6 +890,8 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
         if (K > 0) {
           const char* gn = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s * p.stride + nl + D * TO)) + 1024 * HCH;
           float* outp = FUSED ? nullptr : p.demod + (int64_t)s * p.out_stride + (int64_t)TO * i + R * lane;
+          bool pend = false;                 // FUSED: a finished block's audio not yet computed
+          int64_t q_pend = 0;
           for (int k = 0; k < (int)K; ++k) {
             // issue the next tile's new chunks into the other slot
             {
@@ -767,29 +905,61 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
             }
             issued += NEWC;
             const int mark1 = issued;
+            stamp(0);
             wait_tile(issued - mark);
+            stamp(1);
             f2v* buf = &ring[b][0];
             f4v h0 = lds_read_b128<0>(buf + NEWC * 128 + 2 * lane), h1;
             if constexpr (HCH == 2) h1 = lds_read_b128<0>(buf + (NEWC + 1) * 128 + 2 * lane);
             float ai[R], aq[R];
-            fe_fir_tile<T, D, R, 0, (T > 127 ? 8 : RING_PF)>(buf, lane, tp, ai, aq);
+            bool aud_drained = false;
+            if constexpr (FUSED && T <= 127) {
+              if (pend) {                    // previous block's audio, interleaved into this FIR
+                float o0, o1, o2;
+                fir_audio_tile<T, 2, 2>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2);
+                aud_drained = audio_store(q_pend, o0, o1, o2);
+                dh_shift(true);
+                pend = false;
+              } else {
+                fe_fir_tile<T, D, R, 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
+              }
+            } else {
+              fe_fir_tile<T, D, R, 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
+            }
             lds_wait<0>(h0);
             lds_write_b128(&ring[b ^ 1][0] + 2 * lane, h0);
             if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(&ring[b ^ 1][0] + 128 + 2 * lane, h1); }
+            stamp(2);
             float d[R];
             fast_epi(ai, aq, d);
+            stamp(3);
             if constexpr (!FUSED) {
               typedef float f3v __attribute__((ext_vector_type(3)));
               *reinterpret_cast<f3v*>(outp) = f3v{d[0], d[1], d[2]};
               outp += TO;
               issued += 1;
             } else {
-              if (fused_tail(i, false, d, true)) { mark = 0; b ^= 1; ++i; nl += D * TO; continue; }
+              if constexpr (T <= 127) {
+                dh_write(i, false, d);
+                if (i - TPB * (i / TPB) == TPB - 1) { pend = true; q_pend = i / TPB; }
+                if (aud_drained) { stamp(4); mark = 0; b ^= 1; ++i; nl += D * TO; continue; }
+              } else {
+                if (fused_tail(i, false, d, true)) { mark = 0; b ^= 1; ++i; nl += D * TO; continue; }
+              }
             }
+            stamp(4);
             mark = mark1;
             b ^= 1;
             ++i;
             nl += D * TO;
+          }
+          if constexpr (FUSED) {
+            if (pend) {                      // flush: the block ended on the steady run's last tile
+              float o0, o1, o2;
+              audio_compute(o0, o1, o2);
+              if (audio_store(q_pend, o0, o1, o2)) mark = 0;
+              dh_shift(i < a.tps);           // i: the next tile (same stream unless past the end)
+            }
           }
           u += (int)K;
           kind = 3;
@@ -838,7 +1008,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     }
 
     float ai[R], aq[R];
-    fe_fir_tile<T, D, R, (MODE == 1 || MODE == 4 || MODE == 5) ? 1 : 0, (T > 127 ? 8 : RING_PF)>(buf, lane, tp, ai, aq);
+    fe_fir_tile<T, D, R, (MODE == 1 || MODE == 4 || MODE == 5) ? 1 : 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
 
     if (kind1 == 3) {
       lds_wait<0>(h0);
