@@ -320,9 +320,14 @@ __global__ __launch_bounds__(NT) void fe_kernel(FeParams p, TapsF32 taps) {
 
 // Register-blocked FIR of one tile image (see fe_stream_kernel): lane l produces the R
 // decimated (I, Q) outputs of its window [D R l + D + DELTA, + D(R-1)+T).
-template <int T, int D, int R, int MODE, int PF = 8, bool SAFEW = true>
+// `hook(integral_constant<int, step>)` runs at the start of every step (sample pair):
+// the steady ring loop uses it to spread the next tile's LDS-DMA issue over the FIR.
+struct NoHook {
+  template <typename I> __device__ __forceinline__ void operator()(I) const {}
+};
+template <int T, int D, int R, int MODE, int PF = 8, bool SAFEW = true, typename Hook = NoHook>
 __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v (&tp)[(T + 1) / 2],
-                                            float (&ai)[R], float (&aq)[R]) {
+                                            float (&ai)[R], float (&aq)[R], Hook hook = Hook{}) {
   constexpr int DELTA = (2 - ((D + T - 1) % 2)) % 2;
   constexpr int NI = D * (R - 1) + T;
   const f2v* win = buf + (D * R * lane + D + DELTA);
@@ -344,17 +349,25 @@ __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v 
     constexpr int NP = (NI + 1) / 2;
     static_assert(PF >= 1 && PF <= 15, "lgkmcnt field");
     f4v qb[NP];
-    static_for<0, (PF < NP ? PF : NP)>([&](auto I) { qb[I] = lds_read_b128<16 * I>(win4); });
-    if constexpr (SAFEW) lds_wait<PF - 1 < NP - 1 ? PF - 1 : NP - 1>(qb[0]);
+    // MODE 2 (tuning): no LDS reads, every step filters the same register values
+    const f4v seed = f4v{1e-3f * lane, 2e-3f, 3e-3f, 4e-3f};
+    auto rd = [&](auto I) {
+      if constexpr (MODE == 2) qb[I] = seed;
+      else qb[I] = lds_read_b128<16 * I>(win4);
+    };
+    static_for<0, (PF < NP ? PF : NP)>(rd);
+    if constexpr (MODE == 2) {
+    } else if constexpr (SAFEW) lds_wait<PF - 1 < NP - 1 ? PF - 1 : NP - 1>(qb[0]);
     else lds_wait_ordered<PF - 1 < NP - 1 ? PF - 1 : NP - 1>();
     static_for<0, NP>([&](auto I) {
       constexpr int ip = I;
+      hook(I);
       // the wait "redefines" qb[ip] ("+v"): the register allocator may then not copy or
       // spill the in-flight value before the data has arrived (it costs one s_nop per
       // step: hipcc's gfx950 dst-forwarding hazard rule, applied conservatively to asm)
       // the read PF pairs ahead; qb[ip] itself was waited for one step earlier, so the
       // step's FMAs separate each wait from the first reader of its register
-      if constexpr (ip + PF < NP) qb[ip + PF] = lds_read_b128<16 * (ip + PF)>(win4);
+      if constexpr (ip + PF < NP) rd(std::integral_constant<int, ip + PF>{});
       const f4v q = qb[ip];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -379,7 +392,7 @@ __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v 
       // per step, see sdr_common.h); else an operand-free wait, valid because every reader
       // is a volatile asm and the kernel's register use leaves the allocator no reason to
       // copy (r01: T=101 at 231 VGPRs; the parity tests check each compiled kernel).
-      if constexpr (ip + 1 < NP) {
+      if constexpr (ip + 1 < NP && MODE != 2) {
         constexpr int issued_r = (ip + PF + 1 < NP) ? ip + PF + 1 : NP;
         if constexpr (SAFEW) lds_wait<issued_r - (ip + 2)>(qb[ip + 1]);
         else lds_wait_ordered<issued_r - (ip + 2)>();
@@ -434,10 +447,11 @@ struct Sched {
 template <int v> struct CW { static_assert(v >= 0 && v <= 15, "lgkmcnt field"); static constexpr int value = v; };
 }  // namespace fa
 
-template <int T, int PF, int APF>
+template <int T, int PF, int APF, typename Hook = NoHook>
 __device__ __forceinline__ void fir_audio_tile(const f2v* buf, int lane, const f2v (&tp)[(T + 1) / 2],
                                                float (&ai)[3], float (&aq)[3], const float* aw,
-                                               const f4v* ptab, float& o0, float& o1, float& o2) {
+                                               const f4v* ptab, float& o0, float& o1, float& o2,
+                                               Hook hook = Hook{}) {
   constexpr int D = 10, R = 3;
   constexpr int NI = D * (R - 1) + T;
   constexpr int NP = (NI + 1) / 2;                   // FE steps (sample pairs)
@@ -463,6 +477,7 @@ __device__ __forceinline__ void fir_audio_tile(const f2v* buf, int lane, const f
   static_for<0, (APF < NS ? APF : NS)>(rd_aud);
   static_for<0, NP>([&](auto I) {
     constexpr int t = I;
+    hook(I);
     if constexpr (t + PF < NP) qb[t + PF] = lds_read_b128<16 * (t + PF)>(win4);
     static_for<S::ab(t), S::ab(t + 1)>([&](auto K) {
       constexpr int k = K;
@@ -653,6 +668,18 @@ void fe_stream_kernel(FeParams p, TapsF32 taps, int64_t total_tiles) {
 #ifndef RING_PF
 #define RING_PF 12
 #endif
+#ifndef RING_STG             // steady loop: VGPR-staged prefetch depth (0 = LDS-DMA, 1 ahead)
+#define RING_STG 0
+#endif
+#ifndef RING_SPREAD          // steady loop: spread the next tile's DMA issue over the FIR
+#define RING_SPREAD 1
+#endif
+#ifndef RING_SPREAD_T0       // first FIR step that issues a group of 4 chunks
+#define RING_SPREAD_T0 2
+#endif
+#ifndef RING_SPREAD_DT       // FIR steps between groups
+#define RING_SPREAD_DT 8
+#endif
 struct RingArgs {
   int64_t total;       // work units: tiles (FE), or audio blocks (FUSED), over all streams
   int per_wave;        // units per wave (contiguous run)
@@ -671,6 +698,21 @@ struct RingArgs {
 template <int T, bool FUSED = false, int MODE = 0>
 __global__ __launch_bounds__(64)
 void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
+  // MODE = MB | (SV << 4): MB selects tuning ablations (0 = product), SV a DMA-issue
+  // schedule for A/B runs in one process (0 = the RING_SPREAD* defaults)
+  constexpr int MB = MODE & 15, SV = (MODE >> 4) & 15;
+  // steady-loop ablations (tuning only): 0x100 trivial epilogue, 0x200 no audio FIR,
+  // 0x400 FE FIR without LDS reads
+  constexpr bool AB_NOEPI = MODE & 0x100, AB_NOAUD = MODE & 0x200, AB_NOLDS = MODE & 0x400;
+  constexpr int FM = AB_NOLDS ? 2 : 0;
+  // steady-loop prefetch: STG = 0 -> the next tile by LDS-DMA (one tile ahead); STG >= 2 ->
+  // tiles t+1..t+STG by 16-B loads into VGPR stages, written to the free LDS slot by the
+  // wave after the FIR of tile t (STG tiles in flight instead of one)
+  constexpr int STG = (MODE & 0x3000) ? (((MODE >> 12) & 3) + 1) : RING_STG;
+
+  constexpr int SPR = SV == 0 ? RING_SPREAD : (SV == 1 ? 0 : 1);
+  constexpr int ST0 = SV == 0 ? RING_SPREAD_T0 : (SV == 3 ? 4 : 2);
+  constexpr int SDT = SV == 0 ? RING_SPREAD_DT : (SV == 2 ? 4 : (SV == 3 ? 14 : 8));
   constexpr int D = 10, R = 3, TO = 64 * R;
   constexpr int NEWC = D * TO / 128;                 // 15 new 1-KiB chunks per tile
   constexpr int NCH = (D * TO + T + 1 + 127) / 128;  // chunks per tile image
@@ -712,7 +754,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   // tile (s, i): outputs m0 = TO*i ..; image = samples [n_lo, n_lo + L) of stream s,
   // n_lo = D*(m0-1) - (T-1) (output m0-1's window first, for the predecessor)
   auto n_lo_of = [&](int i) { return (int64_t)(D * TO) * i - D - (T - 1); };
-  auto interior = [&](int64_t nl) { return MODE != 2 && nl >= -p.hist && nl + L <= p.n; };
+  auto interior = [&](int64_t nl) { return MB != 2 && nl >= -p.hist && nl + L <= p.n; };
   // issue chunks [0 or HCH, NCH) of tile image nl (stream s) into ring slot b
   auto issue = [&](int s, int64_t nl, int b, bool full) {
     const char* g = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s * p.stride + nl));
@@ -758,11 +800,11 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   bool have = false;
   int wacc = 0;
   int b = 0;
-  // MODE 6 (tuning): per-phase s_memtime accounting -> p.q_ds as uint64[grid][8]
+  // MB 6 (tuning): per-phase s_memtime accounting -> p.q_ds as uint64[grid][8]
   uint64_t tph[6] = {0, 0, 0, 0, 0, 0};
   uint64_t tlast = 0;
   auto stamp = [&](int k) {
-    if constexpr (MODE == 6) {
+    if constexpr (MB == 6) {
       uint64_t t;
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
       if (k >= 0) tph[k] += t - tlast;
@@ -871,7 +913,9 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[R - 1]), 63));
   };
   auto wait_tile = [&](int nw) {                   // VMEM ops issued after the tile's loads
-    if (nw == NEWC) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC) : "memory");
+    if (nw == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (nw == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else if (nw == NEWC) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC) : "memory");
     else if (nw == NEWC + 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC + 1) : "memory");
     else wait_vm_chain(nw);
   };
@@ -879,34 +923,151 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   // fast epilogue (full tile strictly before the last output)
   const int64_t j_int = (p.n + D + (T - 1) - L) / (D * TO);
   const int64_t j_fast = M >= TO + 1 ? (M - TO - 1) / TO : -1;
+  // ---- staged steady run (STG >= 2): tiles i .. i+K-1 of stream s, all interior ----
+  // Entry: tile i's image is in slot b (LDS-DMA in flight, counted by `mark`), or resident
+  // (kind 4).  Tile i+j (j >= 1) is loaded into VGPR stage j % STG; after the FIR of tile t
+  // the wave waits for stage (t+1) % STG, writes it to the other slot (plus the halo chunk
+  // from this slot), and reuses the stage for tile t+1+STG.  Exit: tile i+K resident in
+  // slot b (b, i, nl advanced by K); no loads outstanding.
+  static_assert(STG == 0 || (STG >= 2 && STG * NEWC + 2 <= 63), "stages (vmcnt is 6-bit)");
+  f4v stg[STG > 0 ? STG : 1][NEWC];
+  auto staged_run = [&](int64_t K) {
+    if constexpr (STG > 0) {
+      const unsigned voff16 = 16u * lane;
+      const char* gl = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s * p.stride + nl + D * TO)) + 1024 * HCH;
+      int smark[STG];
+      auto load_stage = [&](auto SQ) {       // next tile to load -> stage SQ; advances gl
+        constexpr int sq = SQ;
+        static_for<0, NEWC>([&](auto C) {
+          constexpr int c = C;
+          gload16_nt_a<1024 * (c % 4)>(stg[sq][c], voff16, gl + 4096 * (c / 4));
+        });
+        gl += D * TO * 8;
+        issued += NEWC;
+        smark[sq] = issued;
+      };
+      const bool resident = (kind == 4);
+      const int mark0 = mark;
+      static_for<1, STG + 1>([&](auto J) {
+        constexpr int j = J;
+        if (j <= K) load_stage(std::integral_constant<int, j % STG>{});
+      });
+      if (!resident) wait_tile(issued - mark0);
+      float* outp = FUSED ? nullptr : p.demod + (int64_t)s * p.out_stride + (int64_t)TO * i + R * lane;
+      bool pend = false;
+      int64_t q_pend = 0;
+      auto body = [&](auto Q, int64_t kk) {
+        constexpr int sn = (Q + 1) % STG;      // stage of tile kk+1
+        f2v* buf = &ring[b][0];
+        f2v* nb = &ring[b ^ 1][0];
+        f4v h0 = lds_read_b128<0>(buf + NEWC * 128 + 2 * lane), h1;
+        if constexpr (HCH == 2) h1 = lds_read_b128<0>(buf + (NEWC + 1) * 128 + 2 * lane);
+        float ai[R], aq[R];
+        bool aud_drained = false;
+        if constexpr (FUSED && T <= 127) {
+          if (pend) {
+            float o0, o1, o2;
+            fir_audio_tile<T, 2, 2>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2);
+            aud_drained = audio_store(q_pend, o0, o1, o2);
+            dh_shift(true);
+            pend = false;
+          } else {
+            fe_fir_tile<T, D, R, 0, RING_PF, true>(buf, lane, tp, ai, aq);
+          }
+        } else {
+          fe_fir_tile<T, D, R, 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
+        }
+        // tile kk+1 -> the other slot (its halo from this slot); refill the stage
+        {
+          // steady state: the later stages' loads (+ a few stores) are still outstanding
+          constexpr int LO = (STG - 1) * NEWC;
+          const int nw = issued - smark[sn];
+          bool done = false;
+          static_for<LO, LO + STG + 2>([&](auto V) {
+            constexpr int v = V;
+            if (!done && nw == v) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(v) : "memory"); done = true; }
+          });
+          if (!done) wait_tile(nw);
+        }
+        const unsigned na = lds_addr_of(nb) + 16u * lane;
+        static_for<0, NEWC>([&](auto C) {
+          constexpr int c = C;
+          asm volatile("" : "+a"(stg[sn][c]));
+          lds_write_b128_a<1024 * (HCH + c)>(na, stg[sn][c]);
+        });
+        lds_wait<0>(h0);
+        lds_write_b128(nb + 2 * lane, h0);
+        if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(nb + 128 + 2 * lane, h1); }
+        if (kk + 1 + STG <= K) load_stage(std::integral_constant<int, sn>{});
+        float d[R];
+        fast_epi(ai, aq, d);
+        if constexpr (!FUSED) {
+          typedef float f3v __attribute__((ext_vector_type(3)));
+          *reinterpret_cast<f3v*>(outp) = f3v{d[0], d[1], d[2]};
+          outp += TO;
+          issued += 1;
+        } else if constexpr (T <= 127) {
+          dh_write(i, false, d);
+          if (i - TPB * (i / TPB) == TPB - 1) { pend = true; q_pend = i / TPB; }
+        } else {
+          fused_tail(i, false, d, true);
+        }
+        (void)aud_drained;
+        b ^= 1;
+        ++i;
+        nl += D * TO;
+      };
+      for (int64_t k = 0; k < K; k += STG)
+        static_for<0, STG>([&](auto Q) {
+          if (k + Q < K) body(Q, k + Q);
+        });
+      if constexpr (FUSED) {
+        if (pend) {
+          float o0, o1, o2;
+          audio_compute(o0, o1, o2);
+          audio_store(q_pend, o0, o1, o2);
+          dh_shift(i < a.tps);
+        }
+      }
+      mark = issued;
+    }
+  };
   stamp(-1);
   for (int u = 0; u < U; ++u) {
-    if constexpr (MODE == 0 || MODE == 6) {
+    if constexpr (MB == 0 || MB == 6) {
       // ---- steady run: consecutive interior tiles of one stream, fixed VMEM pattern ----
       if (kind >= 2 && have && i >= 1 && p.i_ds == nullptr) {
         int64_t K = min<int64_t>(U - 1 - u, a.tps - 1 - i);
         K = min<int64_t>(K, j_int - i);
         K = min<int64_t>(K, j_fast - i + 1);
-        if (K > 0) {
+        if (STG > 0 && K > 0) {
+          staged_run(K);
+          u += (int)K;
+          kind = 4;                          // tile u is resident in slot b (written by the run)
+        } else if (K > 0) {
           const char* gn = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s * p.stride + nl + D * TO)) + 1024 * HCH;
           float* outp = FUSED ? nullptr : p.demod + (int64_t)s * p.out_stride + (int64_t)TO * i + R * lane;
           bool pend = false;                 // FUSED: a finished block's audio not yet computed
           int64_t q_pend = 0;
           for (int k = 0; k < (int)K; ++k) {
-            // issue the next tile's new chunks into the other slot
-            {
-              const unsigned lb = lds_addr_of(&ring[b ^ 1][0]) + 1024 * HCH;
-              static_for<0, (NEWC + 3) / 4>([&](auto Q) {
-                constexpr int c = 4 * Q;
-                constexpr int n = (NEWC - c) < 4 ? (NEWC - c) : 4;
-                glds16x<n>(voff, gn + 1024 * c, lb + 1024 * c);
-              });
-              gn += D * TO * 8;
-            }
-            issued += NEWC;
-            const int mark1 = issued;
+            // the next tile's new chunks go into the other slot: issued up front, or (RING_SPREAD)
+            // in groups of 4 spread over the FIR steps, so the VMEM queue never stalls the wave
+            const unsigned lb = lds_addr_of(&ring[b ^ 1][0]) + 1024 * HCH;
+            auto issue_grp = [&](auto Q) {
+              constexpr int c = 4 * Q;
+              constexpr int n = (NEWC - c) < 4 ? (NEWC - c) : 4;
+              glds16x<n>(voff, gn + 1024 * c, lb + 1024 * c);
+            };
+            auto spread = [&](auto I) {
+              constexpr int t = I;
+              if constexpr (SPR && t >= ST0 && (t - ST0) % SDT == 0 && (t - ST0) / SDT < (NEWC + 3) / 4)
+                issue_grp(std::integral_constant<int, (t - ST0) / SDT>{});
+            };
+            if constexpr (!SPR) static_for<0, (NEWC + 3) / 4>(issue_grp);
+            const int mark1 = issued + NEWC;
             stamp(0);
-            wait_tile(issued - mark);
+            wait_tile(issued - mark + (SPR ? 0 : NEWC));
+            issued += NEWC;
             stamp(1);
             f2v* buf = &ring[b][0];
             f4v h0 = lds_read_b128<0>(buf + NEWC * 128 + 2 * lane), h1;
@@ -916,22 +1077,33 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
             if constexpr (FUSED && T <= 127) {
               if (pend) {                    // previous block's audio, interleaved into this FIR
                 float o0, o1, o2;
-                fir_audio_tile<T, 2, 2>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2);
+                if constexpr (AB_NOAUD || AB_NOLDS) {
+                  fe_fir_tile<T, D, R, FM, RING_PF, true>(buf, lane, tp, ai, aq, spread);
+                  o0 = ai[0]; o1 = ai[1]; o2 = ai[2];
+                } else {
+                  fir_audio_tile<T, 2, 2>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2, spread);
+                }
                 aud_drained = audio_store(q_pend, o0, o1, o2);
                 dh_shift(true);
                 pend = false;
               } else {
-                fe_fir_tile<T, D, R, 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
+                fe_fir_tile<T, D, R, FM, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq, spread);
               }
             } else {
-              fe_fir_tile<T, D, R, 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
+              fe_fir_tile<T, D, R, FM, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq, spread);
             }
+            gn += D * TO * 8;
             lds_wait<0>(h0);
             lds_write_b128(&ring[b ^ 1][0] + 2 * lane, h0);
             if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(&ring[b ^ 1][0] + 128 + 2 * lane, h1); }
             stamp(2);
             float d[R];
-            fast_epi(ai, aq, d);
+            if constexpr (AB_NOEPI) {
+#pragma unroll
+              for (int r = 0; r < R; ++r) d[r] = ai[r] + aq[r];
+            } else {
+              fast_epi(ai, aq, d);
+            }
             stamp(3);
             if constexpr (!FUSED) {
               typedef float f3v __attribute__((ext_vector_type(3)));
@@ -973,7 +1145,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     const int64_t nl1 = (s1 == s) ? nl + D * TO : n_lo_of(0);
     int kind1 = 0, mark1 = 0;
     if (u + 1 < U) {
-      if (s1 == s && MODE != 2 && MODE != 5 && nl1 + L <= p.n && nl1 + HCH * 128 >= -p.hist) kind1 = 3;
+      if (s1 == s && MB != 2 && MB != 5 && nl1 + L <= p.n && nl1 + HCH * 128 >= -p.hist) kind1 = 3;
       else kind1 = interior(nl1) ? 2 : 1;
       if (kind1 >= 2) {
         issue(s1, nl1, b ^ 1, kind1 == 2);
@@ -985,14 +1157,16 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     const int64_t m0 = (int64_t)TO * i;
     stamp(0);
     // ---- this tile's image ----
-    if (kind >= 2) {
+    if (kind == 4) {
+      // resident: written by the staged run (the FIR's LDS waits order it)
+    } else if (kind >= 2) {
       wait_tile(issued - mark);
     } else {
       const float* base = iqf + 2 * ((int64_t)s * p.stride);
       for (int e = lane; e < L; e += 64) {
         const int64_t nn = nl + e;
         f2v x = f2v{0.f, 0.f};
-        if (MODE == 2) x = f2v{(float)e * 1e-4f, (float)lane};
+        if (MB == 2) x = f2v{(float)e * 1e-4f, (float)lane};
         else if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
         buf[e] = x;
       }
@@ -1008,7 +1182,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     }
 
     float ai[R], aq[R];
-    fe_fir_tile<T, D, R, (MODE == 1 || MODE == 4 || MODE == 5) ? 1 : 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
+    fe_fir_tile<T, D, R, (MB == 1 || MB == 4 || MB == 5) ? 1 : 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
 
     if (kind1 == 3) {
       lds_wait<0>(h0);
@@ -1021,7 +1195,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     // ---- epilogue ----
     float d[R];
     const bool fast = i >= 1 && m0 + TO < M && p.i_ds == nullptr && have;
-    if (MODE == 4 || MODE == 5) {          // tuning: memory pipeline only
+    if (MB == 4 || MB == 5) {          // tuning: memory pipeline only
       carry += ai[0] + aq[0];
       d[0] = d[1] = d[2] = carry;
     } else if (fast) {
@@ -1050,7 +1224,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     }
 
     stamp(3);
-    if constexpr (FUSED && (MODE < 4 || MODE == 6)) {
+    if constexpr (FUSED && (MB < 4 || MB == 6)) {
       const bool warm = (i + 1) % TPB == 0 && u == 0 && U % TPB == 1;
       if (fused_tail(i, warm, d, s1 == s)) mark1 = 0;
     }
@@ -1067,7 +1241,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     kind = kind1; mark = mark1;
     b ^= 1;
   }
-  if constexpr (MODE == 6) {
+  if constexpr (MB == 6) {
     if (lane == 0) {
       uint64_t* o = reinterpret_cast<uint64_t*>(p.q_ds) + 8 * blockIdx.x;
       for (int k = 0; k < 5; ++k) o[k] = tph[k];

@@ -99,6 +99,23 @@ __device__ __forceinline__ void lds_write_b128(void* lds_base, const f4v& v) {
   asm volatile("ds_write_b128 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 
+// 16-B-per-lane non-temporal load into AGPRs (saddr form): the caller owns vmcnt.  AGPRs
+// (the upper half of the 512-entry file at one wave per SIMD) hold in-flight staging data
+// the compiler never needs for arithmetic, so it has no reason to copy a register whose
+// load has not landed (a VGPR destination above 256 live registers gets "spilled" to an
+// AGPR right after the load instruction, i.e. before the data arrives).
+template <int OFF>
+__device__ __forceinline__ void gload16_nt_a(f4v& dst, unsigned voff, const void* sbase) {
+  static_assert(OFF >= 0 && OFF < 4096, "12-bit immediate");
+  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3 nt" : "=a"(dst) : "v"(voff), "s"(sbase), "i"(OFF) : "memory");
+}
+// ds_write_b128 of AGPR data with an immediate offset (16-bit).
+template <int OFF>
+__device__ __forceinline__ void lds_write_b128_a(unsigned lds_addr, const f4v& v) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16-bit");
+  asm volatile("ds_write_b128 %0, %1 offset:%2" : : "v"(lds_addr), "a"(v), "i"(OFF) : "memory");
+}
+
 // N consecutive 1-KiB chunks by 16-B-per-lane LDS-DMA in the saddr form: wave-uniform
 // global base in an SGPR pair + per-lane 32-bit byte offset; the immediate offset is
 // applied to BOTH the global and the LDS address (M0 = LDS byte address), so up to four

@@ -1,0 +1,122 @@
+// A/B harness (not part of the product): times variants of the ring kernels interleaved
+// in one process (rounds x variants, 10 launches each) and prints median / min per
+// launch, so box-to-box and clock drift cancel out of the comparison.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/ab_tune.hip -o tools/ab_tune
+// usage: tools/ab_tune [rounds]
+#include "../real-time-software-defined-radio_amd/csrc/fe.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+struct Variant {
+  std::string name;
+  double bytes;
+  std::function<void(hipStream_t)> launch;
+  std::vector<float> us;
+};
+
+template <int MODE>
+void ring_fused(FeParams p, const TapsF32& taps, const float* ataps, float* audio, hipStream_t st) {
+  const int64_t M = (p.n + 9) / 10;
+  RingArgs ra{};
+  ra.ab = (int)((M + 959) / 960);
+  ra.tps = 5 * ra.ab;
+  ra.total = (int64_t)ra.ab * p.nstreams;
+  ra.audio = audio; ra.audio_stride = (M + 4) / 5; ra.ataps = ataps;
+  const int64_t slots = 256LL * 4;
+  ra.per_wave = (int)((ra.total + slots - 1) / slots);
+  const int grid = (int)((ra.total + ra.per_wave - 1) / ra.per_wave);
+  p.tiles_per_stream = ra.tps;
+  p.demod = nullptr;
+  hipLaunchKernelGGL((fe_ring_kernel<101, true, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
+}
+
+template <int MODE>
+void ring_fe(FeParams p, const TapsF32& taps, hipStream_t st) {
+  const int64_t M = (p.n + 9) / 10;
+  RingArgs ra{};
+  ra.tps = (int)((M + 191) / 192);
+  ra.total = (int64_t)ra.tps * p.nstreams;
+  const int64_t slots = 256LL * 4;
+  ra.per_wave = (int)((ra.total + slots - 1) / slots);
+  const int grid = (int)((ra.total + ra.per_wave - 1) / ra.per_wave);
+  p.tiles_per_stream = ra.tps;
+  p.vec_out = 1;
+  hipLaunchKernelGGL((fe_ring_kernel<101, false, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
+}
+
+int main(int argc, char** argv) {
+  const int rounds = argc > 1 ? atoi(argv[1]) : 8;
+  const char* sel = argc > 2 ? argv[2] : "";
+  const int64_t n = 64LL * 1024000;  // complex samples
+  const int64_t M = n / 10;
+  float *iq, *out, *aud;
+  CK(hipMalloc(&iq, n * 8));
+  CK(hipMalloc(&out, n * 8));
+  CK(hipMalloc(&aud, (M / 5 + 64) * 4));
+  std::vector<float> h(2 * n);
+  for (int64_t i = 0; i < 2 * n; ++i) h[i] = (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f;
+  CK(hipMemcpy(iq, h.data(), n * 8, hipMemcpyHostToDevice));
+  hipStream_t st; CK(hipStreamCreate(&st));
+  TapsF32 taps{}; for (int k = 0; k < 101; ++k) taps.h[k] = 0.01f * (k % 7);
+  float* tdev; CK(hipMalloc(&tdev, 1024)); CK(hipMemcpy(tdev, taps.h, 1024, hipMemcpyHostToDevice));
+  FeParams p{};
+  p.iq = iq; p.n = n; p.stride = n; p.hist = 0; p.nstreams = 1; p.taps_dev = tdev; p.demod = out; p.out_stride = M;
+  const double fb = n * 8.0 + (M / 5) * 4.0, eb = n * 8.0 + M * 4.0;
+  std::vector<Variant> v;
+#define FV(NAME, MODE) v.push_back({NAME, fb, [&](hipStream_t s) { ring_fused<MODE>(p, taps, tdev, aud, s); }, {}})
+#define EV(NAME, MODE) v.push_back({NAME, eb, [&](hipStream_t s) { ring_fe<MODE>(p, taps, s); }, {}})
+  FV("fused default", 0x00);
+  FV("fused stg2", 0x1000);
+  FV("fused stg3", 0x2000);
+  FV("fused stg4", 0x3000);
+  FV("fused DMA only", 0x05);
+  EV("fe default", 0x00);
+  EV("fe stg2", 0x1000);
+  EV("fe stg3", 0x2000);
+  if (*sel) v.erase(std::remove_if(v.begin(), v.end(), [&](const Variant& x) { return x.name.find(sel) == std::string::npos; }), v.end());
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  for (auto& x : v) for (int i = 0; i < 3; ++i) x.launch(st);
+  for (int i = 0; i < 400; ++i) v[0].launch(st);   // settle the clocks (~40 ms of load)
+  CK(hipStreamSynchronize(st));
+  const int it = 10;
+  for (int r = 0; r < rounds; ++r)
+    for (auto& x : v) {
+      CK(hipEventRecord(a, st));
+      for (int i = 0; i < it; ++i) x.launch(st);
+      CK(hipEventRecord(b, st));
+      CK(hipEventSynchronize(b));
+      float ms; CK(hipEventElapsedTime(&ms, a, b));
+      x.us.push_back(ms * 1e3f / it);
+    }
+  CK(hipGetLastError());
+  // outputs vs the first variant of the same kind (the fused kernels write `aud`, FE `out`)
+  std::vector<float> ref_a(M / 5), ref_e(M), got(M);
+  bool have_a = false, have_e = false;
+  for (auto& x : v) {
+    const bool fused = x.bytes == fb;
+    CK(hipMemset(fused ? aud : out, 0, (fused ? M / 5 : M) * 4));
+    x.launch(st);
+    CK(hipStreamSynchronize(st));
+    const size_t cnt = fused ? M / 5 : M;
+    CK(hipMemcpy(got.data(), fused ? aud : out, cnt * 4, hipMemcpyDeviceToHost));
+    std::vector<float>& ref = fused ? ref_a : ref_e;
+    bool& have = fused ? have_a : have_e;
+    if (!have) { std::copy(got.begin(), got.begin() + cnt, ref.begin()); have = true; continue; }
+    double md = 0; size_t bad = 0;
+    for (size_t i = 0; i < cnt; ++i) { double d = fabs((double)got[i] - ref[i]); if (!(d <= md)) md = d; if (!(d < 1e-6)) ++bad; }
+    printf("%-24s vs first: max |diff| %.3g, %zu of %zu over 1e-6\n", x.name.c_str(), md, bad, cnt);
+  }
+  for (auto& x : v) {
+    std::sort(x.us.begin(), x.us.end());
+    const float med = x.us[x.us.size() / 2], mn = x.us[0];
+    printf("%-24s median %7.2f us (%6.1f GB/s, frac %.3f)  min %7.2f  max %7.2f\n", x.name.c_str(), med,
+           x.bytes / med / 1e3, x.bytes / med / 1e3 / 8000.0, mn, x.us.back());
+  }
+  return 0;
+}
