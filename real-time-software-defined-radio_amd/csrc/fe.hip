@@ -738,9 +738,12 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   __shared__ __attribute__((aligned(16))) f4v ptab[FUSED ? NW + 1 : 1];
 
   const int lane = threadIdx.x;
-  const int64_t u0 = (int64_t)blockIdx.x * a.per_wave;
-  if (u0 >= a.total) return;
-  const int nunits = (int)min<int64_t>(a.per_wave, a.total - u0);
+  // FUSED: balanced tile ranges [g0, g1) over a.total tiles; FE: runs of per_wave tiles
+  const int64_t g0 = FUSED ? (int64_t)blockIdx.x * a.total / gridDim.x : (int64_t)blockIdx.x * a.per_wave;
+  const int64_t g1 = FUSED ? ((int64_t)blockIdx.x + 1) * a.total / gridDim.x : min<int64_t>(g0 + a.per_wave, a.total);
+  if (g0 >= g1) return;
+  const int64_t u0 = g0;
+  const int nunits = (int)(g1 - g0);
   const int64_t M = (p.n + D - 1) / D;
 
   f2v tp[TP];
@@ -773,14 +776,16 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
 
   // tile sequence of this wave
   int s, i, U;
+  bool mid = false;
   if constexpr (FUSED) {
-    s = (int)(u0 / a.ab);
-    const int q0 = (int)(u0 - (int64_t)s * a.ab);
-    i = TPB * q0 - (q0 > 0 ? 1 : 0);
-    U = nunits * TPB + (q0 > 0 ? 1 : 0);
-    if (q0 == 0)
-      for (int e = lane; e < HA; e += 64) dh[e] = 0.f;          // stream start: zero history
-    for (int e = lane; e < 4; e += 64) dh[HA + BD + e] = 0.f;
+    // a run starting mid-stream first runs the warm-up tile i0-1 (history / predecessor);
+    // a run may start and end mid audio block (audio_store keeps to the outputs it owns)
+    s = (int)(u0 / a.tps);
+    const int i0 = (int)(u0 - (int64_t)s * a.tps);
+    mid = i0 > 0;
+    i = i0 - (mid ? 1 : 0);
+    U = nunits + (mid ? 1 : 0);
+    for (int e = lane; e < HA + BD + 4; e += 64) dh[e] = 0.f;   // finite everywhere (0 * x)
     for (int w = lane; w < NW + 1; w += 64) {               // entry NW: zero (pairs over-read)
       const int k0 = (TA - 1) - w, k1 = k0 + DA, k2 = k0 + 2 * DA;
       ptab[w] = f4v{(k0 >= 0 && k0 < TA) ? a.ataps[k0] : 0.f, (k1 >= 0 && k1 < TA) ? a.ataps[k1] : 0.f,
@@ -851,18 +856,23 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     o2 = a2a + a2b;
   };
   auto audio_store = [&](int64_t q, float o0, float o1, float o2) -> bool {
-    const int64_t A = (M + DA - 1) / DA;
+    // outputs of stream s this run owns: 5 j inside its tile range (each output is
+    // stored by exactly one wave)
+    const int64_t lo = max<int64_t>(g0 - (int64_t)s * a.tps, 0);
+    const int64_t hi = min<int64_t>(g1 - (int64_t)s * a.tps, a.tps);
+    const int64_t jlo = (TO * lo + DA - 1) / DA;
+    const int64_t A = min<int64_t>((TO * hi + DA - 1) / DA, (M + DA - 1) / DA);
     const int64_t j = q * BO + RA * lane;
     float* ao = a.audio + (int64_t)s * a.audio_stride + j;
-    if (q * BO + BO <= A) {
+    if (q * BO >= jlo && q * BO + BO <= A) {
       typedef float f3v __attribute__((ext_vector_type(3)));
       *reinterpret_cast<f3v*>(ao) = f3v{o0, o1, o2};
       issued += 1;
       return false;
     }
-    if (j < A) ao[0] = o0;
-    if (j + 1 < A) ao[1] = o1;
-    if (j + 2 < A) ao[2] = o2;
+    if (j >= jlo && j < A) ao[0] = o0;
+    if (j + 1 >= jlo && j + 1 < A) ao[1] = o1;
+    if (j + 2 >= jlo && j + 2 < A) ao[2] = o2;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     issued = 0;
     return true;
@@ -884,10 +894,10 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   };
   // FUSED (general path): demod values of tile i -> history; after the block's last tile,
   // the block's audio outputs and the history shift.  Returns true if vmcnt was drained.
-  auto fused_tail = [&](int i, bool warm, const float (&d)[R], bool next_same) -> bool {
+  auto fused_tail = [&](int i, bool warm, const float (&d)[R], bool next_same, bool last = false) -> bool {
     dh_write(i, warm, d);
     const int ib = i - TPB * (i / TPB);
-    if (warm || ib != TPB - 1) return false;
+    if (warm || (ib != TPB - 1 && !last)) return false;
     float o0, o1, o2;
     audio_compute(o0, o1, o2);
     const bool drained = audio_store(i / TPB, o0, o1, o2);
@@ -1225,8 +1235,8 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
 
     stamp(3);
     if constexpr (FUSED && (MB < 4 || MB == 6)) {
-      const bool warm = (i + 1) % TPB == 0 && u == 0 && U % TPB == 1;
-      if (fused_tail(i, warm, d, s1 == s)) mark1 = 0;
+      const bool warm = (i + 1) % TPB == 0 && u == 0 && mid;   // warm-up tile = previous block's last
+      if (fused_tail(i, warm, d, s1 == s, u + 1 == U && !(u == 0 && mid))) mark1 = 0;
     }
 
     stamp(4);
@@ -1560,6 +1570,341 @@ __global__ void iq_zf_kernel(const void* iq_all, int64_t n, int64_t stride, cons
   zf_q[k] = sq;
 }
 
+// ---------------------------------------------------------------------------------
+// fe_slot_kernel: the f32 front end at two waves per SIMD (T <= 127).
+//
+// fe_ring_kernel holds two 16-KiB image slots per wave, hence one wave per SIMD: its VALU
+// issues ~35 % of the time and a wave's per-tile work (FIR + epilogue + audio, ~2.7 us)
+// is longer than the memory system needs to deliver the next tile, so that launch is
+// issue/latency-bound.  Here a wave holds ONE slot: the next tile's 15 new
+// 1-KiB chunks are loaded into AGPRs (16 B per lane each) while the current tile is
+// filtered, and written into the slot after the FIR (the halo chunk moves from position
+// 15 to 0 through a VGPR).  Half the LDS lets a second wave share each SIMD and issue
+// while the first one waits.
+//  * Work: contiguous, balanced tile ranges (tile granularity).
+//  * FUSED (sdr_fe_mono_dev): the 5 tiles of an audio block keep their demod values in
+//    VGPRs (3 per lane per tile) plus the previous block's last tile (the 150-sample
+//    history).  After the block's last FIR the slot is free: history and block are
+//    written into it and the audio FIR (outputs 3l..3l+2 of lane l) reads them there,
+//    before the next image is written.  A run starting mid-stream first runs one warm-up
+//    tile; a run ending mid-block computes that block from the tiles it has.  Audio output
+//    j is stored by the wave whose tile range holds its newest input sample 5j, so every
+//    output is written exactly once.
+// ---------------------------------------------------------------------------------
+struct SlotArgs {
+  int64_t total;        // tiles over all streams
+  int tps;              // tiles per stream (FUSED: 5 x audio blocks)
+  float* audio;         // FUSED: ceil(M/5) outputs per stream, audio_stride apart
+  int64_t audio_stride;
+  const float* ataps;   // FUSED: 151 audio taps (device)
+};
+
+// audio FIR of one block (a[j] = sum_k g[k] d[5j - k]): lane l -> outputs 3l..3l+2 over
+// its 161-sample window aw = dh + HA - 150 + 15 l; tap triples {g[150-w], g[155-w],
+// g[160-w]} by broadcast ds_read_b128 of ptab; reads issued APF steps ahead, counted waits
+__device__ __forceinline__ void audio_block3(const float* aw, const f4v* ptab, float& o0, float& o1,
+                                             float& o2) {
+  asm volatile("" ::: "memory");
+  f2v acc01a = f2v{0.f, 0.f}, acc01b = f2v{0.f, 0.f};
+  float a2a = 0.f, a2b = 0.f;
+  constexpr int NS = 81, APF = 5;   // 3*APF <= 15 (lgkmcnt field)
+  f2v xq[NS];
+  f4v ta[NS], tb[NS];
+  auto rd = [&](auto K) {
+    constexpr int k = K;
+    xq[k] = lds_read2_b32<2 * k, 2 * k + 1>(aw);
+    ta[k] = lds_read_b128<32 * k>(ptab);
+    tb[k] = lds_read_b128<32 * k + 16>(ptab);
+  };
+  static_for<0, APF>(rd);
+  static_for<0, NS>([&](auto K) {
+    constexpr int k = K;
+    if constexpr (k + APF < NS) {
+      rd(std::integral_constant<int, k + APF>{});
+      lds_wait3<3 * APF>(xq[k], ta[k], tb[k]);
+    } else {
+      lds_wait3<3 * (NS - 1 - k)>(xq[k], ta[k], tb[k]);
+    }
+    pk_fma_bcast_x_ordered<false>(acc01a, f2v{ta[k].x, ta[k].y}, xq[k]);
+    pk_fma_bcast_x_ordered<true>(acc01b, f2v{tb[k].x, tb[k].y}, xq[k]);
+    fmac_ordered(a2a, ta[k].z, xq[k].x);
+    fmac_ordered(a2b, tb[k].z, xq[k].y);
+  });
+  o0 = acc01a.x + acc01b.x;
+  o1 = acc01a.y + acc01b.y;
+  o2 = a2a + a2b;
+}
+
+// PF: FIR reads in flight; VST: stage in VGPRs (true) or AGPRs (false)
+// MB (tuning only; 0 = product): 1 = no FIR (memory pipeline + epilogue)
+template <int T, bool FUSED, int PF = 4, bool VST = true, int MB = 0>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
+  constexpr int D = 10, R = 3, TO = 64 * R;
+  constexpr int NEWC = D * TO / 128;                 // 15 new 1-KiB chunks per tile
+  constexpr int NCH = (D * TO + T + 1 + 127) / 128;  // chunks per tile image
+  constexpr int L = NCH * 128;                       // image length (complex samples)
+  constexpr int TP = (T + 1) / 2;
+  static_assert((T & 1) == 1 && NCH == NEWC + 1, "odd tap counts up to 127 (one halo chunk)");
+  constexpr int TA = 151, DA = 5, BO = 64 * R, HA = 152, NW = DA * (R - 1) + TA;
+  static_assert((HA + TO * DA + 4) * 4 <= L * 8, "audio history + block fit in the slot");
+  __shared__ __attribute__((aligned(16))) f2v slot[L];
+  __shared__ __attribute__((aligned(16))) f4v ptab[FUSED ? NW + 1 : 1];
+  float* const dh = reinterpret_cast<float*>(&slot[0]);   // FUSED audio window, aliases the slot
+
+  const int lane = threadIdx.x;
+  const int64_t g0 = (int64_t)blockIdx.x * a.total / gridDim.x;
+  const int64_t g1 = ((int64_t)blockIdx.x + 1) * a.total / gridDim.x;
+  if (g0 >= g1) return;
+  const int64_t M = (p.n + D - 1) / D;
+
+  // FE taps as VGPR pairs {h[2j], h[2j+1]}: held for the whole launch (FE), or re-read from
+  // an LDS table before each tile's FIR (FUSED: frees the registers for the audio FIR)
+  __shared__ __attribute__((aligned(16))) f2v tlds[FUSED ? TP + 1 : 1];
+  f2v tp[TP];
+  if constexpr (FUSED) {
+    for (int j = lane; j < TP + 1; j += 64)
+      tlds[j] = (j < TP) ? f2v{p.taps_dev[2 * j], (2 * j + 1 < T) ? p.taps_dev[2 * j + 1] : 0.f} : f2v{0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int j = 0; j < TP; ++j) tp[j] = f2v{taps.h[2 * j], (2 * j + 1 < T) ? taps.h[2 * j + 1] : 0.f};
+#pragma unroll
+    for (int j = 0; j < TP; ++j) asm volatile("" : "+v"(tp[j]));
+  }
+  // this lane's taps for the cooperative predecessor output (a run's first tile), loaded
+  // before any stage load is in flight
+  const float hk0 = p.taps_dev[lane];
+  const float hk1 = (lane + 64 < T) ? p.taps_dev[lane + 64] : 0.f;
+  if constexpr (FUSED) {
+    for (int w = lane; w < NW + 1; w += 64) {               // entry NW: zero (pairs over-read)
+      const int k0 = (TA - 1) - w, k1 = k0 + DA, k2 = k0 + 2 * DA;
+      ptab[w] = f4v{(k0 >= 0 && k0 < TA) ? a.ataps[k0] : 0.f, (k1 >= 0 && k1 < TA) ? a.ataps[k1] : 0.f,
+                    (k2 >= 0 && k2 < TA) ? a.ataps[k2] : 0.f, 0.f};
+    }
+  }
+  const unsigned voff = 16u * lane;
+  const float* iqf = reinterpret_cast<const float*>(p.iq);
+  // tile (s, i): outputs TO*i ..; image = samples [n_lo, n_lo + L), n_lo = D*(m0-1) - (T-1)
+  auto n_lo_of = [&](int ii) { return (int64_t)(D * TO) * ii - D - (T - 1); };
+  auto interior = [&](int64_t nl) { return nl >= -p.hist && nl + L <= p.n; };
+
+  // whole image into the slot, waited for (run start, stream change, stream head / tail):
+  // LDS-DMA when interior, else guarded loads (zeros outside [-hist, n))
+  auto build_sync = [&](int ss, int64_t nl) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (interior(nl)) {
+      const char* g = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)ss * p.stride + nl));
+      const unsigned lb = lds_addr_of(slot);
+      static_for<0, (NCH + 3) / 4>([&](auto Q) {
+        constexpr int c = 4 * Q;
+        constexpr int n = (NCH - c) < 4 ? (NCH - c) : 4;
+        glds16x<n>(voff, g + 1024 * c, lb + 1024 * c);
+      });
+    } else {
+      const float* base = iqf + 2 * ((int64_t)ss * p.stride);
+      for (int e = lane; e < L; e += 64) {
+        const int64_t nn = nl + e;
+        f2v x = f2v{0.f, 0.f};
+        if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
+        slot[e] = x;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  };
+  // the next tile's new chunks [1, NCH) -> AGPR stage (16 B per lane per chunk)
+  f4v stg[NEWC];
+  auto load_stage = [&](int ss, int64_t nl) {
+    const char* gl = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)ss * p.stride + nl)) + 1024;
+    static_for<0, NEWC>([&](auto C) {
+      constexpr int c = C;
+      if constexpr (VST) gload16_nt_v<1024 * (c % 4)>(stg[c], voff, gl + 4096 * (c / 4));
+      else gload16_nt_a<1024 * (c % 4)>(stg[c], voff, gl + 4096 * (c / 4));
+    });
+  };
+
+  int s = (int)(g0 / a.tps);
+  int i = (int)(g0 - (int64_t)s * a.tps);
+  const bool warm0 = FUSED && i > 0;                   // FUSED: warm-up tile i-1 first
+  if (warm0) --i;
+  const int U = (int)(g1 - g0) + (warm0 ? 1 : 0);
+  // FUSED: the audio outputs of stream s this run stores (5 j inside its tile range)
+  int64_t jlo = 0, jhi = 0;
+  auto own = [&]() {
+    const int64_t lo = max<int64_t>(g0 - (int64_t)s * a.tps, 0);
+    const int64_t hi = min<int64_t>(g1 - (int64_t)s * a.tps, a.tps);
+    jlo = (TO * lo + DA - 1) / DA;
+    jhi = min<int64_t>((TO * hi + DA - 1) / DA, (M + DA - 1) / DA);
+  };
+  if constexpr (FUSED) own();
+
+  build_sync(s, n_lo_of(i));
+  float carry = 0.f;
+  bool have = false;
+  int wacc = 0;
+  float dblk[DA][R], hist[R];                          // FUSED: demod of the block's tiles
+#pragma unroll
+  for (int k = 0; k < DA; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) dblk[k][r] = 0.f;
+#pragma unroll
+  for (int r = 0; r < R; ++r) hist[r] = 0.f;
+  auto next_of = [&](int ss, int ii, int& s1, int& i1) {
+    s1 = ss;
+    i1 = ii + 1;
+    if (i1 == a.tps) { i1 = 0; ++s1; }
+  };
+  int s1, i1;
+  next_of(s, i, s1, i1);
+  bool stg1 = U > 1 && s1 == s && interior(n_lo_of(i1));   // next image comes through the stage
+  if (stg1) load_stage(s1, n_lo_of(i1));
+
+  for (int u = 0; u < U; ++u) {
+    const bool lastu = (u + 1 == U);
+    f4v h0;
+    if (stg1) h0 = lds_read_b128<0>(slot + NEWC * 128 + 2 * lane);   // halo of the next tile
+    if constexpr (FUSED) {
+      constexpr int NQ = (TP + 1) / 2;
+      f4v tq[NQ];
+      static_for<0, NQ>([&](auto K) { tq[K] = lds_read_b128<16 * K>(tlds); });
+      static_for<0, NQ>([&](auto K) { lds_wait<0>(tq[K]); });
+      static_for<0, TP>([&](auto J) {
+        constexpr int j = J;
+        tp[j] = (j & 1) ? f2v{tq[j / 2].z, tq[j / 2].w} : f2v{tq[j / 2].x, tq[j / 2].y};
+      });
+    }
+    float ai[R], aq[R];
+    fe_fir_tile<T, D, R, MB == 1 ? 1 : 0, PF, true>(slot, lane, tp, ai, aq);
+    const int64_t m0 = (int64_t)TO * i;
+    float d[R];
+    bool st_fe = false;
+    if (i >= 1 && m0 + TO < M && p.i_ds == nullptr && have) {
+      // interior tile: phases, predecessor (DPP / carry), np.unwrap wrap
+      float phi[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) phi[r] = fast_atan2f(aq[r], ai[r]);
+      const float from_left = __int_as_float(__builtin_amdgcn_update_dpp(
+          0, __float_as_int(phi[R - 1]), 0x138 /*wave_shr:1*/, 0xf, 0xf, false));
+      float prev = (lane == 0) ? carry : from_left;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float dd = phi[r] - prev;
+        if (dd > kPiF) { dd -= k2PiF; wacc -= 1; }
+        else if (dd < -kPiF) { dd += k2PiF; wacc += 1; }
+        d[r] = dd;
+        prev = phi[r];
+      }
+      carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[R - 1]), 63));
+      st_fe = !FUSED;
+    } else {
+      float si = 0.f, sq = 0.f;
+      if (m0 > 0 && !have) {           // output m0-1 (the predecessor): image samples [0, T)
+        const f2v x0 = slot[(T - 1) - lane];
+        si = fmaf(hk0, x0.x, si);
+        sq = fmaf(hk0, x0.y, sq);
+        if (lane + 64 < T) {
+          const f2v x1 = slot[(T - 1) - (lane + 64)];
+          si = fmaf(hk1, x1.x, si);
+          sq = fmaf(hk1, x1.y, sq);
+        }
+        si = wave_sum(si);
+        sq = wave_sum(sq);
+      }
+      carry = fe_epilogue<T, D, R>(p, s, M, m0, lane, ai, aq, si, sq, have, carry, nullptr, d, !FUSED);
+    }
+
+    // FUSED: block bookkeeping and, after the block's last tile (or the run's), its audio
+    const int sp = s;
+    const int64_t jlo_t = jlo, jhi_t = jhi;
+    bool aud = false;
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+    int64_t qa = 0;
+    if constexpr (FUSED) {
+      const int ib = i % DA;
+#pragma unroll
+      for (int k = 0; k < DA; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) dblk[k][r] = (ib == k) ? d[r] : dblk[k][r];
+      if (!(warm0 && u == 0) && (ib == DA - 1 || lastu)) {
+        // the slot is free (the FIR's and epilogue's reads have returned)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane >= 14) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) dh[HA - 150 + 3 * (lane - 14) + r] = hist[r];
+        }
+#pragma unroll
+        for (int k = 0; k < DA; ++k)
+#pragma unroll
+          for (int r = 0; r < R; ++r) dh[HA + TO * k + R * lane + r] = dblk[k][r];
+        if (lane < 4) dh[HA + TO * DA + lane] = 0.f;
+        audio_block3(dh + (HA - (TA - 1) + DA * R * lane), ptab, o0, o1, o2);
+        aud = true;
+        qa = i / DA;
+      }
+      if (ib == DA - 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) hist[r] = dblk[DA - 1][r];
+      }
+    }
+
+    if ((s1 != s || lastu) && p.wraps != nullptr) {
+      const int w = wave_sum_i(wacc);
+      if (lane == 0 && w != 0) atomicAdd(p.wraps + s, w);
+      wacc = 0;
+    }
+    if (!lastu) {
+      // next image into the slot, then the loads of the one after it
+      if (stg1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_wait<0>(h0);
+        lds_write_b128(slot + 2 * lane, h0);
+        const unsigned na = lds_addr_of(slot) + 16u * lane;
+        static_for<0, NEWC>([&](auto C) {
+          constexpr int c = C;
+          if constexpr (VST) {
+            asm volatile("" : "+v"(stg[c]));
+            lds_write_b128_v<1024 * (1 + c)>(na, stg[c]);
+          } else {
+            asm volatile("" : "+a"(stg[c]));
+            lds_write_b128_a<1024 * (1 + c)>(na, stg[c]);
+          }
+        });
+      } else {
+        build_sync(s1, n_lo_of(i1));
+      }
+      have = (s1 == s);
+      if (FUSED && !have) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) hist[r] = 0.f;
+      }
+      s = s1;
+      i = i1;
+      if (FUSED && !have) own();
+      next_of(s, i, s1, i1);
+      stg1 = u + 2 < U && s1 == s && interior(n_lo_of(i1));
+      if (stg1) load_stage(s1, n_lo_of(i1));
+    }
+    // the finished tile's stores, queued behind the next tile's loads
+    if (st_fe) {
+      typedef float f3v __attribute__((ext_vector_type(3)));
+      *reinterpret_cast<f3v*>(p.demod + (int64_t)sp * p.out_stride + m0 + R * lane) = f3v{d[0], d[1], d[2]};
+    }
+    if constexpr (FUSED) {
+      if (aud) {
+        const int64_t j0 = qa * BO, j = j0 + R * lane;
+        float* ao = a.audio + (int64_t)sp * a.audio_stride + j;
+        if (j0 >= jlo_t && j0 + BO <= jhi_t) {
+          typedef float f3v __attribute__((ext_vector_type(3)));
+          *reinterpret_cast<f3v*>(ao) = f3v{o0, o1, o2};
+        } else {
+          if (j >= jlo_t && j < jhi_t) ao[0] = o0;
+          if (j + 1 >= jlo_t && j + 1 < jhi_t) ao[1] = o1;
+          if (j + 2 >= jlo_t && j + 2 < jhi_t) ao[2] = o2;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------
@@ -1604,6 +1949,27 @@ static bool use_circ() {
   }();
   return c;
 }
+// fe_slot_kernel (two waves per SIMD): the default for the FE-only launch at T <= 127
+// (r01 A/B: 104 vs 111 us per 65.5 M samples); the fused launch keeps fe_ring_kernel (95 vs
+// 100 us), unless SDR_FE_KERNEL=slot / ring / circ picks one family for both
+static bool use_slot(bool fused) {
+  static const int c = [] {
+    const char* e = getenv("SDR_FE_KERNEL");
+    return !e ? 0 : (strcmp(e, "slot") == 0 ? 1 : 2);
+  }();
+  return c == 1 || (c == 0 && !fused);
+}
+
+template <int T, bool FUSED>
+static hipError_t launch_slot_t(FeParams p, const TapsF32& taps, SlotArgs sa, hipStream_t st) {
+  if (sa.total <= 0) return hipSuccess;
+  static const int wpc = resident_per_cu(fe_slot_kernel<T, FUSED>, 64);
+  const int64_t slots = (int64_t)cu_count() * std::max(1, std::min(wpc, 8));
+  const int64_t grid = std::min<int64_t>(slots, sa.total);
+  p.tiles_per_stream = sa.tps;
+  hipLaunchKernelGGL((fe_slot_kernel<T, FUSED>), dim3((unsigned)grid), dim3(64), 0, st, p, taps, sa);
+  return hipGetLastError();
+}
 
 template <int T, int D, bool U8>
 static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
@@ -1625,6 +1991,14 @@ static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
   if constexpr (U8) {
     hipLaunchKernelGGL((fe_kernel<T, D, R, NT, true>), dim3((unsigned)tiles), dim3(NT), 0, st, p, *a.taps);
   } else {
+    if constexpr (T <= 127) {
+      if (use_slot(false)) {
+        SlotArgs sa{};
+        sa.tps = (int)((M + 191) / 192);
+        sa.total = (int64_t)sa.tps * a.nstreams;
+        return launch_slot_t<T, false>(p, *a.taps, sa, st);
+      }
+    }
     if (use_circ()) {
       RingArgs ra{};
       ra.tps = (int)((M + 63) / 64);
@@ -1679,6 +2053,13 @@ static hipError_t launch_fe_mono_t(const FeLaunch& a, const float* ataps, float*
   if (ra.total <= 0) return hipSuccess;
   if (ra.total > 0x7fffffff / 5) return hipErrorInvalidValue;
   ra.audio = audio; ra.audio_stride = audio_stride; ra.ataps = ataps;
+  if (use_slot(true)) {
+    SlotArgs sa{};
+    sa.tps = ra.tps;
+    sa.total = (int64_t)sa.tps * a.nstreams;
+    sa.audio = audio; sa.audio_stride = audio_stride; sa.ataps = ataps;
+    return launch_slot_t<T, true>(p, *a.taps, sa, st);
+  }
   if (use_circ()) {
     ra.ab = (int)((M + 319) / 320);
     ra.tps = 5 * ra.ab;
@@ -1693,8 +2074,8 @@ static hipError_t launch_fe_mono_t(const FeLaunch& a, const float* ataps, float*
   }
   static const int wpc = resident_per_cu(fe_ring_kernel<T, true>, 64);
   const int64_t slots = (int64_t)cu_count() * std::min(wpc, 4);
-  ra.per_wave = (int)((ra.total + slots - 1) / slots);
-  const int64_t grid = (ra.total + ra.per_wave - 1) / ra.per_wave;
+  ra.total = (int64_t)ra.tps * a.nstreams;           // tiles: balanced tile ranges per wave
+  const int64_t grid = std::min<int64_t>(slots, ra.total);
   p.tiles_per_stream = ra.tps;
   hipLaunchKernelGGL((fe_ring_kernel<T, true>), dim3((unsigned)grid), dim3(64), 0, st, p, *a.taps, ra);
   return hipGetLastError();

@@ -109,6 +109,17 @@ __device__ __forceinline__ void gload16_nt_a(f4v& dst, unsigned voff, const void
   static_assert(OFF >= 0 && OFF < 4096, "12-bit immediate");
   asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3 nt" : "=a"(dst) : "v"(voff), "s"(sbase), "i"(OFF) : "memory");
 }
+// the same into VGPRs (for kernels whose register budget leaves no room for an AGPR split)
+template <int OFF>
+__device__ __forceinline__ void gload16_nt_v(f4v& dst, unsigned voff, const void* sbase) {
+  static_assert(OFF >= 0 && OFF < 4096, "12-bit immediate");
+  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3 nt" : "=v"(dst) : "v"(voff), "s"(sbase), "i"(OFF) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void lds_write_b128_v(unsigned lds_addr, const f4v& v) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16-bit");
+  asm volatile("ds_write_b128 %0, %1 offset:%2" : : "v"(lds_addr), "v"(v), "i"(OFF) : "memory");
+}
 // ds_write_b128 of AGPR data with an immediate offset (16-bit).
 template <int OFF>
 __device__ __forceinline__ void lds_write_b128_a(unsigned lds_addr, const f4v& v) {

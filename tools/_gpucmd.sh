@@ -1,6 +1,6 @@
 set -e
-R=$(pwd)
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-cd /tmp
-timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_BUSY_CYCLES --kernel-trace -d $R/gpurun_out/clk -o clk --output-format csv -- $R/tools/ab_tune 2 fused > $R/gpurun_out/clk.log 2>&1
+timeout -k 10 120 tools/ab_tune 6 > gpurun_out/ab_slot3.log 2>&1
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_slot3.log 2>&1
+timeout -k 10 120 python3 bench.py --no-cpu > gpurun_out/bench_slot3.json
+timeout -k 10 120 python3 bench.py --no-cpu --path split > gpurun_out/bench_slot3_split.json

@@ -26,11 +26,9 @@ void ring_fused(FeParams p, const TapsF32& taps, const float* ataps, float* audi
   RingArgs ra{};
   ra.ab = (int)((M + 959) / 960);
   ra.tps = 5 * ra.ab;
-  ra.total = (int64_t)ra.ab * p.nstreams;
+  ra.total = (int64_t)ra.tps * p.nstreams;
   ra.audio = audio; ra.audio_stride = (M + 4) / 5; ra.ataps = ataps;
-  const int64_t slots = 256LL * 4;
-  ra.per_wave = (int)((ra.total + slots - 1) / slots);
-  const int grid = (int)((ra.total + ra.per_wave - 1) / ra.per_wave);
+  const int grid = (int)std::min<int64_t>(256LL * 4, ra.total);
   p.tiles_per_stream = ra.tps;
   p.demod = nullptr;
   hipLaunchKernelGGL((fe_ring_kernel<101, true, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
@@ -48,6 +46,24 @@ void ring_fe(FeParams p, const TapsF32& taps, hipStream_t st) {
   p.tiles_per_stream = ra.tps;
   p.vec_out = 1;
   hipLaunchKernelGGL((fe_ring_kernel<101, false, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
+}
+
+template <bool FUSED, int PF, bool VST, int MB = 0>
+void slot_launch(FeParams p, const TapsF32& taps, const float* ataps, float* audio, hipStream_t st, int wpc) {
+  const int64_t M = (p.n + 9) / 10;
+  SlotArgs sa{};
+  if (FUSED) {
+    sa.tps = 5 * (int)((M + 959) / 960);
+    sa.audio = audio; sa.audio_stride = (M + 4) / 5; sa.ataps = ataps;
+    p.demod = nullptr;
+  } else {
+    sa.tps = (int)((M + 191) / 192);
+    p.vec_out = 1;
+  }
+  sa.total = sa.tps;
+  p.tiles_per_stream = sa.tps;
+  const int grid = (int)std::min<int64_t>(256LL * wpc, sa.total);
+  hipLaunchKernelGGL((fe_slot_kernel<101, FUSED, PF, VST, MB>), dim3(grid), dim3(64), 0, st, p, taps, sa);
 }
 
 int main(int argc, char** argv) {
@@ -71,14 +87,13 @@ int main(int argc, char** argv) {
   std::vector<Variant> v;
 #define FV(NAME, MODE) v.push_back({NAME, fb, [&](hipStream_t s) { ring_fused<MODE>(p, taps, tdev, aud, s); }, {}})
 #define EV(NAME, MODE) v.push_back({NAME, eb, [&](hipStream_t s) { ring_fe<MODE>(p, taps, s); }, {}})
-  FV("fused default", 0x00);
-  FV("fused stg2", 0x1000);
-  FV("fused stg3", 0x2000);
-  FV("fused stg4", 0x3000);
-  FV("fused DMA only", 0x05);
-  EV("fe default", 0x00);
-  EV("fe stg2", 0x1000);
-  EV("fe stg3", 0x2000);
+#define SFV(NAME, PF, VST, WPC) v.push_back({NAME, fb, [&](hipStream_t s) { slot_launch<true, PF, VST>(p, taps, tdev, aud, s, WPC); }, {}})
+#define SEV(NAME, PF, VST, WPC) v.push_back({NAME, eb, [&](hipStream_t s) { slot_launch<false, PF, VST>(p, taps, nullptr, nullptr, s, WPC); }, {}})
+  FV("fused ring", 0x00);
+  FV("fused ring DMA only", 0x05);
+  SFV("fused slot pf4 v w8", 4, true, 8);
+  EV("fe ring", 0x00);
+  SEV("fe slot pf4 v w8", 4, true, 8);
   if (*sel) v.erase(std::remove_if(v.begin(), v.end(), [&](const Variant& x) { return x.name.find(sel) == std::string::npos; }), v.end());
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   for (auto& x : v) for (int i = 0; i < 3; ++i) x.launch(st);
