@@ -710,6 +710,12 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   // wave after the FIR of tile t (STG tiles in flight instead of one)
   constexpr int STG = (MODE & 0x3000) ? (((MODE >> 12) & 3) + 1) : RING_STG;
 
+  // A/B overrides (0 = defaults): bits 16-19 FE-FIR reads in flight, 20-22 / 24-26 the
+  // interleaved FE / audio read depths, 0x8000 operand-free LDS waits in the FE FIR
+  constexpr int PFR = ((MODE >> 16) & 15) ? ((MODE >> 16) & 15) : RING_PF;
+  constexpr int FPF = ((MODE >> 20) & 7) ? ((MODE >> 20) & 7) : 2;
+  constexpr int APFX = ((MODE >> 24) & 7) ? ((MODE >> 24) & 7) : 2;
+  constexpr bool SAFE = !(MODE & 0x8000);
   constexpr int SPR = SV == 0 ? RING_SPREAD : (SV == 1 ? 0 : 1);
   constexpr int ST0 = SV == 0 ? RING_SPREAD_T0 : (SV == 3 ? 4 : 2);
   constexpr int SDT = SV == 0 ? RING_SPREAD_DT : (SV == 2 ? 4 : (SV == 3 ? 14 : 8));
@@ -977,15 +983,15 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
         if constexpr (FUSED && T <= 127) {
           if (pend) {
             float o0, o1, o2;
-            fir_audio_tile<T, 2, 2>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2);
+            fir_audio_tile<T, FPF, APFX>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2);
             aud_drained = audio_store(q_pend, o0, o1, o2);
             dh_shift(true);
             pend = false;
           } else {
-            fe_fir_tile<T, D, R, 0, RING_PF, true>(buf, lane, tp, ai, aq);
+            fe_fir_tile<T, D, R, 0, PFR, SAFE>(buf, lane, tp, ai, aq);
           }
         } else {
-          fe_fir_tile<T, D, R, 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
+          fe_fir_tile<T, D, R, 0, (T > 127 ? 8 : PFR), SAFE>(buf, lane, tp, ai, aq);
         }
         // tile kk+1 -> the other slot (its halo from this slot); refill the stage
         {
@@ -1088,19 +1094,19 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
               if (pend) {                    // previous block's audio, interleaved into this FIR
                 float o0, o1, o2;
                 if constexpr (AB_NOAUD || AB_NOLDS) {
-                  fe_fir_tile<T, D, R, FM, RING_PF, true>(buf, lane, tp, ai, aq, spread);
+                  fe_fir_tile<T, D, R, FM, PFR, SAFE>(buf, lane, tp, ai, aq, spread);
                   o0 = ai[0]; o1 = ai[1]; o2 = ai[2];
                 } else {
-                  fir_audio_tile<T, 2, 2>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2, spread);
+                  fir_audio_tile<T, FPF, APFX>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2, spread);
                 }
                 aud_drained = audio_store(q_pend, o0, o1, o2);
                 dh_shift(true);
                 pend = false;
               } else {
-                fe_fir_tile<T, D, R, FM, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq, spread);
+                fe_fir_tile<T, D, R, FM, (T > 127 ? 8 : PFR), SAFE>(buf, lane, tp, ai, aq, spread);
               }
             } else {
-              fe_fir_tile<T, D, R, FM, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq, spread);
+              fe_fir_tile<T, D, R, FM, (T > 127 ? 8 : PFR), SAFE>(buf, lane, tp, ai, aq, spread);
             }
             gn += D * TO * 8;
             lds_wait<0>(h0);
@@ -1192,7 +1198,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
     }
 
     float ai[R], aq[R];
-    fe_fir_tile<T, D, R, (MB == 1 || MB == 4 || MB == 5) ? 1 : 0, (T > 127 ? 8 : RING_PF), true>(buf, lane, tp, ai, aq);
+    fe_fir_tile<T, D, R, (MB == 1 || MB == 4 || MB == 5) ? 1 : 0, (T > 127 ? 8 : PFR), SAFE>(buf, lane, tp, ai, aq);
 
     if (kind1 == 3) {
       lds_wait<0>(h0);
@@ -1636,8 +1642,11 @@ __device__ __forceinline__ void audio_block3(const float* aw, const f4v* ptab, f
 }
 
 // PF: FIR reads in flight; VST: stage in VGPRs (true) or AGPRs (false)
-// MB (tuning only; 0 = product): 1 = no FIR (memory pipeline + epilogue)
-template <int T, bool FUSED, int PF = 4, bool VST = true, int MB = 0>
+// MB (tuning only; 0 = product): 1 = no FIR (memory pipeline + epilogue).
+// PIPE: 0 = the next image staged in registers during the FIR; 1 = no stage: the next
+// image's LDS-DMA is issued after the tile and waited for at once (the SIMD's other wave
+// computes meanwhile; no stage registers, and ~half the bytes in flight)
+template <int T, bool FUSED, int PF = 4, bool VST = true, int MB = 0, int PIPE = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
   constexpr int D = 10, R = 3, TO = 64 * R;
@@ -1756,7 +1765,7 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
   int s1, i1;
   next_of(s, i, s1, i1);
   bool stg1 = U > 1 && s1 == s && interior(n_lo_of(i1));   // next image comes through the stage
-  if (stg1) load_stage(s1, n_lo_of(i1));
+  if (PIPE == 0 && stg1) load_stage(s1, n_lo_of(i1));
 
   for (int u = 0; u < U; ++u) {
     const bool lastu = (u + 1 == U);
@@ -1851,9 +1860,42 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
       if (lane == 0 && w != 0) atomicAdd(p.wraps + s, w);
       wacc = 0;
     }
+    // the finished tile's stores
+    auto stores = [&]() {
+      if (st_fe) {
+        typedef float f3v __attribute__((ext_vector_type(3)));
+        *reinterpret_cast<f3v*>(p.demod + (int64_t)sp * p.out_stride + m0 + R * lane) = f3v{d[0], d[1], d[2]};
+      }
+      if constexpr (FUSED) {
+        if (aud) {
+          const int64_t j0 = qa * BO, j = j0 + R * lane;
+          float* ao = a.audio + (int64_t)sp * a.audio_stride + j;
+          if (j0 >= jlo_t && j0 + BO <= jhi_t) {
+            typedef float f3v __attribute__((ext_vector_type(3)));
+            *reinterpret_cast<f3v*>(ao) = f3v{o0, o1, o2};
+          } else {
+            if (j >= jlo_t && j < jhi_t) ao[0] = o0;
+            if (j + 1 >= jlo_t && j + 1 < jhi_t) ao[1] = o1;
+            if (j + 2 >= jlo_t && j + 2 < jhi_t) ao[2] = o2;
+          }
+        }
+      }
+    };
     if (!lastu) {
       // next image into the slot, then the loads of the one after it
-      if (stg1) {
+      if (PIPE == 1) stores();
+      if (stg1 && PIPE == 1) {
+        lds_wait<0>(h0);
+        lds_write_b128(slot + 2 * lane, h0);
+        const char* g = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s1 * p.stride + n_lo_of(i1))) + 1024;
+        const unsigned lb = lds_addr_of(slot) + 1024;
+        static_for<0, (NEWC + 3) / 4>([&](auto Q) {
+          constexpr int c = 4 * Q;
+          constexpr int n = (NEWC - c) < 4 ? (NEWC - c) : 4;
+          glds16x<n>(voff, g + 1024 * c, lb + 1024 * c);
+        });
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (stg1) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_wait<0>(h0);
         lds_write_b128(slot + 2 * lane, h0);
@@ -1881,27 +1923,10 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
       if (FUSED && !have) own();
       next_of(s, i, s1, i1);
       stg1 = u + 2 < U && s1 == s && interior(n_lo_of(i1));
-      if (stg1) load_stage(s1, n_lo_of(i1));
+      if (PIPE == 0 && stg1) load_stage(s1, n_lo_of(i1));
     }
-    // the finished tile's stores, queued behind the next tile's loads
-    if (st_fe) {
-      typedef float f3v __attribute__((ext_vector_type(3)));
-      *reinterpret_cast<f3v*>(p.demod + (int64_t)sp * p.out_stride + m0 + R * lane) = f3v{d[0], d[1], d[2]};
-    }
-    if constexpr (FUSED) {
-      if (aud) {
-        const int64_t j0 = qa * BO, j = j0 + R * lane;
-        float* ao = a.audio + (int64_t)sp * a.audio_stride + j;
-        if (j0 >= jlo_t && j0 + BO <= jhi_t) {
-          typedef float f3v __attribute__((ext_vector_type(3)));
-          *reinterpret_cast<f3v*>(ao) = f3v{o0, o1, o2};
-        } else {
-          if (j >= jlo_t && j < jhi_t) ao[0] = o0;
-          if (j + 1 >= jlo_t && j + 1 < jhi_t) ao[1] = o1;
-          if (j + 2 >= jlo_t && j + 2 < jhi_t) ao[2] = o2;
-        }
-      }
-    }
+    // (PIPE 0) queued behind the next tile's loads
+    if (PIPE == 0 || lastu) stores();
   }
 }
 

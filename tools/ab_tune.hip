@@ -48,7 +48,7 @@ void ring_fe(FeParams p, const TapsF32& taps, hipStream_t st) {
   hipLaunchKernelGGL((fe_ring_kernel<101, false, MODE>), dim3(grid), dim3(64), 0, st, p, taps, ra);
 }
 
-template <bool FUSED, int PF, bool VST, int MB = 0>
+template <bool FUSED, int PF, bool VST, int MB = 0, int PIPE = 0>
 void slot_launch(FeParams p, const TapsF32& taps, const float* ataps, float* audio, hipStream_t st, int wpc) {
   const int64_t M = (p.n + 9) / 10;
   SlotArgs sa{};
@@ -63,7 +63,7 @@ void slot_launch(FeParams p, const TapsF32& taps, const float* ataps, float* aud
   sa.total = sa.tps;
   p.tiles_per_stream = sa.tps;
   const int grid = (int)std::min<int64_t>(256LL * wpc, sa.total);
-  hipLaunchKernelGGL((fe_slot_kernel<101, FUSED, PF, VST, MB>), dim3(grid), dim3(64), 0, st, p, taps, sa);
+  hipLaunchKernelGGL((fe_slot_kernel<101, FUSED, PF, VST, MB, PIPE>), dim3(grid), dim3(64), 0, st, p, taps, sa);
 }
 
 int main(int argc, char** argv) {
@@ -92,8 +92,13 @@ int main(int argc, char** argv) {
   FV("fused ring", 0x00);
   FV("fused ring DMA only", 0x05);
   SFV("fused slot pf4 v w8", 4, true, 8);
+  v.push_back({"fused slotdma pf8 w8", fb, [&](hipStream_t s) { slot_launch<true, 8, true, 0, 1>(p, taps, tdev, aud, s, 8); }, {}});
+  v.push_back({"fused slotdma pf12 w8", fb, [&](hipStream_t s) { slot_launch<true, 12, true, 0, 1>(p, taps, tdev, aud, s, 8); }, {}});
+  v.push_back({"fused slotdma nofir w8", fb, [&](hipStream_t s) { slot_launch<true, 8, true, 1, 1>(p, taps, tdev, aud, s, 8); }, {}});
   EV("fe ring", 0x00);
   SEV("fe slot pf4 v w8", 4, true, 8);
+  v.push_back({"fe slotdma pf8 w8", eb, [&](hipStream_t s) { slot_launch<false, 8, true, 0, 1>(p, taps, nullptr, nullptr, s, 8); }, {}});
+  v.push_back({"fe slotdma pf12 w8", eb, [&](hipStream_t s) { slot_launch<false, 12, true, 0, 1>(p, taps, nullptr, nullptr, s, 8); }, {}});
   if (*sel) v.erase(std::remove_if(v.begin(), v.end(), [&](const Variant& x) { return x.name.find(sel) == std::string::npos; }), v.end());
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   for (auto& x : v) for (int i = 0; i < 3; ++i) x.launch(st);

@@ -12,7 +12,7 @@ for path in split fused; do
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_${tag}_${path} -o prof --output-format csv \
     -- python3 $R/bench.py --no-cpu --steps 20 --warmup 5 --path $path > $R/gpurun_out/prof_${tag}_${path}.json
   timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_${tag}_${path}_fetch -o pmc --output-format csv \
-    -- python3 $R/bench.py --no-cpu --steps 5 --warmup 2 --path $path > /dev/null
+    -- python3 $R/bench.py --no-cpu --steps 5 --warmup 2 --settle-ms 0 --path $path > /dev/null
   timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_${tag}_${path}_write -o pmc --output-format csv \
-    -- python3 $R/bench.py --no-cpu --steps 5 --warmup 2 --path $path > /dev/null
+    -- python3 $R/bench.py --no-cpu --steps 5 --warmup 2 --settle-ms 0 --path $path > /dev/null
 done
