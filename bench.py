@@ -199,7 +199,7 @@ def main():
         _lib.check(lib.sdr_fir_dev(h, d_dm.ptr, None, 1.0, 0, M, M, 0, 1, aup, TA, 5, None, 0, None, d_au.ptr, A),
                    "mono")
 
-    # the fused kernel covers f32 IQ; u8 IQ runs the FE + FIR pair inside sdr_fe_mono_dev
+    # fused: fe_ring_kernel for f32 IQ, fe_slot_kernel (u8 converted on the way in) for u8
     stages = [fused] if args.path == "fused" else [fe, mono]
     tm = _lib.Timer(ctx)
     # fused: one kernel per step -> one event pair around the whole timed region (per-step
@@ -248,11 +248,12 @@ def main():
     if args.path == "fused":
         # compulsory HBM bytes of the fused kernel: IQ in + audio out
         k_bytes = n * bpc + A * 4
-        kname = f"fe_ring_kernel<{args.taps},fused> (sdr_fe_mono_dev: FE {args.taps} taps + audio {args.audio_taps} taps)"
+        kname = (f"fe_slot_kernel<{args.taps},fused,u8>" if args.iq == "u8" else f"fe_ring_kernel<{args.taps},fused>") + \
+            f" (sdr_fe_mono_dev: FE {args.taps} taps + audio {args.audio_taps} taps)"
         kernels = {"fe_mono": round(k_avg, 5)}
     else:
         k_bytes = n * bpc + M * 4                    # IQ in + demod out
-        kname = f"fe_ring_kernel<{args.taps}> (sdr_rf_frontend_dev)"
+        kname = f"fe_slot_kernel<{args.taps}{',u8' if args.iq == 'u8' else ''}> (sdr_rf_frontend_dev)"
         mono_bytes = M * 4 + A * 4
         kernels = {"fe": round(k_avg, 5), "mono": round(stage_ms[1], 5),
                    "mono_gbs": round(mono_bytes / (stage_ms[1] * 1e-3) / 1e9, 1)}

@@ -401,11 +401,11 @@ int sdr_fe_mono_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t
   const int u8 = iq_dtype == SDR_IQ_U8;
   const int64_t xs = nstreams > 1 ? stride : ceil_div(n, 2) * 2;
   const int64_t as = nstreams > 1 ? audio_stride : A;
-  const bool fused = !u8 && rf_decim == 10 && rf_taps == 101 && audio_taps == 151 &&
-                     audio_decim == 5 && xs % 2 == 0 && ((uintptr_t)iq % 16) == 0 &&
+  const bool fused = rf_decim == 10 && rf_taps == 101 && audio_taps == 151 &&
+                     audio_decim == 5 && xs % 2 == 0 && ((uintptr_t)iq % (u8 ? 4 : 16)) == 0 &&
                      ((uintptr_t)audio % 4) == 0;
   if (fused) {
-    FeLaunch a{iq, n, xs, 0, nstreams, rts->dev_f32, &rts->h, rf_taps, rf_decim, 0, nullptr, nullptr, 0,
+    FeLaunch a{iq, n, xs, 0, nstreams, rts->dev_f32, &rts->h, rf_taps, rf_decim, u8, nullptr, nullptr, 0,
                nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr};
     const hipError_t e = sdr_launch_fe_mono(a, ats->dev_f32, audio_taps, audio_decim, audio, as, c->stream);
     if (e == hipSuccess) return SDR_OK;

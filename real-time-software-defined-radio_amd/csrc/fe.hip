@@ -1646,15 +1646,20 @@ __device__ __forceinline__ void audio_block3(const float* aw, const f4v* ptab, f
 // PIPE: 0 = the next image staged in registers during the FIR; 1 = no stage: the next
 // image's LDS-DMA is issued after the tile and waited for at once (the SIMD's other wave
 // computes meanwhile; no stage registers, and ~half the bytes in flight)
-template <int T, bool FUSED, int PF = 4, bool VST = true, int MB = 0, int PIPE = 0>
+// U8: interleaved u8 IQ; the stage holds the next tile's 15 new 128-sample chunks as one
+// dword per lane (2 B per complex sample), converted to (x-128)/128 f32 pairs when it is
+// written into the slot (the same f32 image as the f32 input).
+template <int T, bool FUSED, int PF = 4, bool VST = true, int MB = 0, int PIPE = 0, bool U8 = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
   constexpr int D = 10, R = 3, TO = 64 * R;
-  constexpr int NEWC = D * TO / 128;                 // 15 new 1-KiB chunks per tile
+  constexpr int NEWC = D * TO / 128;                 // 15 new 128-sample chunks per tile
   constexpr int NCH = (D * TO + T + 1 + 127) / 128;  // chunks per tile image
+  constexpr int HCH = NCH - NEWC;                    // halo chunks shared with the next tile
   constexpr int L = NCH * 128;                       // image length (complex samples)
   constexpr int TP = (T + 1) / 2;
-  static_assert((T & 1) == 1 && NCH == NEWC + 1, "odd tap counts up to 127 (one halo chunk)");
+  static_assert((T & 1) == 1 && (HCH == 1 || HCH == 2), "odd tap counts 101..235");
+  static_assert(!U8 || (PIPE == 0 && VST), "u8: register stage");
   constexpr int TA = 151, DA = 5, BO = 64 * R, HA = 152, NW = DA * (R - 1) + TA;
   static_assert((HA + TO * DA + 4) * 4 <= L * 8, "audio history + block fit in the slot");
   __shared__ __attribute__((aligned(16))) f2v slot[L];
@@ -1682,8 +1687,10 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
   }
   // this lane's taps for the cooperative predecessor output (a run's first tile), loaded
   // before any stage load is in flight
-  const float hk0 = p.taps_dev[lane];
-  const float hk1 = (lane + 64 < T) ? p.taps_dev[lane + 64] : 0.f;
+  constexpr int NK = (T + 63) / 64;
+  float hk[NK];
+#pragma unroll
+  for (int q = 0; q < NK; ++q) hk[q] = (lane + 64 * q < T) ? p.taps_dev[lane + 64 * q] : 0.f;
   if constexpr (FUSED) {
     for (int w = lane; w < NW + 1; w += 64) {               // entry NW: zero (pairs over-read)
       const int k0 = (TA - 1) - w, k1 = k0 + DA, k2 = k0 + 2 * DA;
@@ -1696,12 +1703,21 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
   // tile (s, i): outputs TO*i ..; image = samples [n_lo, n_lo + L), n_lo = D*(m0-1) - (T-1)
   auto n_lo_of = [&](int ii) { return (int64_t)(D * TO) * ii - D - (T - 1); };
   auto interior = [&](int64_t nl) { return nl >= -p.hist && nl + L <= p.n; };
+  auto cvt8 = [](unsigned b) { return fmaf((float)b, 0.0078125f, -1.0f); };   // (b-128)/128, exact
 
   // whole image into the slot, waited for (run start, stream change, stream head / tail):
   // LDS-DMA when interior, else guarded loads (zeros outside [-hist, n))
   auto build_sync = [&](int ss, int64_t nl) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    if (interior(nl)) {
+    if constexpr (U8) {
+      const uint8_t* base = reinterpret_cast<const uint8_t*>(p.iq) + 2 * ((int64_t)ss * p.stride);
+      for (int e = lane; e < L; e += 64) {
+        const int64_t nn = nl + e;
+        f2v x = f2v{0.f, 0.f};
+        if (nn >= -p.hist && nn < p.n) x = f2v{cvt8(base[2 * nn]), cvt8(base[2 * nn + 1])};
+        slot[e] = x;
+      }
+    } else if (interior(nl)) {
       const char* g = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)ss * p.stride + nl));
       const unsigned lb = lds_addr_of(slot);
       static_for<0, (NCH + 3) / 4>([&](auto Q) {
@@ -1720,15 +1736,25 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   };
-  // the next tile's new chunks [1, NCH) -> AGPR stage (16 B per lane per chunk)
-  f4v stg[NEWC];
+  // the next tile's new chunks [HCH, NCH) -> register stage (16 B per lane per chunk; u8:
+  // 4 B per lane per chunk)
+  f4v stg[U8 ? 1 : NEWC];
+  unsigned stg8[U8 ? NEWC : 1];
   auto load_stage = [&](int ss, int64_t nl) {
-    const char* gl = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)ss * p.stride + nl)) + 1024;
-    static_for<0, NEWC>([&](auto C) {
-      constexpr int c = C;
-      if constexpr (VST) gload16_nt_v<1024 * (c % 4)>(stg[c], voff, gl + 4096 * (c / 4));
-      else gload16_nt_a<1024 * (c % 4)>(stg[c], voff, gl + 4096 * (c / 4));
-    });
+    if constexpr (U8) {
+      const char* gb = reinterpret_cast<const char*>(p.iq) + 2 * ((int64_t)ss * p.stride + nl) + 256 * HCH;
+      static_for<0, NEWC>([&](auto C) {
+        constexpr int c = C;
+        gload4_nt_v<256 * c>(stg8[c], 4u * lane, gb);
+      });
+    } else {
+      const char* gl = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)ss * p.stride + nl)) + 1024 * HCH;
+      static_for<0, NEWC>([&](auto C) {
+        constexpr int c = C;
+        if constexpr (VST) gload16_nt_v<1024 * (c % 4)>(stg[c], voff, gl + 4096 * (c / 4));
+        else gload16_nt_a<1024 * (c % 4)>(stg[c], voff, gl + 4096 * (c / 4));
+      });
+    }
   };
 
   int s = (int)(g0 / a.tps);
@@ -1769,8 +1795,11 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
 
   for (int u = 0; u < U; ++u) {
     const bool lastu = (u + 1 == U);
-    f4v h0;
-    if (stg1) h0 = lds_read_b128<0>(slot + NEWC * 128 + 2 * lane);   // halo of the next tile
+    f4v h0, h1;                                                        // halo of the next tile
+    if (stg1) {
+      h0 = lds_read_b128<0>(slot + NEWC * 128 + 2 * lane);
+      if constexpr (HCH == 2) h1 = lds_read_b128<0>(slot + (NEWC + 1) * 128 + 2 * lane);
+    }
     if constexpr (FUSED) {
       constexpr int NQ = (TP + 1) / 2;
       f4v tq[NQ];
@@ -1807,13 +1836,13 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
     } else {
       float si = 0.f, sq = 0.f;
       if (m0 > 0 && !have) {           // output m0-1 (the predecessor): image samples [0, T)
-        const f2v x0 = slot[(T - 1) - lane];
-        si = fmaf(hk0, x0.x, si);
-        sq = fmaf(hk0, x0.y, sq);
-        if (lane + 64 < T) {
-          const f2v x1 = slot[(T - 1) - (lane + 64)];
-          si = fmaf(hk1, x1.x, si);
-          sq = fmaf(hk1, x1.y, sq);
+#pragma unroll
+        for (int q = 0; q < NK; ++q) {
+          if (lane + 64 * q < T) {
+            const f2v x = slot[(T - 1) - (lane + 64 * q)];
+            si = fmaf(hk[q], x.x, si);
+            sq = fmaf(hk[q], x.y, sq);
+          }
         }
         si = wave_sum(si);
         sq = wave_sum(sq);
@@ -1887,8 +1916,9 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
       if (stg1 && PIPE == 1) {
         lds_wait<0>(h0);
         lds_write_b128(slot + 2 * lane, h0);
-        const char* g = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s1 * p.stride + n_lo_of(i1))) + 1024;
-        const unsigned lb = lds_addr_of(slot) + 1024;
+        if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(slot + 128 + 2 * lane, h1); }
+        const char* g = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s1 * p.stride + n_lo_of(i1))) + 1024 * HCH;
+        const unsigned lb = lds_addr_of(slot) + 1024 * HCH;
         static_for<0, (NEWC + 3) / 4>([&](auto Q) {
           constexpr int c = 4 * Q;
           constexpr int n = (NEWC - c) < 4 ? (NEWC - c) : 4;
@@ -1899,15 +1929,21 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_wait<0>(h0);
         lds_write_b128(slot + 2 * lane, h0);
+        if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(slot + 128 + 2 * lane, h1); }
         const unsigned na = lds_addr_of(slot) + 16u * lane;
         static_for<0, NEWC>([&](auto C) {
           constexpr int c = C;
-          if constexpr (VST) {
+          if constexpr (U8) {
+            asm volatile("" : "+v"(stg8[c]));
+            const unsigned b = stg8[c];
+            const f4v v = f4v{cvt8(b & 0xff), cvt8((b >> 8) & 0xff), cvt8((b >> 16) & 0xff), cvt8(b >> 24)};
+            lds_write_b128_v<1024 * (HCH + c)>(na, v);
+          } else if constexpr (VST) {
             asm volatile("" : "+v"(stg[c]));
-            lds_write_b128_v<1024 * (1 + c)>(na, stg[c]);
+            lds_write_b128_v<1024 * (HCH + c)>(na, stg[c]);
           } else {
             asm volatile("" : "+a"(stg[c]));
-            lds_write_b128_a<1024 * (1 + c)>(na, stg[c]);
+            lds_write_b128_a<1024 * (HCH + c)>(na, stg[c]);
           }
         });
       } else {
@@ -1985,14 +2021,14 @@ static bool use_slot(bool fused) {
   return c == 1 || (c == 0 && !fused);
 }
 
-template <int T, bool FUSED>
+template <int T, bool FUSED, bool U8 = false>
 static hipError_t launch_slot_t(FeParams p, const TapsF32& taps, SlotArgs sa, hipStream_t st) {
   if (sa.total <= 0) return hipSuccess;
-  static const int wpc = resident_per_cu(fe_slot_kernel<T, FUSED>, 64);
+  static const int wpc = resident_per_cu(fe_slot_kernel<T, FUSED, 4, true, 0, 0, U8>, 64);
   const int64_t slots = (int64_t)cu_count() * std::max(1, std::min(wpc, 8));
   const int64_t grid = std::min<int64_t>(slots, sa.total);
   p.tiles_per_stream = sa.tps;
-  hipLaunchKernelGGL((fe_slot_kernel<T, FUSED>), dim3((unsigned)grid), dim3(64), 0, st, p, taps, sa);
+  hipLaunchKernelGGL((fe_slot_kernel<T, FUSED, 4, true, 0, 0, U8>), dim3((unsigned)grid), dim3(64), 0, st, p, taps, sa);
   return hipGetLastError();
 }
 
@@ -2014,6 +2050,12 @@ static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
   if (tiles <= 0) return hipSuccess;
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
   if constexpr (U8) {
+    if (use_slot(false)) {   // u8 IQ: the slot kernel (2 B per sample staged, converted on write)
+      SlotArgs sa{};
+      sa.tps = (int)((M + 191) / 192);
+      sa.total = (int64_t)sa.tps * a.nstreams;
+      return launch_slot_t<T, false, true>(p, *a.taps, sa, st);
+    }
     hipLaunchKernelGGL((fe_kernel<T, D, R, NT, true>), dim3((unsigned)tiles), dim3(NT), 0, st, p, *a.taps);
   } else {
     if constexpr (T <= 127) {
@@ -2078,12 +2120,12 @@ static hipError_t launch_fe_mono_t(const FeLaunch& a, const float* ataps, float*
   if (ra.total <= 0) return hipSuccess;
   if (ra.total > 0x7fffffff / 5) return hipErrorInvalidValue;
   ra.audio = audio; ra.audio_stride = audio_stride; ra.ataps = ataps;
-  if (use_slot(true)) {
+  if (a.u8 || use_slot(true)) {     // u8 IQ: only the slot kernel converts on the way in
     SlotArgs sa{};
     sa.tps = ra.tps;
     sa.total = (int64_t)sa.tps * a.nstreams;
     sa.audio = audio; sa.audio_stride = audio_stride; sa.ataps = ataps;
-    return launch_slot_t<T, true>(p, *a.taps, sa, st);
+    return a.u8 ? launch_slot_t<T, true, true>(p, *a.taps, sa, st) : launch_slot_t<T, true>(p, *a.taps, sa, st);
   }
   if (use_circ()) {
     ra.ab = (int)((M + 319) / 320);
@@ -2111,7 +2153,7 @@ static hipError_t launch_fe_mono_t(const FeLaunch& a, const float* ataps, float*
 // configs); anything else returns hipErrorInvalidValue and the C-ABI runs the two-kernel path.
 hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
                               int64_t audio_stride, hipStream_t st) {
-  if (a.D != 10 || a.u8 || TA != 151 || DA != 5) return hipErrorInvalidValue;
+  if (a.D != 10 || TA != 151 || DA != 5) return hipErrorInvalidValue;
   switch (a.T) {
     case 101: return launch_fe_mono_t<101>(a, ataps, audio, audio_stride, st);
     default: return hipErrorInvalidValue;   // 151 RF taps: 3 waves/CU by LDS -> two-kernel path

@@ -120,6 +120,12 @@ __device__ __forceinline__ void lds_write_b128_v(unsigned lds_addr, const f4v& v
   static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16-bit");
   asm volatile("ds_write_b128 %0, %1 offset:%2" : : "v"(lds_addr), "v"(v), "i"(OFF) : "memory");
 }
+// 4-B-per-lane non-temporal load (one dword: two u8 complex samples) into a VGPR
+template <int OFF>
+__device__ __forceinline__ void gload4_nt_v(unsigned& dst, unsigned voff, const void* sbase) {
+  static_assert(OFF >= 0 && OFF < 4096, "12-bit immediate");
+  asm volatile("global_load_dword %0, %1, %2 offset:%3 nt" : "=v"(dst) : "v"(voff), "s"(sbase), "i"(OFF) : "memory");
+}
 // ds_write_b128 of AGPR data with an immediate offset (16-bit).
 template <int OFF>
 __device__ __forceinline__ void lds_write_b128_a(unsigned lds_addr, const f4v& v) {
