@@ -43,12 +43,22 @@ __device__ inline double reduce_2pi(double a) {
   return r;
 }
 
-__global__ void pll_loop_kernel(const float* in, int64_t n, int64_t in_stride, int nstreams,
-                                PllCfg cfg, double* state, int64_t state_stride, double* theta,
-                                int64_t th_stride) {
+// One wave per stream.  Every lane runs the same recurrence (wave-uniform values, no
+// divergence); the inputs come from LDS in chunks of PCH samples, the next chunk's global
+// loads are in flight (in registers) while the current chunk runs, and the phases go out
+// through LDS as coalesced stores.  (A lone lane reading x[k] from global memory per step
+// waits an L2 round trip every sample.)
+constexpr int PCH = 512;
+__global__ __launch_bounds__(64) void pll_loop_kernel(const float* in, int64_t n, int64_t in_stride,
+                                                      int nstreams, PllCfg cfg, double* state,
+                                                      int64_t state_stride, double* theta,
+                                                      int64_t th_stride) {
 #pragma clang fp contract(off)  // Python evaluates a*b + c with two roundings
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x;
   if (s >= nstreams) return;
+  __shared__ float xs[2][PCH];
+  __shared__ double ths[PCH];
   const float* x = in + (int64_t)s * in_stride;
   double* st = state + (int64_t)s * state_stride;
   double* th = theta + (int64_t)s * th_stride;
@@ -57,23 +67,47 @@ __global__ void pll_loop_kernel(const float* in, int64_t n, int64_t in_stride, i
   const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
   double arg = 0.0;
   bool literal = true;  // first sample uses the caller's (fI, fQ)
-  for (int64_t k = 0; k < n; ++k) {
-    const double xv = (double)x[k];
-    double e;
-    if (literal || !(xv > 0.0 || xv < 0.0)) {
-      if (!literal) { fI = cos(arg); fQ = sin(arg); }
-      e = atan2(xv * (-fQ), xv * fI);
-    } else {
-      e = reduce_2pi(xv > 0.0 ? -arg : kPi - arg);
-      if (e <= -kPi) e += 2.0 * kPi;   // atan2 range is (-pi, pi]
-    }
-    literal = false;
-    integ = integ + cfg.ki * e;
-    phase = phase + cfg.kp * e + integ;
-    arg = w * ((off + (double)k) + 1.0) + phase;
-    th[k] = arg;
+  constexpr int PL = PCH / 64;
+  const int64_t nch = (n + PCH - 1) / PCH;
+  for (int j = 0; j < PL; ++j) {
+    const int64_t k = lane + 64 * j;
+    xs[0][lane + 64 * j] = k < n ? x[k] : 0.f;
   }
-  if (n > 0) {
+  __syncthreads();
+  for (int64_t c = 0; c < nch; ++c) {
+    const int buf = (int)(c & 1);
+    float pre[PL];
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {               // next chunk: loads in flight meanwhile
+      const int64_t k = (c + 1) * PCH + lane + 64 * j;
+      pre[j] = k < n ? x[k] : 0.f;
+    }
+    const int kn = (int)min<int64_t>(PCH, n - c * PCH);
+#pragma unroll 8
+    for (int kk = 0; kk < kn; ++kk) {
+      const int64_t k = c * PCH + kk;
+      const double xv = (double)xs[buf][kk];
+      double e;
+      if (literal || !(xv > 0.0 || xv < 0.0)) {
+        if (!literal) { fI = cos(arg); fQ = sin(arg); }
+        e = atan2(xv * (-fQ), xv * fI);
+      } else {
+        e = reduce_2pi(xv > 0.0 ? -arg : kPi - arg);
+        if (e <= -kPi) e += 2.0 * kPi;   // atan2 range is (-pi, pi]
+      }
+      literal = false;
+      integ = integ + cfg.ki * e;
+      phase = phase + cfg.kp * e + integ;
+      arg = w * ((off + (double)k) + 1.0) + phase;
+      if (lane == 0) ths[kk] = arg;
+    }
+    __syncthreads();
+    for (int e = lane; e < kn; e += 64) th[c * PCH + e] = ths[e];
+#pragma unroll
+    for (int j = 0; j < PL; ++j) xs[buf ^ 1][lane + 64 * j] = pre[j];
+    __syncthreads();
+  }
+  if (n > 0 && lane == 0) {
     st[0] = integ;
     st[1] = phase;
     st[2] = cos(arg);
@@ -131,7 +165,7 @@ hipError_t sdr_launch_pll(const float* in, int64_t n, int64_t in_stride, int nst
   const int nb = (nstreams + 63) / 64;
   hipLaunchKernelGGL(nco_prologue_kernel, dim3(nb), dim3(64), 0, st, state_dev, (int64_t)6,
                      nstreams, cfg, nco0, ncoq0);
-  hipLaunchKernelGGL(pll_loop_kernel, dim3(nb), dim3(64), 0, st, in, n, in_stride, nstreams, cfg,
+  hipLaunchKernelGGL(pll_loop_kernel, dim3(nstreams), dim3(64), 0, st, in, n, in_stride, nstreams, cfg,
                      state_dev, (int64_t)6, theta, th_stride);
   const int64_t nout = n + 1;
   hipLaunchKernelGGL(nco_kernel, dim3((unsigned)((nout + 255) / 256), nstreams), dim3(256), 0, st,
