@@ -174,6 +174,26 @@ int sdr_pll_dev(sdr_ctx* ctx, const float* in, int64_t n, int64_t in_stride, int
 int sdr_stereo_combine_dev(sdr_ctx* ctx, const float* mono, const float* side, int64_t n,
                            float* left, float* right);
 
+/* ---- RDS link layer (host code) -----------------------------------
+ * model/fmRDSblock.py:207-346 (src/fm_radio.cpp:444-729 frame_thread): per block of the
+ * in-phase RRC output (57 kS/s, 24 samples per symbol), clock and data recovery from a
+ * carried symbol offset, Manchester decoding of symbol pairs (with the carried lone
+ * symbol), differential decoding, and the syndrome scan of every 26-bit window.
+ * events: 3 int64 per syndrome match {type 0..3 = A..D, position, accepted}, where
+ * accepted = 1 for the reference's "Syndrome X at position N" prints and 0 for its
+ * "False positive" prints; positions count across blocks as the reference's printposition.
+ * symbols / bits / diff (optional, NULL to skip): the sampled symbols, the Manchester bits
+ * and the bits the scan saw (carried bits first), each count written to n_*.
+ * The state (offset, start position, lone symbol, previous bit, carried bits, positions)
+ * lives in the sdr_rds_link object; one object per stream.  No GPU is used. */
+typedef struct sdr_rds_link sdr_rds_link;
+int sdr_rds_link_create(sdr_rds_link** out);
+void sdr_rds_link_destroy(sdr_rds_link* link);
+int sdr_rds_link_block(sdr_rds_link* link, const double* rrc_i, int64_t n, int64_t* events,
+                       int64_t max_events, int64_t* n_events, double* symbols, int64_t max_symbols,
+                       int64_t* n_symbols, uint8_t* bits, int64_t max_bits, int64_t* n_bits,
+                       uint8_t* diff, int64_t max_diff, int64_t* n_diff);
+
 #ifdef __cplusplus
 }
 #endif

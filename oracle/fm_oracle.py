@@ -242,3 +242,99 @@ def mono_basic(iq, rf_taps=101, audio_taps=151, demod_fn=fm_demod_arctan):
     demod, _ = demod_fn(i_f[::10], q_f[::10], 0.0)
     audio = lfilter_fir(au_b, demod)[::5]
     return audio, np.int16((audio / 2) * 32767)
+
+
+# ---- RDS link layer ---------------------------------------------
+# Parity matrix of model/fmRDSblock.py:49 (26 x 10) and the syndromes of :300-330.
+RDS_H = np.array([[1,0,0,0,0,0,0,0,0,0],[0,1,0,0,0,0,0,0,0,0],[0,0,1,0,0,0,0,0,0,0],[0,0,0,1,0,0,0,0,0,0],
+                  [0,0,0,0,1,0,0,0,0,0],[0,0,0,0,0,1,0,0,0,0],[0,0,0,0,0,0,1,0,0,0],[0,0,0,0,0,0,0,1,0,0],
+                  [0,0,0,0,0,0,0,0,1,0],[0,0,0,0,0,0,0,0,0,1],[1,0,1,1,0,1,1,1,0,0],[0,1,0,1,1,0,1,1,1,0],
+                  [0,0,1,0,1,1,0,1,1,1],[1,0,1,0,0,0,0,1,1,1],[1,1,1,0,0,1,1,1,1,1],[1,1,0,0,0,1,0,0,1,1],
+                  [1,1,0,1,0,1,0,1,0,1],[1,1,0,1,1,1,0,1,1,0],[0,1,1,0,1,1,1,0,1,1],[1,0,0,0,0,0,0,0,0,1],
+                  [1,1,1,1,0,1,1,1,0,0],[0,1,1,1,1,0,1,1,1,0],[0,0,1,1,1,1,0,1,1,1],[1,0,1,0,1,0,0,1,1,1],
+                  [1,1,1,0,0,0,1,1,1,1],[1,1,0,0,0,1,1,0,1,1]], dtype=np.int64)
+RDS_SYNDROMES = {0: [1,1,1,1,0,1,1,0,0,0], 1: [1,1,1,1,0,1,0,1,0,0],      # A, B
+                 2: [1,0,0,1,0,1,1,1,0,0], 3: [1,0,0,1,0,1,1,0,0,0]}      # C, D
+
+
+def rds_link(rrc_blocks):
+    """Restatement of model/fmRDSblock.py:207-346 (clock and data recovery, Manchester and
+    differential decoding, syndrome frame sync) over the per-block in-phase RRC outputs.
+    Returns per block: symbols, bits, diff (the bits the syndrome scan sees, carried bits
+    first) and events [(type 0..3 = A..D, position, accepted)], where accepted = the
+    'Syndrome X at position' prints and not accepted = the 'False positive' prints.
+    One deviation: a tie in the block-0 screening (:244-248 leaves start_pos unbound, a
+    NameError) takes start_pos = 0."""
+    out = []
+    st = dict(block_count=0, int_offset=0, start_pos=0, lonely_bit=0.0, front_bit=0, prebit=0,
+              printposition=0, prev_sync_bits=np.zeros(0), last_position=-1)
+    for rrc in rrc_blocks:
+        rrc = np.asarray(rrc, dtype=np.float64)
+        r = {}
+        if st["block_count"] == 0:                                             # :208-209
+            st["int_offset"] = int(np.where(rrc[0:24] == np.max(rrc[0:24]))[0][0])
+        io = st["int_offset"]
+        s = rrc[io::24]                                                        # :216
+        # :219 (value search in the last 24 samples; the value sits at a known index)
+        st["int_offset"] = 24 - int(np.where(rrc[len(rrc) - 24:] == s[-1])[0][0])
+        if st["block_count"] == 0:                                             # :233-249
+            c0 = c1 = 0
+            for m in range(int(len(s) / 4)):
+                if (s[2 * m] > 0 and s[2 * m + 1] > 0) or (s[2 * m] < 0 and s[2 * m + 1] < 0):
+                    c0 += 1
+                elif (s[2 * m + 1] > 0 and s[2 * m + 2] > 0) or (s[2 * m + 1] < 0 and s[2 * m + 2] < 0):
+                    c1 += 1
+            st["start_pos"] = 1 if c0 > c1 else 0
+        sp = st["start_pos"]
+        bits = np.zeros(int(len(s) / 2) - sp)                                  # :251
+        if sp == 1 and st["block_count"] != 0:                                 # :255-259
+            if st["lonely_bit"] > s[0]:
+                st["front_bit"] = 1
+            elif st["lonely_bit"] < s[0]:
+                st["front_bit"] = 0
+        for k in range(len(bits)):                                             # :261-269
+            if sp + 2 * k + 1 > len(s) - 1:
+                break
+            if s[2 * k + sp] > s[2 * k + 1 + sp]:
+                bits[k] = 1
+            elif s[2 * k + sp] < s[2 * k + 1 + sp]:
+                bits[k] = 0
+        if sp == 1:                                                            # :271-276
+            bits = np.insert(bits, 0, st["front_bit"], axis=0)
+            st["lonely_bit"] = s[-1]
+        if st["block_count"] == 0:                                             # :280-284
+            st["prebit"] = bits[0]
+            off = 1
+        else:
+            off = 0
+        diff = np.zeros(len(bits) - off)
+        for t in range(len(diff)):                                             # :286-289
+            pb, b = bool(st["prebit"]), bool(bits[t + off])
+            diff[t] = (pb and not b) or (not pb and b)
+            st["prebit"] = bits[t + off]
+        st["prebit"] = bits[-1]                                                # :291
+        if st["block_count"] != 0:                                             # :295-296
+            diff = np.insert(diff, 0, st["prev_sync_bits"], axis=0)
+        events = []
+        position = 0
+        while True:                                                            # :299-341
+            blk = diff[position:position + 26].astype(np.int64)
+            syn = ((blk @ RDS_H) % 2).tolist()
+            for typ, pat in RDS_SYNDROMES.items():
+                if syn == pat:
+                    pp = st["printposition"]
+                    if st["last_position"] == -1 or pp - st["last_position"] == 26:
+                        events.append((typ, pp, 1))
+                        st["last_position"] = pp
+                    else:
+                        events.append((typ, pp, 0))
+                    break
+            position += 1
+            if position + 26 > len(diff) - 1:
+                break
+            st["printposition"] += 1
+        st["prev_sync_bits"] = diff[position - 1:]                            # :343
+        st["block_count"] += 1
+        r.update(symbols=s, bits=bits, diff=diff, events=events)
+        out.append(r)
+    return out

@@ -70,6 +70,10 @@ SIGNATURES = {
     "sdr_pll_dev": (_i32, [_vp, _vp, _i64, _i64, _i32, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp,
                            _i64]),
     "sdr_stereo_combine_dev": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
+    "sdr_rds_link_create": (_i32, [_c.POINTER(_vp)]),
+    "sdr_rds_link_destroy": (None, [_vp]),
+    "sdr_rds_link_block": (_i32, [_vp, _dp, _i64, _vp, _i64, _c.POINTER(_i64), _vp, _i64, _c.POINTER(_i64),
+                                  _vp, _i64, _c.POINTER(_i64), _vp, _i64, _c.POINTER(_i64)]),
 }
 
 _lib = None

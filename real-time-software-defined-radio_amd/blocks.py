@@ -185,3 +185,54 @@ class RdsBlockProcessor(MonoBlockProcessor):
                        lpf_q=self.lpf_out_q.download(M), resample_i=self.res_i.download(R),
                        resample_q=self.res_q.download(R))
         return {k: v.astype(np.float64) for k, v in out.items()}
+
+
+class RdsLinkLayer:
+    """RDS link layer of model/fmRDSblock.py:207-346 on the host (libsdr C++, no GPU):
+    clock and data recovery, Manchester and differential decoding, syndrome frame sync.
+
+    process(rrc_i) takes one block of the in-phase RRC output (RdsBlockProcessor's
+    'rrc_i') and returns dict(events=[(type, position, accepted)], symbols, bits, diff):
+    type 0..3 = syndrome A..D, accepted = the reference's "Syndrome X at position N"
+    prints (1) or its "False positive" prints (0); the state carries across calls."""
+
+    TYPES = "ABCD"
+
+    def __init__(self):
+        import ctypes
+        self._c = ctypes
+        self.lib = _lib.load_library()
+        h = ctypes.c_void_p()
+        check(self.lib.sdr_rds_link_create(ctypes.byref(h)), "sdr_rds_link_create")
+        self.handle = h
+
+    def process(self, rrc_i):
+        c = self._c
+        x = np.ascontiguousarray(rrc_i, dtype=np.float64)
+        n = len(x)
+        ns_max = n // 24 + 2
+        nb_max = ns_max // 2 + 2
+        nd_max = nb_max + 64
+        ev = np.empty(3 * (nd_max + 1), dtype=np.int64)
+        sym = np.empty(ns_max)
+        bits = np.empty(nb_max, dtype=np.uint8)
+        diff = np.empty(nd_max, dtype=np.uint8)
+        ne, ns, nb, nd = c.c_int64(), c.c_int64(), c.c_int64(), c.c_int64()
+        vp = lambda a: a.ctypes.data_as(c.c_void_p)  # noqa: E731
+        check(self.lib.sdr_rds_link_block(self.handle, f64p(x), n, vp(ev), nd_max + 1, c.byref(ne), vp(sym),
+                                          ns_max, c.byref(ns), vp(bits), nb_max, c.byref(nb), vp(diff), nd_max,
+                                          c.byref(nd)), "sdr_rds_link_block")
+        events = [tuple(int(v) for v in ev[3 * k:3 * k + 3]) for k in range(ne.value)]
+        return dict(events=events, symbols=sym[:ns.value].copy(), bits=bits[:nb.value].copy(),
+                    diff=diff[:nd.value].copy())
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.sdr_rds_link_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -13,7 +13,9 @@
 // message of the calling thread's last failure.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <new>
 #include <cstdarg>
 #include <cstdio>
 #include <deque>
@@ -727,6 +729,153 @@ int sdr_mono_block(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, const do
   TRY(d2h(c, &ph1, dph, sizeof(double)));
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (prev_phase) *prev_phase = ph1;
+  return SDR_OK;
+}
+
+// ---- RDS link layer (host side) --------------------------------
+// model/fmRDSblock.py:207-346: clock and data recovery (every 24th RRC sample from a
+// carried offset), Manchester decoding of symbol pairs, differential decoding, and the
+// syndrome scan of every 26-bit window with the in-frame / false-positive rule.  Bit
+// level, sequential and a few hundred bits per block: CPU code.  The one deviation: a tie
+// in the block-0 screening (where the reference's start_pos is unbound) takes 0.
+}  // extern "C"
+
+struct sdr_rds_link {
+  int64_t block_count = 0, int_offset = 0, printposition = 0, last_position = -1;
+  int start_pos = 0, front_bit = 0, prebit = 0;
+  double lonely_bit = 0.0;
+  std::vector<uint8_t> prev_sync_bits;
+};
+
+namespace {
+// parity matrix H (26 x 10), model/fmRDSblock.py:49, one row per bit as 10-bit masks (bit i = column i)
+constexpr uint8_t kRdsH[26][10] = {
+    {1,0,0,0,0,0,0,0,0,0},{0,1,0,0,0,0,0,0,0,0},{0,0,1,0,0,0,0,0,0,0},{0,0,0,1,0,0,0,0,0,0},
+    {0,0,0,0,1,0,0,0,0,0},{0,0,0,0,0,1,0,0,0,0},{0,0,0,0,0,0,1,0,0,0},{0,0,0,0,0,0,0,1,0,0},
+    {0,0,0,0,0,0,0,0,1,0},{0,0,0,0,0,0,0,0,0,1},{1,0,1,1,0,1,1,1,0,0},{0,1,0,1,1,0,1,1,1,0},
+    {0,0,1,0,1,1,0,1,1,1},{1,0,1,0,0,0,0,1,1,1},{1,1,1,0,0,1,1,1,1,1},{1,1,0,0,0,1,0,0,1,1},
+    {1,1,0,1,0,1,0,1,0,1},{1,1,0,1,1,1,0,1,1,0},{0,1,1,0,1,1,1,0,1,1},{1,0,0,0,0,0,0,0,0,1},
+    {1,1,1,1,0,1,1,1,0,0},{0,1,1,1,1,0,1,1,1,0},{0,0,1,1,1,1,0,1,1,1},{1,0,1,0,1,0,0,1,1,1},
+    {1,1,1,0,0,0,1,1,1,1},{1,1,0,0,0,1,1,0,1,1}};
+// syndromes A, B, C, D (model/fmRDSblock.py:300, :307, :314, :321)
+constexpr uint8_t kRdsSyn[4][10] = {{1,1,1,1,0,1,1,0,0,0}, {1,1,1,1,0,1,0,1,0,0},
+                                    {1,0,0,1,0,1,1,1,0,0}, {1,0,0,1,0,1,1,0,0,0}};
+}  // namespace
+
+extern "C" {
+
+int sdr_rds_link_create(sdr_rds_link** out) {
+  if (!out) return fail(SDR_EINVAL, "sdr_rds_link_create: out is NULL");
+  *out = new (std::nothrow) sdr_rds_link();
+  return *out ? SDR_OK : fail(SDR_ENOMEM, "sdr_rds_link_create: out of memory");
+}
+
+void sdr_rds_link_destroy(sdr_rds_link* l) { delete l; }
+
+int sdr_rds_link_block(sdr_rds_link* l, const double* rrc_i, int64_t n, int64_t* events,
+                       int64_t max_events, int64_t* n_events, double* symbols, int64_t max_symbols,
+                       int64_t* n_symbols, uint8_t* bits, int64_t max_bits, int64_t* n_bits,
+                       uint8_t* diff_out, int64_t max_diff, int64_t* n_diff) {
+  if (!l || !rrc_i) return fail(SDR_EINVAL, "sdr_rds_link_block: NULL link or input");
+  if (n < 24) return fail(SDR_EINVAL, "sdr_rds_link_block: block of %lld samples (< 24)", (long long)n);
+  if (l->block_count == 0) {                                          // :208-209 first index of the max
+    int64_t best = 0;
+    for (int64_t k = 1; k < 24; ++k)
+      if (rrc_i[k] > rrc_i[best]) best = k;
+    for (int64_t k = 0; k < 24; ++k)
+      if (std::isnan(rrc_i[k])) return fail(SDR_EINVAL, "sdr_rds_link_block: NaN in the first 24 samples");
+    l->int_offset = best;
+  }
+  const int64_t io = l->int_offset;
+  if (io >= n) return fail(SDR_EINVAL, "sdr_rds_link_block: symbol offset %lld beyond the block", (long long)io);
+  std::vector<double> s;                                              // :216
+  for (int64_t k = io; k < n; k += 24) s.push_back(rrc_i[k]);
+  const int64_t ns = (int64_t)s.size();
+  {                                                                   // :219 value search
+    int64_t j = -1;
+    for (int64_t k = 0; k < 24 && j < 0; ++k)
+      if (rrc_i[n - 24 + k] == s.back()) j = k;
+    if (j < 0) return fail(SDR_EINVAL, "sdr_rds_link_block: last symbol not in the last 24 samples");
+    l->int_offset = 24 - j;
+  }
+  if (l->block_count == 0) {                                          // :233-249
+    int64_t c0 = 0, c1 = 0;
+    for (int64_t m = 0; m < ns / 4; ++m) {
+      if ((s[2 * m] > 0 && s[2 * m + 1] > 0) || (s[2 * m] < 0 && s[2 * m + 1] < 0)) ++c0;
+      else if ((s[2 * m + 1] > 0 && s[2 * m + 2] > 0) || (s[2 * m + 1] < 0 && s[2 * m + 2] < 0)) ++c1;
+    }
+    l->start_pos = c0 > c1 ? 1 : 0;
+  }
+  const int sp = l->start_pos;
+  std::vector<uint8_t> b((size_t)std::max<int64_t>(ns / 2 - sp, 0), 0);   // :251
+  if (sp == 1 && l->block_count != 0) {                               // :255-259
+    if (l->lonely_bit > s[0]) l->front_bit = 1;
+    else if (l->lonely_bit < s[0]) l->front_bit = 0;
+  }
+  for (int64_t k = 0; k < (int64_t)b.size(); ++k) {                   // :261-269
+    if (sp + 2 * k + 1 > ns - 1) break;
+    if (s[2 * k + sp] > s[2 * k + 1 + sp]) b[k] = 1;
+    else if (s[2 * k + sp] < s[2 * k + 1 + sp]) b[k] = 0;
+  }
+  if (sp == 1) {                                                      // :271-276
+    b.insert(b.begin(), (uint8_t)l->front_bit);
+    l->lonely_bit = s.back();
+  }
+  if (b.empty()) return fail(SDR_EINVAL, "sdr_rds_link_block: no bits in the block");
+  int64_t off = 0;
+  if (l->block_count == 0) {                                          // :280-284
+    l->prebit = b[0];
+    off = 1;
+  }
+  std::vector<uint8_t> d(l->block_count != 0 ? l->prev_sync_bits : std::vector<uint8_t>());   // :295-296
+  for (int64_t t = 0; t + off < (int64_t)b.size(); ++t) {             // :286-289
+    d.push_back((uint8_t)(l->prebit ^ b[t + off]));
+    l->prebit = b[t + off];
+  }
+  l->prebit = b.back();                                               // :291
+  if (d.size() < 26) return fail(SDR_EINVAL, "sdr_rds_link_block: %zu bits to scan (< 26)", d.size());
+  int64_t ne = 0;
+  int64_t position = 0;
+  for (;;) {                                                          // :299-341
+    uint8_t syn[10] = {0};
+    for (int i = 0; i < 10; ++i)
+      for (int j = 0; j < 26; ++j) syn[i] ^= (uint8_t)(d[position + j] & kRdsH[j][i]);
+    for (int typ = 0; typ < 4; ++typ) {
+      if (std::memcmp(syn, kRdsSyn[typ], 10) != 0) continue;
+      const int64_t pp = l->printposition;
+      const bool ok = l->last_position == -1 || pp - l->last_position == 26;
+      if (ok) l->last_position = pp;
+      if (events && ne < max_events) {
+        events[3 * ne] = typ;
+        events[3 * ne + 1] = pp;
+        events[3 * ne + 2] = ok ? 1 : 0;
+      }
+      ++ne;
+      break;
+    }
+    ++position;
+    if (position + 26 > (int64_t)d.size() - 1) break;
+    ++l->printposition;
+  }
+  l->prev_sync_bits.assign(d.begin() + (position - 1), d.end());      // :343
+  ++l->block_count;
+  if (n_events) *n_events = ne;
+  if (n_symbols) *n_symbols = ns;
+  if (n_bits) *n_bits = (int64_t)b.size();
+  if (n_diff) *n_diff = (int64_t)d.size();
+  if (events && ne > max_events) return fail(SDR_EINVAL, "sdr_rds_link_block: %lld events > max %lld", (long long)ne, (long long)max_events);
+  if (symbols) {
+    if (ns > max_symbols) return fail(SDR_EINVAL, "sdr_rds_link_block: symbols buffer too small");
+    std::copy(s.begin(), s.end(), symbols);
+  }
+  if (bits) {
+    if ((int64_t)b.size() > max_bits) return fail(SDR_EINVAL, "sdr_rds_link_block: bits buffer too small");
+    std::copy(b.begin(), b.end(), bits);
+  }
+  if (diff_out) {
+    if ((int64_t)d.size() > max_diff) return fail(SDR_EINVAL, "sdr_rds_link_block: diff buffer too small");
+    std::copy(d.begin(), d.end(), diff_out);
+  }
   return SDR_OK;
 }
 

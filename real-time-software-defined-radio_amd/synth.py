@@ -13,14 +13,51 @@ import numpy as np
 FS = 2.4e6
 
 
+# RDS block coding (IEC 62106): 26-bit blocks = 16 information bits + 10-bit checkword,
+# checkword = (m(x) x^10 mod g(x)) XOR offset word; g(x) = x^10+x^8+x^7+x^5+x^4+x^3+1.
+RDS_POLY = 0x5B9
+RDS_OFFSETS = {"A": 0x0FC, "B": 0x198, "C": 0x168, "D": 0x1B4}
+
+
+def rds_block_bits(info: int, offset: str) -> list:
+    """26 bits (MSB first) of one RDS block."""
+    reg = (info & 0xFFFF) << 10
+    for b in range(25, 9, -1):
+        if reg & (1 << b):
+            reg ^= RDS_POLY << (b - 10)
+    word = ((info & 0xFFFF) << 10) | ((reg & 0x3FF) ^ RDS_OFFSETS[offset])
+    return [(word >> (25 - k)) & 1 for k in range(26)]
+
+
+def rds_symbols(nbits: int, seed: int = 0) -> np.ndarray:
+    """+-1 biphase symbols (2 per bit, 2375 symbols/s) of a stream of RDS groups (A B C D
+    blocks, random information words): differential encoding e_t = e_(t-1) xor d_t, then
+    Manchester e=1 -> (+1, -1), e=0 -> (-1, +1) -- the inverse of the decoder in
+    model/fmRDSblock.py:250-292."""
+    rng = np.random.default_rng(seed)
+    bits = []
+    while len(bits) < nbits:
+        for off in "ABCD":
+            bits += rds_block_bits(int(rng.integers(0, 1 << 16)), off)
+    e, sym = 0, np.empty(2 * nbits)
+    for t in range(nbits):
+        e ^= bits[t]
+        sym[2 * t], sym[2 * t + 1] = (1.0, -1.0) if e else (-1.0, 1.0)
+    return sym
+
+
 def fm_iq(n_complex: int, seed: int = 0, fs: float = FS, snr_db: float = 30.0, chunk: int = 1 << 22,
-          dtype=np.float32) -> np.ndarray:
-    """Interleaved float32 IQ of `n_complex` samples (generated in chunks to bound memory)."""
+          dtype=np.float32, rds_groups: bool = False, rds_phase: float = 0.0) -> np.ndarray:
+    """Interleaved float32 IQ of `n_complex` samples (generated in chunks to bound memory).
+    rds_groups: the 57 kHz subcarrier carries coded RDS groups (rds_symbols) at carrier
+    phase `rds_phase` instead of random symbols."""
     rng = np.random.default_rng(seed)
     out = np.empty(2 * n_complex, dtype=np.float32)
     sym_len = fs / 2375.0
     nsym = int(np.ceil(n_complex / sym_len)) + 2
     symbols = rng.choice(np.array([-1.0, 1.0]), size=nsym)
+    if rds_groups:
+        symbols = rds_symbols((nsym + 1) // 2, seed)[:nsym]
     noise_rng = np.random.default_rng(seed + 1_000_003)
     amp = 0.5
     sigma = amp / np.sqrt(2.0) * 10 ** (-snr_db / 20.0)
@@ -33,7 +70,7 @@ def fm_iq(n_complex: int, seed: int = 0, fs: float = FS, snr_db: float = 30.0, c
         rds = symbols[((start + np.arange(n)) / sym_len).astype(np.int64)]
         mpx = (0.45 * (left + right) / 2 + 0.1 * np.cos(2 * np.pi * 19e3 * t)
                + 0.45 * (left - right) / 2 * np.cos(2 * np.pi * 38e3 * t)
-               + 0.05 * rds * np.cos(2 * np.pi * 57e3 * t))
+               + 0.05 * rds * np.cos(2 * np.pi * 57e3 * t + rds_phase))
         phi = phase0 + 2 * np.pi * 75e3 * np.cumsum(mpx) / fs
         phase0 = float(phi[-1])
         noise = noise_rng.standard_normal((n, 2)) * sigma
