@@ -1,0 +1,215 @@
+// fm_radio_gpu: the live receiver -- u8 IQ on stdin, interleaved int16
+// L/R at 48 kHz on stdout, every DSP stage on the GPU through libsdr's C-ABI.
+//
+//   rtl_sdr -f 99.9M -s 2.4M - | fm_radio_gpu | aplay -f S16_LE -c 2 -r 48000
+//
+// Replaces the mode-0 runtime of src/fm_radio.cpp: readStdInBlock (src/iofunc.cpp:61-69,
+// blocks of 307 200 bytes, :23), rf_thread (:31-147), mono_stero_thread (:150-318) and its
+// int16 writer (:286-302, value * 16384, NaN -> 0).  The DSP follows the Python model
+// (model/fmMonoBlock.py:80-173 with the intended combiner) with firwin taps,
+// as the parity oracle does; the reference C++'s own tap designs and its per-block state
+// resets are not reproduced.
+//
+// Runtime: instead of four threads and a mutex/condvar queue, one host thread and the
+// context's HIP stream with a two-slot pinned ring: while the GPU processes block k
+// (async H2D, kernels, async D2H), the host writes block k-1's audio and reads block k+1.
+// All filter / demod / PLL state stays in device memory between blocks.
+//
+// Options: --mono (mono only, both channels = mono), --rf-taps N (default 151, the
+// reference's), --blocks N (stop after N blocks).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/sdr.h"
+
+namespace {
+
+constexpr int64_t kBlock = 153600;     // complex samples per block (307 200 bytes, src/fm_radio.cpp:23)
+constexpr int SDR_MAX_TAPS_ABI = 256;
+
+[[noreturn]] void die(const char* what) {
+  std::fprintf(stderr, "fm_radio_gpu: %s: %s\n", what, sdr_last_error());
+  std::exit(1);
+}
+void ck(int rc, const char* what) {
+  if (rc != SDR_OK) die(what);
+}
+void hk(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "fm_radio_gpu: %s: %s\n", what, hipGetErrorString(e));
+    std::exit(1);
+  }
+}
+
+// scipy.signal.firwin(numtaps, cutoff, window='hann'[, pass_zero='bandpass']) with
+// scale=True (scipy/signal/_fir_filter_design.py): windowed sum of sincs, normalised to
+// unit gain at DC (low-pass) or at the band centre (band-pass).
+double sinc(double x) { return x == 0.0 ? 1.0 : std::sin(M_PI * x) / (M_PI * x); }
+std::vector<double> firwin(int n, double lo, double hi) {   // lo = 0: low-pass to hi
+  std::vector<double> h(n);
+  const double alpha = 0.5 * (n - 1);
+  for (int k = 0; k < n; ++k) {
+    const double m = k - alpha;
+    double v = hi * sinc(hi * m);
+    if (lo > 0.0) v -= lo * sinc(lo * m);
+    const double w = 0.5 - 0.5 * std::cos(2.0 * M_PI * k / (n - 1));
+    h[k] = v * w;
+  }
+  const double f = lo > 0.0 ? 0.5 * (lo + hi) : 0.0;
+  double s = 0.0;
+  for (int k = 0; k < n; ++k) s += h[k] * std::cos(M_PI * (k - alpha) * f);
+  for (double& v : h) v /= s;
+  return h;
+}
+
+struct Dev {
+  sdr_ctx* c;
+  void* alloc(int64_t bytes) {
+    void* p = nullptr;
+    ck(sdr_malloc(c, bytes, &p), "sdr_malloc");
+    ck(sdr_memset(c, p, 0, bytes), "sdr_memset");
+    return p;
+  }
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  bool mono = false, print_taps = false;
+  int rf_taps = 151;
+  long long max_blocks = -1;
+  for (int i = 1; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--mono")) mono = true;
+    else if (!std::strcmp(argv[i], "--print-taps")) print_taps = true;
+    else if (!std::strcmp(argv[i], "--rf-taps") && i + 1 < argc) rf_taps = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--blocks") && i + 1 < argc) max_blocks = std::atoll(argv[++i]);
+    else {
+      std::fprintf(stderr, "usage: fm_radio_gpu [--mono] [--rf-taps N] [--blocks N] [--print-taps] "
+                           "< iq_u8 > pcm_s16le_stereo\n");
+      return 2;
+    }
+  }
+  if (rf_taps < 3 || rf_taps > SDR_MAX_TAPS_ABI) {
+    std::fprintf(stderr, "fm_radio_gpu: --rf-taps %d out of range\n", rf_taps);
+    return 2;
+  }
+  // taps (model/fmMonoBlock.py:22-45, :115, :150, :159)
+  const std::vector<double> rf_b = firwin(rf_taps, 0.0, 100e3 / 1.2e6);
+  const std::vector<double> au_b = firwin(151, 0.0, 16e3 / 120e3);
+  const std::vector<double> pil_b = firwin(151, 18.5e3 / 120e3, 19.5e3 / 120e3);
+  const std::vector<double> ext_b = firwin(151, 22e3 / 120e3, 54e3 / 120e3);
+  const std::vector<double> ste_b = firwin(151, 0.0, 16e3 / 120e3);
+  if (print_taps) {                    // (no GPU) one line per filter, for the design test
+    for (const auto* t : {&rf_b, &au_b, &pil_b, &ext_b, &ste_b}) {
+      for (size_t k = 0; k < t->size(); ++k) std::printf(k ? " %.17g" : "%.17g", (*t)[k]);
+      std::printf("\n");
+    }
+    return 0;
+  }
+  sdr_ctx* c = nullptr;
+  const char* dev_env = std::getenv("SDR_DEVICE");
+  ck(sdr_create(dev_env ? std::atoi(dev_env) : 0, &c), "sdr_create");
+  hipStream_t st = static_cast<hipStream_t>(sdr_stream(c));
+  Dev d{c};
+  const int64_t M = kBlock / 10, A = M / 5, Z = rf_taps - 1;
+
+  // device state and intermediates (persist across blocks)
+  auto* d_iq = static_cast<uint8_t*>(d.alloc(2 * kBlock));
+  auto* rf_st = static_cast<double*>(d.alloc(8 * (2 * Z + 1)));    // zi_i | zi_q | phase
+  auto* d_dm = static_cast<float*>(d.alloc(4 * M + 16));
+  auto* d_au = static_cast<float*>(d.alloc(4 * A + 16));
+  auto* zi_au = static_cast<double*>(d.alloc(8 * 150));
+  auto* zi_pil = static_cast<double*>(d.alloc(8 * 150));
+  auto* zi_ext = static_cast<double*>(d.alloc(8 * 150));
+  auto* zi_ste = static_cast<double*>(d.alloc(8 * 150));
+  auto* d_bpr = static_cast<float*>(d.alloc(4 * M + 16));
+  auto* d_bpe = static_cast<float*>(d.alloc(4 * M + 16));
+  auto* d_nco = static_cast<float*>(d.alloc(4 * (M + 1) + 16));
+  auto* d_st = static_cast<float*>(d.alloc(4 * A + 16));
+  auto* d_l = static_cast<float*>(d.alloc(4 * A + 16));
+  auto* d_r = static_cast<float*>(d.alloc(4 * A + 16));
+  auto* pll = static_cast<double*>(d.alloc(8 * 6));
+  const double pll0[6] = {0.0, 0.0, 1.0, 0.0, 1.0, 0.0};             // model/fmMonoBlock.py:76
+  hk(hipMemcpyAsync(pll, pll0, sizeof pll0, hipMemcpyHostToDevice, st), "pll state");   // after the memsets
+  hk(hipStreamSynchronize(st), "hipStreamSynchronize");
+
+  // two-slot pinned ring
+  uint8_t* h_in[2];
+  float* h_out[2];
+  hipEvent_t done[2];
+  for (int k = 0; k < 2; ++k) {
+    hk(hipHostMalloc(reinterpret_cast<void**>(&h_in[k]), 2 * kBlock, hipHostMallocDefault), "hipHostMalloc");
+    hk(hipHostMalloc(reinterpret_cast<void**>(&h_out[k]), 8 * A, hipHostMallocDefault), "hipHostMalloc");
+    hk(hipEventCreateWithFlags(&done[k], hipEventDisableTiming), "hipEventCreate");
+  }
+  std::vector<int16_t> pcm(2 * A);
+  auto emit = [&](int slot) {          // block in h_out[slot] -> int16 L/R (src/fm_radio.cpp:286-302)
+    hk(hipEventSynchronize(done[slot]), "hipEventSynchronize");
+    const float* L = h_out[slot];
+    const float* R = h_out[slot] + A;
+    for (int64_t i = 0; i < A; ++i) {
+      pcm[2 * i] = std::isnan(L[i]) ? 0 : static_cast<int16_t>(L[i] * 16384.0f);
+      pcm[2 * i + 1] = std::isnan(R[i]) ? 0 : static_cast<int16_t>(R[i] * 16384.0f);
+    }
+    if (std::fwrite(pcm.data(), sizeof(int16_t), pcm.size(), stdout) != pcm.size()) std::exit(0);
+  };
+  auto read_block = [&](uint8_t* dst) {
+    size_t got = 0;
+    while (got < (size_t)(2 * kBlock)) {
+      const size_t r = std::fread(dst + got, 1, 2 * kBlock - got, stdin);
+      if (r == 0) return false;        // EOF: a partial last block is dropped (as :106-109)
+      got += r;
+    }
+    return true;
+  };
+
+  long long k = 0;
+  int pending = -1;                    // slot whose audio is still to be written
+  while ((max_blocks < 0 || k < max_blocks) && read_block(h_in[k & 1])) {
+    const int slot = (int)(k & 1);
+    hk(hipMemcpyAsync(d_iq, h_in[slot], 2 * kBlock, hipMemcpyHostToDevice, st), "H2D");
+    ck(sdr_rf_frontend_dev(c, d_iq, SDR_IQ_U8, kBlock, kBlock, 0, 1, rf_b.data(), rf_taps, 10, rf_st,
+                           rf_st + Z, Z, rf_st, rf_st + Z, rf_st + 2 * Z, d_dm, M, nullptr, nullptr),
+       "front end");                                                  // :86-98
+    ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, au_b.data(), 151, 5, zi_au, 150, zi_au,
+                   d_au, A), "mono");                                 // :101-109
+    const float* out_l = d_au;
+    const float* out_r = d_au;
+    if (!mono) {
+      ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, pil_b.data(), 151, 1, zi_pil, 150,
+                     zi_pil, d_bpr, M), "pilot BPF");                 // :115-117
+      ck(sdr_pll_dev(c, d_bpr, M, M, 1, 19e3, 240e3, 2.0, 0.0, 0.01, pll, d_nco, nullptr, M + 1), "PLL");  // :119
+      ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, ext_b.data(), 151, 1, zi_ext, 150,
+                     zi_ext, d_bpe, M), "stereo BPF");                // :150-151
+      ck(sdr_fir_dev(c, d_bpe, d_nco, 2.f, SDR_PRE_MIX, M, M, 0, 1, ste_b.data(), 151, 5, zi_ste, 150,
+                     zi_ste, d_st, A), "stereo LPF");                 // :155-162
+      ck(sdr_stereo_combine_dev(c, d_au, d_st, A, d_l, d_r), "combine");   // :166-170
+      out_l = d_l;
+      out_r = d_r;
+    }
+    if (pending >= 0) {                // before reusing this slot's output buffer
+      emit(pending);
+      pending = -1;
+    }
+    hk(hipMemcpyAsync(h_out[slot], out_l, 4 * A, hipMemcpyDeviceToHost, st), "D2H");
+    hk(hipMemcpyAsync(h_out[slot] + A, out_r, 4 * A, hipMemcpyDeviceToHost, st), "D2H");
+    hk(hipEventRecord(done[slot], st), "hipEventRecord");
+    pending = slot;
+    ++k;
+  }
+  if (pending >= 0) emit(pending);
+  std::fflush(stdout);
+  for (int s = 0; s < 2; ++s) {
+    (void)hipHostFree(h_in[s]);
+    (void)hipHostFree(h_out[s]);
+    (void)hipEventDestroy(done[s]);
+  }
+  sdr_destroy(c);
+  std::fprintf(stderr, "fm_radio_gpu: %lld blocks\n", k);
+  return 0;
+}

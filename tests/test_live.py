@@ -1,0 +1,56 @@
+"""Live receiver fm_radio_gpu: u8 IQ on stdin -> int16 L/R on stdout,
+the mode-0 runtime of src/fm_radio.cpp (:31-318, int16 writer :286-302) on the GPU."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+BIN = os.path.join(ROOT, "real-time-software-defined-radio_amd", "fm_radio_gpu")
+B = 153_600
+
+
+def to_pcm(left, right):
+    """src/fm_radio.cpp:288-297: NaN -> 0, else (short)(x * 16384), truncation toward 0."""
+    out = np.empty(2 * len(left), dtype=np.int16)
+    for k, x in ((0, left), (1, right)):
+        x = np.asarray(x, dtype=np.float32)
+        v = np.trunc(x * np.float32(16384.0))
+        out[k::2] = np.where(np.isnan(x), 0, v).astype(np.int16)
+    return out
+
+
+def test_taps_match_firwin(sdr):
+    """The C++ firwin reproduces scipy.signal.firwin (model/fmMonoBlock.py:43-45, :115, :150, :159)."""
+    res = subprocess.run([BIN, "--print-taps"], capture_output=True, text=True, check=True)
+    rows = [np.array([float(v) for v in line.split()]) for line in res.stdout.splitlines()]
+    rf, au = sdr.design.mono_coeffs(151, 151)
+    pil, ext, ste = sdr.design.stereo_coeffs(151)
+    for got, ref in zip(rows, (rf, au, pil, ext, ste)):
+        assert got.shape == ref.shape and np.max(np.abs(got - ref)) < 1e-15
+
+
+def test_usage_error_exit_code():
+    assert subprocess.run([BIN, "--bogus"], capture_output=True).returncode == 2
+
+
+@pytest.mark.gpu
+def test_live_pipeline_matches_block_processor_and_oracle(sdr, gpu_ctx, oracle):
+    nb = 4
+    iq = sdr.synth.fm_iq(nb * B, seed=9, dtype=np.uint8)
+    res = subprocess.run([BIN], input=iq.tobytes() + b"\x80" * 1000, capture_output=True, check=True, timeout=120)
+    pcm = np.frombuffer(res.stdout, dtype=np.int16)
+    assert pcm.shape == (nb * 2 * (B // 50),)      # the trailing partial block is dropped
+    rf, au = sdr.design.mono_coeffs(151, 151)
+    proc = sdr.StereoBlockProcessor(B, rf, au, iq_dtype=np.uint8)
+    ref = np.concatenate([to_pcm(o["left"], o["right"]) for o in
+                          (proc.process(iq[2 * k * B:2 * (k + 1) * B]) for k in range(nb))])
+    assert np.max(np.abs(pcm.astype(np.int32) - ref)) <= 1
+    x = (iq.astype(np.float64) - 128.0) / 128.0
+    orc = oracle.mono_stereo_blocks(x, B, rf_taps=151, audio_taps=151, stereo=True, nblocks=nb)
+    ora = np.concatenate([to_pcm(r["left"], r["right"]) for r in orc])   # (:80 drops the last block)
+    assert len(ora) == (nb - 1) * 2 * (B // 50)
+    d = np.abs(pcm[:len(ora)].astype(np.int32) - ora)
+    assert d.max() <= 1 and np.mean(d > 0) < 0.01
