@@ -345,8 +345,10 @@ int sdr_rf_frontend_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int
     zfi = tmp;
     zfq = tmp + zs * nstreams;
   }
+  // u8: the slot kernel takes any stream stride (streams whose base is not 4-B aligned
+  // build their images with guarded byte loads); f32 needs 16-B aligned stream bases
   const bool fast = (taps == 101 || taps == 151) && decim == 10 &&
-                    (nstreams <= 1 || stride % G == 0) && ((uintptr_t)iq % 16) == 0;
+                    (nstreams <= 1 || u8 || stride % G == 0) && ((uintptr_t)iq % (u8 ? 4 : 16)) == 0;
   if (fast) {
     FeLaunch a{iq, n, nstreams > 1 ? stride : ceil_div(n, G) * G, hist, nstreams,
                ts->dev_f32, &ts->h, taps, decim, u8, zi_i, zi_q, zs, prev_phase,

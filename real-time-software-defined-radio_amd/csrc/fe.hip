@@ -1790,7 +1790,10 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
   };
   int s1, i1;
   next_of(s, i, s1, i1);
-  bool stg1 = U > 1 && s1 == s && interior(n_lo_of(i1));   // next image comes through the stage
+  // u8 stage loads are dwords: a stream whose base is not 4-B aligned (odd stride, odd
+  // stream) builds every image with guarded byte loads instead
+  auto staged_ok = [&](int ss) { return !U8 || (((int64_t)ss * p.stride) & 1) == 0; };
+  bool stg1 = U > 1 && s1 == s && interior(n_lo_of(i1)) && staged_ok(s1);   // next image via the stage
   if (PIPE == 0 && stg1) load_stage(s1, n_lo_of(i1));
 
   for (int u = 0; u < U; ++u) {
@@ -1958,7 +1961,7 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
       i = i1;
       if (FUSED && !have) own();
       next_of(s, i, s1, i1);
-      stg1 = u + 2 < U && s1 == s && interior(n_lo_of(i1));
+      stg1 = u + 2 < U && s1 == s && interior(n_lo_of(i1)) && staged_ok(s1);
       if (PIPE == 0 && stg1) load_stage(s1, n_lo_of(i1));
     }
     // (PIPE 0) queued behind the next tile's loads
@@ -2050,6 +2053,7 @@ static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
   if (tiles <= 0) return hipSuccess;
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
   if constexpr (U8) {
+    if (a.nstreams > 1 && a.stride % 8 != 0 && !use_slot(false)) return hipErrorInvalidValue;
     if (use_slot(false)) {   // u8 IQ: the slot kernel (2 B per sample staged, converted on write)
       SlotArgs sa{};
       sa.tps = (int)((M + 191) / 192);

@@ -54,3 +54,17 @@ def test_live_pipeline_matches_block_processor_and_oracle(sdr, gpu_ctx, oracle):
     assert len(ora) == (nb - 1) * 2 * (B // 50)
     d = np.abs(pcm[:len(ora)].astype(np.int32) - ora)
     assert d.max() <= 1 and np.mean(d > 0) < 0.01
+
+
+@pytest.mark.gpu
+def test_live_pipeline_mono(sdr, gpu_ctx):
+    """--mono: both channels carry the mono audio of MonoBlockProcessor (u8, 151 taps)."""
+    nb = 3
+    iq = sdr.synth.fm_iq(nb * B, seed=12, dtype=np.uint8)
+    res = subprocess.run([BIN, "--mono"], input=iq.tobytes(), capture_output=True, check=True, timeout=120)
+    pcm = np.frombuffer(res.stdout, dtype=np.int16)
+    rf, au = sdr.design.mono_coeffs(151, 151)
+    proc = sdr.MonoBlockProcessor(B, rf, au, iq_dtype=np.uint8)
+    a = np.concatenate([proc.process(iq[2 * k * B:2 * (k + 1) * B]) for k in range(nb)])
+    ref = to_pcm(a, a)
+    assert pcm.shape == ref.shape and np.max(np.abs(pcm.astype(np.int32) - ref)) <= 1
