@@ -1549,24 +1549,34 @@ void fe_circ_kernel(FeParams p, TapsF32 taps, RingArgs a) {
 // lfilter final state zf for the I and Q channels of an interleaved IQ block
 // (scipy _signaltools.py:2153-2172), computed in f64:
 //   zf[k] = sum_{j=k+1}^{T-1} b[j] * x[N-1-(j-k-1)]  +  (N+k < T-1 ? zi[N+k] : 0)
+// One 256-thread block per stream (T <= 256): the T-1 newest samples and the taps are
+// staged in LDS, then each output's f64 dot product runs from LDS.
 template <bool U8>
-__global__ void iq_zf_kernel(const void* iq_all, int64_t n, int64_t stride, const double* b, int T,
-                             const double* zi_i, const double* zi_q, int64_t zi_stride,
-                             double* zf_i, double* zf_q) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= T - 1) return;
+__global__ __launch_bounds__(256) void iq_zf_kernel(const void* iq_all, int64_t n, int64_t stride,
+                                                    const double* b, int T, const double* zi_i,
+                                                    const double* zi_q, int64_t zi_stride,
+                                                    double* zf_i, double* zf_q) {
+  __shared__ float2 xs[SDR_MAX_TAPS];   // xs[i] = x[n-1-i]
+  __shared__ double bs[SDR_MAX_TAPS];
+  const int k = threadIdx.x;
   const int s = blockIdx.y;
   const void* iq = reinterpret_cast<const char*>(iq_all) + (int64_t)s * stride * (U8 ? 2 : 8);
   if (zi_i != nullptr) { zi_i += (int64_t)s * zi_stride; zi_q += (int64_t)s * zi_stride; }
   zf_i += (int64_t)s * zi_stride;
   zf_q += (int64_t)s * zi_stride;
+  const int L = (int)min<int64_t>(n, T - 1);
+  if (k < L) xs[k] = IqLoad<U8>::load1(iq, n - 1 - k);
+  if (k < T) bs[k] = b[k];
+  __syncthreads();
+  if (k >= T - 1) return;
+  // zf[k] = sum_{j=k+1}^{T-1} b[j] x[n-1-(j-k-1)] over the terms with a sample (j-k-1 < n)
+  const int jhi = (int)min<int64_t>(T - 1, n + k);
   double si = 0.0, sq = 0.0;
-  for (int j = k + 1; j < T; ++j) {
-    const int64_t idx = n - 1 - (j - k - 1);
-    if (idx < 0) break;
-    float2 x = IqLoad<U8>::load1(iq, idx);
-    si = fma(b[j], (double)x.x, si);
-    sq = fma(b[j], (double)x.y, sq);
+#pragma unroll 4
+  for (int j = k + 1; j <= jhi; ++j) {
+    const float2 v = xs[j - k - 1];
+    si = fma(bs[j], (double)v.x, si);
+    sq = fma(bs[j], (double)v.y, sq);
   }
   if (n + k < T - 1 && zi_i != nullptr) {
     si += zi_i[n + k];
@@ -2168,7 +2178,8 @@ hipError_t sdr_launch_iq_zf(const void* iq, int u8, int64_t n, int64_t stride, i
                             const double* b_dev, int T, const double* zi_i, const double* zi_q,
                             int64_t zi_stride, double* zf_i, double* zf_q, hipStream_t st) {
   if (T <= 1 || nstreams <= 0) return hipSuccess;
-  const dim3 grid((T - 1 + 255) / 256, nstreams);
+  if (T > SDR_MAX_TAPS) return hipErrorInvalidValue;
+  const dim3 grid(1, nstreams);
   if (u8)
     hipLaunchKernelGGL(iq_zf_kernel<true>, grid, dim3(256), 0, st, iq, n, stride, b_dev, T, zi_i, zi_q, zi_stride, zf_i, zf_q);
   else

@@ -188,28 +188,41 @@ __global__ __launch_bounds__(256) void resample_kernel(const float* x, int64_t n
 // lfilter final state (f64) for a real stream after an optional pre-op and an
 // optional zero-stuffing factor U (U = 1: plain stream):
 //   zf[k] = sum_{j=k+1}^{T-1} b[j] u[NU+k-j] + (NU+k < T-1 ? zi[NU+k] : 0),  NU = n*U.
-__global__ void zf_kernel(const float* x, const float* c, float gain, int pre, int64_t n,
-                          int64_t x_stride, int U, const double* b, int T, const double* zi,
-                          int64_t zi_stride, double* zf) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= T - 1) return;
+// One 256-thread block per stream (T <= SDR_MAX_TAPS = 256): the <= T-1 newest inputs
+// (pre-op applied) and the taps are staged in LDS first, so the per-output f64 dot
+// product runs from LDS instead of waiting a global-memory round trip per term.
+__global__ __launch_bounds__(256) void zf_kernel(const float* x, const float* c, float gain, int pre,
+                                                 int64_t n, int64_t x_stride, int U, const double* b,
+                                                 int T, const double* zi, int64_t zi_stride, double* zf) {
+  __shared__ double us[SDR_MAX_TAPS];
+  __shared__ double bs[SDR_MAX_TAPS];
+  const int k = threadIdx.x;
   const int s = blockIdx.y;
   x += (int64_t)s * x_stride;
   if (c != nullptr) c += (int64_t)s * x_stride;
   if (zi != nullptr) zi += (int64_t)s * zi_stride;
   zf += (int64_t)s * zi_stride;
   const int64_t nu = n * U;
-  double acc = 0.0;
-  for (int j = k + 1; j < T; ++j) {
-    const int64_t idx = nu + k - j;
-    if (idx < 0) break;
-    if (idx % U) continue;
-    const int64_t xi = idx / U;
+  // inputs used: x[n-L .. n-1], L = min(n, floor((T-1)/U)); us[i] = u(x[n-1-i])
+  const int L = (int)min<int64_t>(n, (T - 1) / U);
+  if (k < L) {
+    const int64_t xi = n - 1 - k;
     double v = (double)x[xi];
     if (pre == PRE_SQUARE) v = v * v;
     else if (pre == PRE_MIX) v = (double)((x[xi] * c[xi]) * gain);
-    acc = fma(b[j], v, acc);
+    us[k] = v;
   }
+  if (k < T) bs[k] = b[k];
+  __syncthreads();
+  if (k >= T - 1) return;
+  // The terms with idx = nu + k - j >= 0 on the zero-stuffed grid (idx % U == 0): since
+  // nu % U == 0 that is j = k (mod U), so j walks k+U, k+2U, ... up to min(T-1, nu+k) while
+  // the input walks back from x[n-1] -- same terms, same ascending-j order, no divisions.
+  const int jhi = (int)min<int64_t>(T - 1, nu + k);
+  double acc = 0.0;
+  int i = 0;
+#pragma unroll 4
+  for (int j = k + U; j <= jhi; j += U, ++i) acc = fma(bs[j], us[i], acc);
   if (zi != nullptr && nu + k < T - 1) acc += zi[nu + k];
   zf[k] = acc;
 }
@@ -299,7 +312,8 @@ hipError_t sdr_launch_zf(const float* x, const float* c, float gain, int pre, in
                          int64_t x_stride, int nstreams, int U, const double* b_dev, int T,
                          const double* zi, int64_t zi_stride, double* zf, hipStream_t st) {
   if (T <= 1 || nstreams <= 0) return hipSuccess;
-  hipLaunchKernelGGL(zf_kernel, dim3((T - 1 + 255) / 256, nstreams), dim3(256), 0, st, x, c, gain,
+  if (T > SDR_MAX_TAPS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(zf_kernel, dim3(1, nstreams), dim3(256), 0, st, x, c, gain,
                      pre, n, x_stride, U, b_dev, T, zi, zi_stride, zf);
   return hipGetLastError();
 }

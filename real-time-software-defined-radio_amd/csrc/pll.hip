@@ -57,7 +57,7 @@ __global__ __launch_bounds__(64) void pll_loop_kernel(const float* in, int64_t n
   const int s = blockIdx.x;
   const int lane = threadIdx.x;
   if (s >= nstreams) return;
-  __shared__ float xs[2][PCH];
+  __shared__ alignas(16) float xs[2][PCH];
   __shared__ double ths[PCH];
   const float* x = in + (int64_t)s * in_stride;
   double* st = state + (int64_t)s * state_stride;
@@ -66,7 +66,33 @@ __global__ __launch_bounds__(64) void pll_loop_kernel(const float* in, int64_t n
   const double off = st[5];
   const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
   double arg = 0.0;
-  bool literal = true;  // first sample uses the caller's (fI, fQ)
+  // One step of model/fmPll.py:23-41.  General form: the first sample of a call uses the
+  // caller's (fI, fQ) literally, and an input of 0 or NaN takes atan2 on the products.
+  auto general = [&](float xf, int64_t k, bool literal) {
+    const double xv = (double)xf;
+    double e;
+    if (literal || !(xv > 0.0 || xv < 0.0)) {
+      if (!literal) { fI = cos(arg); fQ = sin(arg); }
+      e = atan2(xv * (-fQ), xv * fI);
+    } else {
+      e = reduce_2pi(xv > 0.0 ? -arg : kPi - arg);
+      if (e <= -kPi) e += 2.0 * kPi;   // atan2 range is (-pi, pi]
+    }
+    integ = integ + cfg.ki * e;
+    phase = phase + cfg.kp * e + integ;
+    arg = w * ((off + (double)k) + 1.0) + phase;
+  };
+  // Fast form for x != 0: atan2(-x sin a, x cos a) = wrap(-a) or wrap(pi - a), branch-free;
+  // `base` = (off + k) + 1 kept as a running exact integer in double (< 2^53).
+  double base = 0.0;
+  auto fast = [&](float xf) {
+    const double r = reduce_2pi(xf > 0.f ? -arg : kPi - arg);
+    const double e = r <= -kPi ? r + 2.0 * kPi : r;
+    integ = integ + cfg.ki * e;
+    phase = phase + cfg.kp * e + integ;
+    base = base + 1.0;
+    arg = w * base + phase;
+  };
   constexpr int PL = PCH / 64;
   const int64_t nch = (n + PCH - 1) / PCH;
   for (int j = 0; j < PL; ++j) {
@@ -83,23 +109,44 @@ __global__ __launch_bounds__(64) void pll_loop_kernel(const float* in, int64_t n
       pre[j] = k < n ? x[k] : 0.f;
     }
     const int kn = (int)min<int64_t>(PCH, n - c * PCH);
-#pragma unroll 8
-    for (int kk = 0; kk < kn; ++kk) {
-      const int64_t k = c * PCH + kk;
-      const double xv = (double)xs[buf][kk];
-      double e;
-      if (literal || !(xv > 0.0 || xv < 0.0)) {
-        if (!literal) { fI = cos(arg); fQ = sin(arg); }
-        e = atan2(xv * (-fQ), xv * fI);
-      } else {
-        e = reduce_2pi(xv > 0.0 ? -arg : kPi - arg);
-        if (e <= -kPi) e += 2.0 * kPi;   // atan2 range is (-pi, pi]
+    const float* xc = xs[buf];
+    int kk = 0;
+    if (c == 0) {                                // the literal first sample
+      general(xc[0], 0, true);
+      if (lane == 0) ths[0] = arg;
+      kk = 1;
+    }
+    // wave vote: does the chunk hold a 0 or NaN input (the general form's other case)?
+    bool odd = false;
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      const int e = lane + 64 * j;
+      const float v = xc[e];
+      odd |= e < kn && !(v > 0.f || v < 0.f);
+    }
+    if (__any(odd)) {
+      for (; kk < kn; ++kk) {
+        general(xc[kk], c * PCH + kk, false);
+        if (lane == 0) ths[kk] = arg;
       }
-      literal = false;
-      integ = integ + cfg.ki * e;
-      phase = phase + cfg.kp * e + integ;
-      arg = w * ((off + (double)k) + 1.0) + phase;
-      if (lane == 0) ths[kk] = arg;
+    } else {
+      base = (off + (double)(c * PCH + kk - 1)) + 1.0;
+      // groups of 4: the next group's LDS reads are in flight during this group's steps
+      const int ng = (kn - kk) / 4;
+      float n0 = xc[kk], n1 = xc[kk + 1], n2 = xc[kk + 2], n3 = xc[kk + 3];  // kk+3 < PCH
+      for (int g = 0; g < ng; ++g, kk += 4) {
+        const float c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+        if (g + 1 < ng) { n0 = xc[kk + 4]; n1 = xc[kk + 5]; n2 = xc[kk + 6]; n3 = xc[kk + 7]; }
+        fast(c0); const double a0 = arg;
+        fast(c1); const double a1 = arg;
+        fast(c2); const double a2 = arg;
+        fast(c3);
+        if (lane == 0) { ths[kk] = a0; ths[kk + 1] = a1; ths[kk + 2] = a2; ths[kk + 3] = arg; }
+      }
+      for (; kk < kn; ++kk) {
+        fast(xc[kk]);
+        if (lane == 0) ths[kk] = arg;
+      }
     }
     __syncthreads();
     for (int e = lane; e < kn; e += 64) th[c * PCH + e] = ths[e];

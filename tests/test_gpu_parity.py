@@ -187,6 +187,23 @@ def test_fm_pll_chained(sdr, gpu_ctx, golden):
         assert maxabs(st, u[f"pll{j}_state"]) < 1e-6, j
 
 
+def test_fm_pll_zero_and_signed_inputs(sdr, gpu_ctx, oracle):
+    """The PLL kernel's fast step (x != 0) and its general step (first sample of a call,
+    x == 0) across chunk boundaries (512 samples), chained over two calls."""
+    rng = np.random.default_rng(5)
+    t = np.arange(3000)
+    x = (np.cos(2 * np.pi * 19e3 / 240e3 * t + 0.3) + 0.05 * rng.standard_normal(3000)).astype(np.float32)
+    x[[0, 1, 511, 512, 513, 1024, 2047, 2999]] = 0.0        # zeros at chunk edges
+    x[1500:1540] = 0.0                                         # a run of zeros
+    st = [0.0, 0.0, 1.0, 0.0, 1.0, 0.0]
+    sr = list(st)
+    for a, b in ((0, 1700), (1700, 3000)):
+        nco, ncoq, st = sdr.fmPll(x[a:b], 19e3, 240e3, st, 2)
+        nr, nqr, sr = oracle.fm_pll(x[a:b].astype(np.float64), 19e3, 240e3, sr, 2)
+        assert maxabs(nco[1:], nr[1:]) < 2e-6 and maxabs(ncoq[1:], nqr[1:]) < 2e-6
+        assert maxabs(st, sr) < 1e-6
+
+
 def test_resample_matches_oracle(sdr, gpu_ctx, oracle):
     rng = np.random.default_rng(3)
     b = sdr.design.rds_coeffs()["anti_img"]
