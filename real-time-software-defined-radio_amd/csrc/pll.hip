@@ -86,7 +86,8 @@ __global__ __launch_bounds__(64) void pll_loop_kernel(const float* in, int64_t n
   // `base` = (off + k) + 1 kept as a running exact integer in double (< 2^53).
   double base = 0.0;
   auto fast = [&](float xf) {
-    const double r = reduce_2pi(xf > 0.f ? -arg : kPi - arg);
+    const double sel = xf > 0.f ? 0.0 : kPi;                 // off the chain: x is known
+    const double r = reduce_2pi(sel - arg);
     const double e = r <= -kPi ? r + 2.0 * kPi : r;
     integ = integ + cfg.ki * e;
     phase = phase + cfg.kp * e + integ;
