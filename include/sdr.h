@@ -41,11 +41,14 @@ enum {
   SDR_EINVAL = -1,      /* bad argument (shape, NULL, range) */
   SDR_EHIP = -2,        /* HIP runtime error */
   SDR_ENOMEM = -3,      /* device allocation failed */
-  SDR_EUNSUPPORTED = -4 /* valid but not implemented configuration */
+  SDR_EUNSUPPORTED = -4, /* valid but not implemented configuration */
+  SDR_EDOMAIN = -5       /* math domain error the reference raises (log10 of 0) */
 };
 
 enum { SDR_IQ_F32 = 0, SDR_IQ_U8 = 1 };                  /* interleaved IQ sample types */
 enum { SDR_PRE_NONE = 0, SDR_PRE_SQUARE = 1, SDR_PRE_MIX = 2 }; /* FIR input pre-ops */
+enum { SDR_REAL_F32 = 0, SDR_REAL_F64 = 1 };              /* real sample types (PSD) */
+#define SDR_DFT_MAX_N (1 << 16)
 
 typedef struct sdr_ctx sdr_ctx;
 
@@ -173,6 +176,23 @@ int sdr_pll_dev(sdr_ctx* ctx, const float* in, int64_t n, int64_t in_stride, int
  * src/fm_radio.cpp:250-251): left = (mono+side)/2, right = (mono-side)/2. */
 int sdr_stereo_combine_dev(sdr_ctx* ctx, const float* mono, const float* side, int64_t n,
                            float* left, float* right);
+
+/* ---- spectral diagnostics -----------------------------------------
+ * Bartlett PSD, model/fmSupportLib.py:66-140 (estimatePSD; the C++ src/fourier.cpp:36-110
+ * advances sample and list positions by the same nfft/2 and is not the parity target):
+ * floor(n/nfft) non-overlapping segments, Hann window pow(sin(i*pi/nfft), 2), FFT in f64,
+ * 10*log10(2/(fs*nfft/2) * |X_k|^2) for k < nfft/2, averaged over segments in dB.
+ * psd: nfft/2 doubles (NaN when n < nfft, as the reference's 0/0).  nfft: a power of two in
+ * [2, SDR_PSD_MAX_NFFT = 4096].  SDR_EDOMAIN if a bin has zero power (the reference's
+ * math.log10 raises).  The frequency axis np.arange(0, fs/2, fs/nfft) is the caller's.
+ * sdr_psd: host f64 samples.  sdr_psd_dev: device samples (SDR_REAL_F32 / _F64), device psd. */
+int sdr_psd(sdr_ctx* ctx, const double* x, int64_t n, int nfft, double fs, double* psd);
+int sdr_psd_dev(sdr_ctx* ctx, const void* x, int dtype, int64_t n, int nfft, double fs, double* psd);
+
+/* Direct DFT, model/fmSupportLib.py:46-60: X_m = sum_k x_k exp(i*2*pi*(-k*m)/n), f64, the
+ * angle rounded as the reference's expression rounds it.  X: 2n doubles (re, im
+ * interleaved = numpy complex128).  n <= SDR_DFT_MAX_N. */
+int sdr_dft(sdr_ctx* ctx, const double* x, int64_t n, double* X);
 
 /* ---- RDS link layer (host code) -----------------------------------
  * model/fmRDSblock.py:207-346 (src/fm_radio.cpp:444-729 frame_thread): per block of the

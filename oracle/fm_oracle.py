@@ -338,3 +338,46 @@ def rds_link(rrc_blocks):
         r.update(symbols=s, bits=bits, diff=diff, events=events)
         out.append(r)
     return out
+
+
+# ---- spectral diagnostics --------------------------------------------
+def estimate_psd(samples, nfft, fs):
+    """Restatement of model/fmSupportLib.py:66-140 (estimatePSD): Bartlett estimate over
+    floor(len/nfft) non-overlapping segments; Hann window pow(sin(i*pi/N), 2) (:80-82);
+    np.fft.fft per segment (:101); 2 * (1/(Fs*N/2)) * |X_k|^2 for k < N/2 (:115-117);
+    10*log10 per bin (:120-121, raises on a zero bin); dB averaged over segments in
+    segment order (:128-137).  Returns (freq, psd_est)."""
+    x = np.asarray(samples, dtype=np.float64)
+    freq = np.arange(0, fs / 2, fs / nfft)
+    hann = np.array([math.sin(i * math.pi / nfft) ** 2 for i in range(nfft)])
+    nseg = len(x) // nfft
+    half = nfft // 2
+    rows = []
+    for k in range(nseg):
+        xf = np.fft.fft(x[k * nfft:(k + 1) * nfft] * hann, nfft)[:half]
+        p = 2 * (1 / (fs * nfft / 2) * np.abs(xf) ** 2)
+        if np.any(p <= 0):
+            raise ValueError("math domain error")
+        rows.append(10 * np.log10(p))
+    est = np.zeros(half)
+    for row in rows:
+        est += row
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return freq, est / nseg
+
+
+def dft(x):
+    """Restatement of model/fmSupportLib.py:46-60: X_m = sum_k x_k exp(i*2*pi*(-k*m)/N), the
+    angle rounded as the reference's expression rounds it, summed in k order."""
+    x = np.asarray(x, dtype=np.float64)
+    n = len(x)
+    k = np.arange(n, dtype=np.int64)
+    out = np.zeros(n, dtype=np.complex128)
+    for m in range(n):
+        ang = (2 * math.pi) * (-k * m).astype(np.float64) / n
+        terms = x * np.cos(ang) + 1j * (x * np.sin(ang))
+        acc = 0j
+        for t in terms:
+            acc += t
+        out[m] = acc
+    return out

@@ -15,7 +15,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SDR_LIB", os.path.join(_HERE, "libsdr.so"))
 
-SDR_OK, SDR_EINVAL, SDR_EHIP, SDR_ENOMEM, SDR_EUNSUPPORTED = 0, -1, -2, -3, -4
+SDR_OK, SDR_EINVAL, SDR_EHIP, SDR_ENOMEM, SDR_EUNSUPPORTED, SDR_EDOMAIN = 0, -1, -2, -3, -4, -5
+SDR_REAL_F32, SDR_REAL_F64 = 0, 1
 SDR_IQ_F32, SDR_IQ_U8 = 0, 1
 SDR_PRE_NONE, SDR_PRE_SQUARE, SDR_PRE_MIX = 0, 1, 2
 
@@ -70,6 +71,9 @@ SIGNATURES = {
     "sdr_pll_dev": (_i32, [_vp, _vp, _i64, _i64, _i32, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp,
                            _i64]),
     "sdr_stereo_combine_dev": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
+    "sdr_psd": (_i32, [_vp, _dp, _i64, _i32, _f64, _dp]),
+    "sdr_psd_dev": (_i32, [_vp, _vp, _i32, _i64, _i32, _f64, _vp]),
+    "sdr_dft": (_i32, [_vp, _dp, _i64, _dp]),
     "sdr_rds_link_create": (_i32, [_c.POINTER(_vp)]),
     "sdr_rds_link_destroy": (None, [_vp]),
     "sdr_rds_link_block": (_i32, [_vp, _dp, _i64, _vp, _i64, _c.POINTER(_i64), _vp, _i64, _c.POINTER(_i64),
@@ -115,6 +119,8 @@ def check(rc: int, what: str = "") -> None:
         raise NotImplementedError(msg)
     if rc == SDR_ENOMEM:
         raise MemoryError(msg)
+    if rc == SDR_EDOMAIN:
+        raise ValueError("math domain error: " + msg)   # as math.log10(0) raises
     raise SdrError(msg)
 
 

@@ -60,6 +60,9 @@ hipError_t sdr_launch_zf(const float* x, const float* c, float gain, int pre, in
                          const double* zi, int64_t zi_stride, double* zf, hipStream_t st);
 hipError_t sdr_launch_combine(const float* mono, const float* side, int64_t n, float* left,
                               float* right, hipStream_t st);
+hipError_t sdr_launch_psd(const void* x, int f64, int64_t n, int logn, double fs, double* seg_db,
+                          double* out, int* zero_flag, hipStream_t st);
+hipError_t sdr_launch_dft(const double* x, int64_t n, double* X, hipStream_t st);
 hipError_t sdr_launch_pll(const float* in, int64_t n, int64_t in_stride, int nstreams,
                           const PllCfg& cfg, double* state_dev, double* theta, int64_t th_stride,
                           double* nco0, double* ncoq0, float* nco_i, float* nco_q,
@@ -91,6 +94,7 @@ int fail(int code, const char* fmt, ...) {
 // scratch slots owned by a context (grown on demand, never shrunk)
 enum Slot {
   S_IN, S_IN2, S_OUT, S_OUT2, S_OUT3, S_OUT4, S_STATE, S_STATE2, S_MISC, S_THETA, S_PHI, S_WRAP,
+  S_PSD,
   S_NSLOT
 };
 
@@ -677,6 +681,65 @@ int sdr_pll(sdr_ctx* c, const float* in, int64_t n, double freq, double fs, doub
   TRY(d2h(c, nco_i, dO, sizeof(float) * (n + 1)));
   if (nco_q) TRY(d2h(c, nco_q, dO + (n + 1), sizeof(float) * (n + 1)));
   TRY(d2h(c, state6, ds, sizeof(double) * 6));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SDR_OK;
+}
+
+// ---- spectral diagnostics ------------------------------------------
+int sdr_psd_dev(sdr_ctx* c, const void* x, int dtype, int64_t n, int nfft, double fs, double* psd) {
+  CHECK_CTX(c);
+  if (n < 0) return fail(SDR_EINVAL, "negative size");
+  if (dtype != SDR_REAL_F32 && dtype != SDR_REAL_F64) return fail(SDR_EINVAL, "dtype %d", dtype);
+  if (nfft < 2 || nfft > SDR_PSD_MAX_NFFT || (nfft & (nfft - 1)))
+    return fail(SDR_EUNSUPPORTED, "nfft=%d: a power of two in [2, %d]", nfft, SDR_PSD_MAX_NFFT);
+  if (psd == nullptr || (n >= nfft && x == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  TRY(set_dev(c));
+  const int64_t nseg = n / nfft;
+  const int half = nfft / 2;
+  void* ws;
+  TRY(scratch(c, S_PSD, sizeof(double) * (size_t)(nseg * half) + 64, &ws));
+  int* flag = reinterpret_cast<int*>(static_cast<char*>(ws) + sizeof(double) * (size_t)(nseg * half));
+  HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
+  int logn = 0;
+  while ((1 << logn) < nfft) ++logn;
+  HIP_TRY(sdr_launch_psd(x, dtype == SDR_REAL_F64, n, logn, fs, static_cast<double*>(ws), psd, flag, c->stream));
+  int zero = 0;
+  HIP_TRY(hipMemcpyAsync(&zero, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (zero) return fail(SDR_EDOMAIN, "a bin with zero power: log10(0) (model/fmSupportLib.py:121 raises)");
+  return SDR_OK;
+}
+
+int sdr_psd(sdr_ctx* c, const double* x, int64_t n, int nfft, double fs, double* psd) {
+  CHECK_CTX(c);
+  if (n < 0) return fail(SDR_EINVAL, "negative size");
+  if (psd == nullptr || (n > 0 && x == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  if (nfft < 2 || nfft > SDR_PSD_MAX_NFFT || (nfft & (nfft - 1)))
+    return fail(SDR_EUNSUPPORTED, "nfft=%d: a power of two in [2, %d]", nfft, SDR_PSD_MAX_NFFT);
+  TRY(set_dev(c));
+  const int64_t used = n / nfft * nfft;
+  double *dx, *dp;
+  TRY(scratch(c, S_IN, sizeof(double) * (size_t)used, (void**)&dx));
+  TRY(scratch(c, S_OUT, sizeof(double) * (size_t)(nfft / 2), (void**)&dp));
+  TRY(h2d(c, dx, x, sizeof(double) * (size_t)used));
+  TRY(sdr_psd_dev(c, dx, SDR_REAL_F64, used, nfft, fs, dp));
+  TRY(d2h(c, psd, dp, sizeof(double) * (size_t)(nfft / 2)));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SDR_OK;
+}
+
+int sdr_dft(sdr_ctx* c, const double* x, int64_t n, double* X) {
+  CHECK_CTX(c);
+  if (n < 0 || n > SDR_DFT_MAX_N) return fail(SDR_EINVAL, "n=%lld outside [0, %d]", (long long)n, SDR_DFT_MAX_N);
+  if (n > 0 && (x == nullptr || X == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
+  if (n == 0) return SDR_OK;
+  TRY(set_dev(c));
+  double *dx, *dX;
+  TRY(scratch(c, S_IN, sizeof(double) * (size_t)n, (void**)&dx));
+  TRY(scratch(c, S_OUT, sizeof(double) * 2 * (size_t)n, (void**)&dX));
+  TRY(h2d(c, dx, x, sizeof(double) * (size_t)n));
+  HIP_TRY(sdr_launch_dft(dx, n, dX, c->stream));
+  TRY(d2h(c, X, dX, sizeof(double) * 2 * (size_t)n));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SDR_OK;
 }

@@ -8,6 +8,8 @@ per block.  Same names, argument meaning, return shapes and error behaviour:
     fmPll(pllIn, freq, Fs, recovery_state, ncoScale=1.0, phaseAdjust=0.0,
           normBandwidth=0.01)                  model/fmPll.py:4-46
     my_convoloution(x, h, N_taps, my_zi)       model/fmSupportLib.py:157-176
+    estimatePSD(samples, NFFT, Fs)             model/fmSupportLib.py:66-140 (Bartlett PSD)
+    DFT(x)                                     model/fmSupportLib.py:46-60
 
 plus the fused forms the hot path is built from:
 
@@ -294,3 +296,26 @@ def fm_mono_streams(iq, rf_coeff, audio_coeff, rf_decim=10, audio_decim=5, ctx=N
         d_iq.free()
         d_au.free()
     return out[0] if one else out
+
+
+def estimatePSD(samples, NFFT, Fs, ctx=None):
+    """(freq, psd_est) of model/fmSupportLib.py:66-140: Bartlett estimate over
+    floor(len/NFFT) non-overlapping Hann-windowed segments, per-segment dB averaged.
+    The segments' FFTs and dB values run in f64 on the GPU (sdr_psd); NFFT must be a power
+    of two <= 4096.  A zero-power bin raises ValueError like the reference's math.log10."""
+    x = _check_x(samples).astype(np.float64)
+    nfft = int(NFFT)
+    freq = np.arange(0, Fs / 2, Fs / nfft)
+    psd = np.empty(nfft // 2, dtype=np.float64)
+    c = _ctx(ctx)
+    check(c.lib.sdr_psd(c.handle, f64p(c_f64(x)), x.shape[0], nfft, float(Fs), f64p(psd)), "sdr_psd")
+    return freq, psd
+
+
+def DFT(x, ctx=None):
+    """Xf of model/fmSupportLib.py:46-60 (direct O(N^2) DFT, complex128), on the GPU."""
+    x = c_f64(_check_x(x).astype(np.float64))
+    out = np.empty(2 * x.shape[0], dtype=np.float64)
+    c = _ctx(ctx)
+    check(c.lib.sdr_dft(c.handle, f64p(x), x.shape[0], f64p(out)), "sdr_dft")
+    return out.view(np.complex128)
