@@ -49,6 +49,7 @@ enum { SDR_IQ_F32 = 0, SDR_IQ_U8 = 1 };                  /* interleaved IQ sampl
 enum { SDR_PRE_NONE = 0, SDR_PRE_SQUARE = 1, SDR_PRE_MIX = 2 }; /* FIR input pre-ops */
 enum { SDR_REAL_F32 = 0, SDR_REAL_F64 = 1 };              /* real sample types (PSD) */
 #define SDR_DFT_MAX_N (1 << 16)
+#define SDR_MAX_RESAMPLE_TAPS 4096                           /* sdr_resample* filter length */
 
 typedef struct sdr_ctx sdr_ctx;
 
@@ -109,7 +110,10 @@ int sdr_lfilter(sdr_ctx* ctx, const float* x, const float* mix, float gain, int 
 /* Rational resampler: lfilter(b, 1.0, zero-stuff(x, up), zi)[::down] * up, without
  * materialising the zero-stuffed stream; zi lives on the upsampled stream.
  * Replaces model/fmRDSblock.py:184-199 and src/filter.cpp:301-339
- * (convolveWithDecimMode1RDS).  y: ceil(n*up/down) floats. */
+ * (convolveWithDecimMode1RDS), and the mode-1 audio resampler src/filter.cpp:222-298
+ * (convolveWithDecimMode1[Pointer], 24/125 at 6 MHz, src/fm_radio.cpp:174-180, :228) whose
+ * output is y/up (the reference applies the up gain at the int16 conversion, :297).
+ * taps <= SDR_MAX_RESAMPLE_TAPS.  y: ceil(n*up/down) floats. */
 int sdr_resample(sdr_ctx* ctx, const float* x, int64_t n, const double* b, int taps, int up,
                  int down, double* zi_inout, float* y);
 

@@ -38,3 +38,20 @@ extern "C" void ref_fe_streams(const float* iq, int64_t n_complex, int64_t strid
     ref_fe_stream(iq + 2 * (int64_t)s * stride, n_complex, block, taps, T, D,
                   demod_out + (int64_t)s * out_stride);
 }
+
+// Mode-1 audio resampler of the reference, src/filter.cpp:222-259 (convolveWithDecimMode1),
+// run block by block as src/fm_radio.cpp:228 runs it: the output vector zeroed between
+// blocks (:305) and the reference's own raw-history zi carried (T-1 floats, zero at
+// start).  y_out: nblocks x floor(block*up/decim) floats.  Used to pin sdr_resample's
+// 24/125 path (tests/golden/make_mode1_golden.py).
+extern "C" void ref_mode1_resample_blocks(const float* x, int64_t nblocks, int64_t block,
+                                          const float* taps, int T, int decim, int up, float* y_out) {
+  std::vector<float> h(taps, taps + T), zi(T - 1, 0.f), xb(block), y;
+  const int64_t ny = block * up / decim;
+  for (int64_t b = 0; b < nblocks; ++b) {
+    std::copy(x + b * block, x + (b + 1) * block, xb.begin());
+    std::fill(y.begin(), y.end(), 0.f);
+    convolveWithDecimMode1(y, xb, h, zi, decim, up);
+    std::copy(y.begin(), y.begin() + ny, y_out + b * ny);
+  }
+}

@@ -140,9 +140,11 @@ int scratch(sdr_ctx* c, Slot s, size_t bytes, void** out) {
   return SDR_OK;
 }
 
-int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out) {
+// max_T: SDR_MAX_TAPS for the FIR kernels (taps also passed by value, TapsF32), up to
+// SDR_MAX_RESAMPLE_TAPS for the resampler (device arrays only; h holds the first 256).
+int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T = SDR_MAX_TAPS) {
   if (b == nullptr) return fail(SDR_EINVAL, "taps pointer is NULL");
-  if (T < 1 || T > SDR_MAX_TAPS) return fail(SDR_EINVAL, "taps=%d outside [1, %d]", T, SDR_MAX_TAPS);
+  if (T < 1 || T > max_T) return fail(SDR_EINVAL, "taps=%d outside [1, %d]", T, max_T);
   for (const TapSet& t : c->taps)
     if ((int)t.b.size() == T && std::memcmp(t.b.data(), b, sizeof(double) * T) == 0) {
       *out = &t;
@@ -156,10 +158,13 @@ int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out) {
   TapSet t;
   t.b.assign(b, b + T);
   std::memset(&t.h, 0, sizeof t.h);
-  for (int k = 0; k < T; ++k) t.h.h[k] = (float)b[k];
-  HIP_TRY(hipMalloc(&t.dev_f32, sizeof(float) * SDR_MAX_TAPS));
-  HIP_TRY(hipMalloc(&t.dev_f64, sizeof(double) * SDR_MAX_TAPS));
-  HIP_TRY(hipMemcpy(t.dev_f32, t.h.h, sizeof(float) * T, hipMemcpyHostToDevice));
+  std::vector<float> f(T);
+  for (int k = 0; k < T; ++k) f[k] = (float)b[k];
+  for (int k = 0; k < std::min(T, SDR_MAX_TAPS); ++k) t.h.h[k] = f[k];
+  const int cap = std::max(T, SDR_MAX_TAPS);
+  HIP_TRY(hipMalloc(&t.dev_f32, sizeof(float) * cap));
+  HIP_TRY(hipMalloc(&t.dev_f64, sizeof(double) * cap));
+  HIP_TRY(hipMemcpy(t.dev_f32, f.data(), sizeof(float) * T, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(t.dev_f64, b, sizeof(double) * T, hipMemcpyHostToDevice));
   c->taps.push_back(std::move(t));
   *out = &c->taps.back();
@@ -466,7 +471,7 @@ int sdr_resample_dev(sdr_ctx* c, const float* x, int64_t n, const double* b, int
   if (n > 0 && (x == nullptr || y == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
   TRY(set_dev(c));
   const TapSet* ts;
-  TRY(get_taps(c, b, taps, &ts));
+  TRY(get_taps(c, b, taps, &ts, SDR_MAX_RESAMPLE_TAPS));
   double* zfo = zf;
   const bool alias = zf && zf == zi;
   if (alias) TRY(scratch(c, S_STATE2, sizeof(double) * (size_t)taps, (void**)&zfo));
@@ -619,7 +624,8 @@ int sdr_resample(sdr_ctx* c, const float* x, int64_t n, const double* b, int tap
                  double* zi_inout, float* y) {
   CHECK_CTX(c);
   if (n < 0 || up < 1 || down < 1) return fail(SDR_EINVAL, "bad resampler sizes");
-  if (taps < 1 || taps > SDR_MAX_TAPS) return fail(SDR_EINVAL, "taps=%d outside [1, %d]", taps, SDR_MAX_TAPS);
+  if (taps < 1 || taps > SDR_MAX_RESAMPLE_TAPS)
+    return fail(SDR_EINVAL, "taps=%d outside [1, %d]", taps, SDR_MAX_RESAMPLE_TAPS);
   if (n > 0 && (x == nullptr || y == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
   TRY(set_dev(c));
   const int64_t M = ceil_div(n * up, down);

@@ -164,10 +164,13 @@ __global__ __launch_bounds__(256) void fir_generic_kernel(FirParams p, const flo
 // zero-stuffed stream: u[j] = x[j/U] if j % U == 0 else 0,
 //   r[m] = U * ( sum_k h[k] u[D m - k]  +  (D m < T-1 ? zi[D m] : 0) ),
 // only taps with (D m - k) % U == 0 contribute (~T/U per output).
+// Taps (T <= SDR_MAX_RESAMPLE_TAPS) staged in dynamic LDS.  Output m reads the zero-stuffed
+// stream at j0 = D*m: the nonzero terms are k = j0 mod U, +U, ... with input index
+// (j0 - k)/U walking down by one, so one division per output, none per term.
 __global__ __launch_bounds__(256) void resample_kernel(const float* x, int64_t n, const float* taps,
                                                        int T, int U, int D, const double* zi,
                                                        float* y) {
-  __shared__ float h[SDR_MAX_TAPS];
+  extern __shared__ float h[];
   for (int k = threadIdx.x; k < T; k += blockDim.x) h[k] = taps[k];
   __syncthreads();
   const int64_t nu = n * U;
@@ -175,12 +178,11 @@ __global__ __launch_bounds__(256) void resample_kernel(const float* x, int64_t n
   const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
   const int64_t j0 = D * m;
+  const int k0 = (int)(j0 % U);
+  const int khi = (int)min<int64_t>(T - 1, j0);      // terms with j0 - k >= 0
+  int64_t xi = (j0 - k0) / U;
   float acc = 0.f;
-  for (int k = (int)(j0 % U); k < T; k += U) {
-    const int64_t j = j0 - k;
-    if (j < 0) break;
-    acc = fmaf(h[k], x[j / U], acc);
-  }
+  for (int k = k0; k <= khi; k += U, --xi) acc = fmaf(h[k], x[xi], acc);
   if (zi != nullptr && j0 < T - 1) acc += (float)zi[j0];
   y[m] = acc * (float)U;
 }
@@ -188,15 +190,14 @@ __global__ __launch_bounds__(256) void resample_kernel(const float* x, int64_t n
 // lfilter final state (f64) for a real stream after an optional pre-op and an
 // optional zero-stuffing factor U (U = 1: plain stream):
 //   zf[k] = sum_{j=k+1}^{T-1} b[j] u[NU+k-j] + (NU+k < T-1 ? zi[NU+k] : 0),  NU = n*U.
-// One 256-thread block per stream (T <= SDR_MAX_TAPS = 256): the <= T-1 newest inputs
-// (pre-op applied) and the taps are staged in LDS first, so the per-output f64 dot
+// Blocks of 256 outputs per stream (T <= SDR_MAX_RESAMPLE_TAPS): the <= T-1 newest inputs
+// (pre-op applied) and the taps are staged in dynamic LDS first, so each output's f64 dot
 // product runs from LDS instead of waiting a global-memory round trip per term.
 __global__ __launch_bounds__(256) void zf_kernel(const float* x, const float* c, float gain, int pre,
                                                  int64_t n, int64_t x_stride, int U, const double* b,
                                                  int T, const double* zi, int64_t zi_stride, double* zf) {
-  __shared__ double us[SDR_MAX_TAPS];
-  __shared__ double bs[SDR_MAX_TAPS];
-  const int k = threadIdx.x;
+  extern __shared__ double zsh[];
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
   const int s = blockIdx.y;
   x += (int64_t)s * x_stride;
   if (c != nullptr) c += (int64_t)s * x_stride;
@@ -205,14 +206,16 @@ __global__ __launch_bounds__(256) void zf_kernel(const float* x, const float* c,
   const int64_t nu = n * U;
   // inputs used: x[n-L .. n-1], L = min(n, floor((T-1)/U)); us[i] = u(x[n-1-i])
   const int L = (int)min<int64_t>(n, (T - 1) / U);
-  if (k < L) {
-    const int64_t xi = n - 1 - k;
+  double* bs = zsh;
+  double* us = zsh + T;
+  for (int i = threadIdx.x; i < L; i += blockDim.x) {
+    const int64_t xi = n - 1 - i;
     double v = (double)x[xi];
     if (pre == PRE_SQUARE) v = v * v;
     else if (pre == PRE_MIX) v = (double)((x[xi] * c[xi]) * gain);
-    us[k] = v;
+    us[i] = v;
   }
-  if (k < T) bs[k] = b[k];
+  for (int i = threadIdx.x; i < T; i += blockDim.x) bs[i] = b[i];
   __syncthreads();
   if (k >= T - 1) return;
   // The terms with idx = nu + k - j >= 0 on the zero-stuffed grid (idx % U == 0): since
@@ -303,7 +306,8 @@ hipError_t sdr_launch_resample(const float* x, int64_t n, const float* taps_dev,
                                const double* zi, float* y, hipStream_t st) {
   const int64_t M = (n * U + D - 1) / D;
   if (M <= 0) return hipSuccess;
-  hipLaunchKernelGGL(resample_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, x, n,
+  if (T > SDR_MAX_RESAMPLE_TAPS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(resample_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), sizeof(float) * T, st, x, n,
                      taps_dev, T, U, D, zi, y);
   return hipGetLastError();
 }
@@ -312,8 +316,9 @@ hipError_t sdr_launch_zf(const float* x, const float* c, float gain, int pre, in
                          int64_t x_stride, int nstreams, int U, const double* b_dev, int T,
                          const double* zi, int64_t zi_stride, double* zf, hipStream_t st) {
   if (T <= 1 || nstreams <= 0) return hipSuccess;
-  if (T > SDR_MAX_TAPS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(zf_kernel, dim3(1, nstreams), dim3(256), 0, st, x, c, gain,
+  if (T > SDR_MAX_RESAMPLE_TAPS) return hipErrorInvalidValue;
+  const int64_t L = std::min<int64_t>(n, (T - 1) / U);
+  hipLaunchKernelGGL(zf_kernel, dim3((T - 1 + 255) / 256, nstreams), dim3(256), sizeof(double) * (T + L), st, x, c, gain,
                      pre, n, x_stride, U, b_dev, T, zi, zi_stride, zf);
   return hipGetLastError();
 }

@@ -16,7 +16,15 @@
 // All filter / demod / PLL state stays in device memory between blocks.
 //
 // Options: --mono (mono only, both channels = mono), --rf-taps N (default 151, the
-// reference's), --blocks N (stop after N blocks).
+// reference's), --blocks N (stop after N blocks), --mode 1 (2.5 MS/s IQ,
+// src/fm_radio.cpp:36; the 250 kS/s IF goes to 48 kHz through the 24/125 resampler with a
+// 6 MHz, 16 kHz filter, :174-180, :228, whose up-gain the reference applies at the int16
+// write, :229, :297; mono only: the reference designs its mode-1 pilot/stereo band-passes
+// at 6 MHz for 250 kS/s data and runs its PLL at 240 kHz, :201-202, :233, so they have no
+// working form to reproduce).  Mode-1 taps: firwin(3623, 16 kHz at 6 MHz); the reference's
+// 151*24 = 3624-tap sinc design divides 0/0 at its tap 1812 (src/filter.cpp:29-33) and
+// writes NaN audio, i.e. silence (:290-293).  Per block it writes floor(15360*24/125) =
+// 2 949 samples, as the reference does (src/filter.cpp:264).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -81,31 +89,41 @@ struct Dev {
 
 int main(int argc, char** argv) {
   bool mono = false, print_taps = false;
-  int rf_taps = 151;
+  int rf_taps = 151, mode = 0;
   long long max_blocks = -1;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--mono")) mono = true;
     else if (!std::strcmp(argv[i], "--print-taps")) print_taps = true;
     else if (!std::strcmp(argv[i], "--rf-taps") && i + 1 < argc) rf_taps = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--blocks") && i + 1 < argc) max_blocks = std::atoll(argv[++i]);
+    else if (!std::strcmp(argv[i], "--mode") && i + 1 < argc) mode = std::atoi(argv[++i]);
     else {
-      std::fprintf(stderr, "usage: fm_radio_gpu [--mono] [--rf-taps N] [--blocks N] [--print-taps] "
-                           "< iq_u8 > pcm_s16le_stereo\n");
+      std::fprintf(stderr, "usage: fm_radio_gpu [--mode 0|1] [--mono] [--rf-taps N] [--blocks N] "
+                           "[--print-taps] < iq_u8 > pcm_s16le_stereo\n");
       return 2;
     }
   }
+  if (mode != 0 && mode != 1) {
+    std::fprintf(stderr, "fm_radio_gpu: --mode %d: modes 0 (2.4 MS/s) and 1 (2.5 MS/s)\n", mode);
+    return 2;
+  }
+  if (mode == 1) mono = true;
   if (rf_taps < 3 || rf_taps > SDR_MAX_TAPS_ABI) {
     std::fprintf(stderr, "fm_radio_gpu: --rf-taps %d out of range\n", rf_taps);
     return 2;
   }
-  // taps (model/fmMonoBlock.py:22-45, :115, :150, :159)
-  const std::vector<double> rf_b = firwin(rf_taps, 0.0, 100e3 / 1.2e6);
+  // taps (model/fmMonoBlock.py:22-45, :115, :150, :159); mode 1: RF at 2.5 MS/s and the
+  // 24/125 resampler filter at 6 MHz
+  const double rf_fs = mode == 1 ? 2.5e6 : 2.4e6;
+  constexpr int kUp = 24, kDown = 125, kM1Taps = 151 * kUp - 1;
+  const std::vector<double> rf_b = firwin(rf_taps, 0.0, 100e3 / (rf_fs / 2));
+  const std::vector<double> m1_b = firwin(kM1Taps, 0.0, 16e3 / 3e6);
   const std::vector<double> au_b = firwin(151, 0.0, 16e3 / 120e3);
   const std::vector<double> pil_b = firwin(151, 18.5e3 / 120e3, 19.5e3 / 120e3);
   const std::vector<double> ext_b = firwin(151, 22e3 / 120e3, 54e3 / 120e3);
   const std::vector<double> ste_b = firwin(151, 0.0, 16e3 / 120e3);
   if (print_taps) {                    // (no GPU) one line per filter, for the design test
-    for (const auto* t : {&rf_b, &au_b, &pil_b, &ext_b, &ste_b}) {
+    for (const auto* t : {&rf_b, &au_b, &pil_b, &ext_b, &ste_b, &m1_b}) {
       for (size_t k = 0; k < t->size(); ++k) std::printf(k ? " %.17g" : "%.17g", (*t)[k]);
       std::printf("\n");
     }
@@ -116,14 +134,16 @@ int main(int argc, char** argv) {
   ck(sdr_create(dev_env ? std::atoi(dev_env) : 0, &c), "sdr_create");
   hipStream_t st = static_cast<hipStream_t>(sdr_stream(c));
   Dev d{c};
-  const int64_t M = kBlock / 10, A = M / 5, Z = rf_taps - 1;
+  const int64_t M = kBlock / 10, Z = rf_taps - 1;
+  const int64_t A = mode == 1 ? M * kUp / kDown : M / 5;     // audio samples written per block
+  const int64_t AY = mode == 1 ? (M * kUp + kDown - 1) / kDown : A;   // resampler outputs
 
   // device state and intermediates (persist across blocks)
   auto* d_iq = static_cast<uint8_t*>(d.alloc(2 * kBlock));
   auto* rf_st = static_cast<double*>(d.alloc(8 * (2 * Z + 1)));    // zi_i | zi_q | phase
   auto* d_dm = static_cast<float*>(d.alloc(4 * M + 16));
-  auto* d_au = static_cast<float*>(d.alloc(4 * A + 16));
-  auto* zi_au = static_cast<double*>(d.alloc(8 * 150));
+  auto* d_au = static_cast<float*>(d.alloc(4 * AY + 16));
+  auto* zi_au = static_cast<double*>(d.alloc(8 * (mode == 1 ? kM1Taps - 1 : 150)));
   auto* zi_pil = static_cast<double*>(d.alloc(8 * 150));
   auto* zi_ext = static_cast<double*>(d.alloc(8 * 150));
   auto* zi_ste = static_cast<double*>(d.alloc(8 * 150));
@@ -176,8 +196,11 @@ int main(int argc, char** argv) {
     ck(sdr_rf_frontend_dev(c, d_iq, SDR_IQ_U8, kBlock, kBlock, 0, 1, rf_b.data(), rf_taps, 10, rf_st,
                            rf_st + Z, Z, rf_st, rf_st + Z, rf_st + 2 * Z, d_dm, M, nullptr, nullptr),
        "front end");                                                  // :86-98
-    ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, au_b.data(), 151, 5, zi_au, 150, zi_au,
-                   d_au, A), "mono");                                 // :101-109
+    if (mode == 1)                                                    // src/fm_radio.cpp:228
+      ck(sdr_resample_dev(c, d_dm, M, m1_b.data(), kM1Taps, kUp, kDown, zi_au, zi_au, d_au), "mode-1 resampler");
+    else
+      ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, au_b.data(), 151, 5, zi_au, 150, zi_au,
+                     d_au, A), "mono");                               // :101-109
     const float* out_l = d_au;
     const float* out_r = d_au;
     if (!mono) {

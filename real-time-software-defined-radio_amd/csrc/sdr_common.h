@@ -14,6 +14,7 @@
 #include <type_traits>
 
 #define SDR_MAX_TAPS 256
+#define SDR_MAX_RESAMPLE_TAPS 4096   // resampler (sdr_resample*) filters: taps + zf staging fit 64 KiB of LDS
 #define SDR_PSD_MAX_NFFT 4096   // PSD segment length limit: N complex f64 in 64 KiB of LDS
 
 // Taps passed by value through the kernarg segment: with compile-time tap indices

@@ -35,7 +35,7 @@ def _ctx(ctx=None):
     return ctx if ctx is not None else _lib.get_context()
 
 
-def _taps(b, a=1.0):
+def _taps(b, a=1.0, max_taps=256):
     b = np.atleast_1d(np.asarray(b))
     a = np.atleast_1d(np.asarray(a))
     if b.ndim != 1 or a.ndim != 1:
@@ -45,8 +45,8 @@ def _taps(b, a=1.0):
     if np.iscomplexobj(b) or np.iscomplexobj(a):
         raise NotImplementedError(f"input type '{np.result_type(b, a)}' not supported")
     b = np.array(b, dtype=np.float64) / float(a[0])
-    if not 1 <= len(b) <= 256:
-        raise ValueError(f"{len(b)} taps: the GPU path supports 1..256 taps")
+    if not 1 <= len(b) <= max_taps:
+        raise ValueError(f"{len(b)} taps: this GPU path supports 1..{max_taps} taps")
     return np.ascontiguousarray(b)
 
 
@@ -179,8 +179,9 @@ def my_convoloution(x, h, N_taps, my_zi=None, ctx=None):
 
 
 def resample(x, b, zi=None, up: int = 19, down: int = 80, ctx=None):
-    """lfilter(b, 1, zero_stuff(x, up), zi)[::down] * up (model/fmRDSblock.py:184-199)."""
-    b = _taps(b)
+    """lfilter(b, 1, zero_stuff(x, up), zi)[::down] * up (model/fmRDSblock.py:184-199; the
+    mode-1 24/125 audio resampler, src/filter.cpp:222-298, is y / up).  Up to 4096 taps."""
+    b = _taps(b, max_taps=4096)
     x = c_f32(_check_x(x))
     zi = _check_zi(zi, len(b))
     c = _ctx(ctx)

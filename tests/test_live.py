@@ -28,12 +28,16 @@ def test_taps_match_firwin(sdr):
     rows = [np.array([float(v) for v in line.split()]) for line in res.stdout.splitlines()]
     rf, au = sdr.design.mono_coeffs(151, 151)
     pil, ext, ste = sdr.design.stereo_coeffs(151)
-    for got, ref in zip(rows, (rf, au, pil, ext, ste)):
+    from scipy import signal
+    m1 = signal.firwin(3623, 16e3 / 3e6, window="hann")          # mode-1 resampler filter
+    assert len(rows) == 6
+    for got, ref in zip(rows, (rf, au, pil, ext, ste, m1)):
         assert got.shape == ref.shape and np.max(np.abs(got - ref)) < 1e-15
 
 
 def test_usage_error_exit_code():
     assert subprocess.run([BIN, "--bogus"], capture_output=True).returncode == 2
+    assert subprocess.run([BIN, "--mode", "2"], capture_output=True).returncode == 2
 
 
 @pytest.mark.gpu
@@ -68,3 +72,41 @@ def test_live_pipeline_mono(sdr, gpu_ctx):
     a = np.concatenate([proc.process(iq[2 * k * B:2 * (k + 1) * B]) for k in range(nb)])
     ref = to_pcm(a, a)
     assert pcm.shape == ref.shape and np.max(np.abs(pcm.astype(np.int32) - ref)) <= 1
+
+
+@pytest.mark.gpu
+def test_live_pipeline_mode1(sdr, gpu_ctx, oracle):
+    """--mode 1: 2.5 MS/s u8 IQ -> FE (151 taps at 2.5 MHz, decim 10) ->
+    24/125 resampler (3 623 taps at 6 MHz) -> 2 949 mono samples per block on both channels.
+    Against the same chain through the Python API (<= 1 LSB) and the oracle (<= 1 LSB on
+    > 99 % of the samples)."""
+    from scipy import signal
+    nb = 3
+    iq = sdr.synth.fm_iq(nb * B, seed=14, fs=2.5e6, dtype=np.uint8)
+    res = subprocess.run([BIN, "--mode", "1"], input=iq.tobytes(), capture_output=True, check=True, timeout=120)
+    pcm = np.frombuffer(res.stdout, dtype=np.int16)
+    A = (B // 10) * 24 // 125
+    assert pcm.shape == (nb * 2 * A,)
+    rf = signal.firwin(151, 100e3 / 1.25e6, window="hann")
+    h = signal.firwin(3623, 16e3 / 3e6, window="hann")
+    zi_i = zi_q = None
+    ph, zr = 0.0, np.zeros(len(h) - 1)
+    api = []
+    for k in range(nb):
+        d, zi_i, zi_q, ph = sdr.rf_frontend_block(iq[2 * k * B:2 * (k + 1) * B], rf, zi_i, zi_q, ph)
+        y, zr = sdr.resample(d, h, zr, 24, 125)
+        api.append(y[:A])
+    a = np.concatenate(api)
+    assert np.max(np.abs(pcm.astype(np.int32) - to_pcm(a, a))) <= 1
+    x = (iq.astype(np.float64) - 128.0) / 128.0
+    i_f = oracle.lfilter_fir(rf, x[0::2])[::10]
+    q_f = oracle.lfilter_fir(rf, x[1::2])[::10]
+    dm, _ = oracle.fm_demod_arctan(i_f, q_f, 0.0)
+    zo, ora = np.zeros(len(h) - 1), []
+    M = B // 10
+    for k in range(nb):
+        y, zo = oracle.resample(dm[k * M:(k + 1) * M], h, zo, 24, 125)
+        ora.append(y[:A])
+    o = np.concatenate(ora)
+    dd = np.abs(pcm.astype(np.int32) - to_pcm(o, o))
+    assert dd.max() <= 1 and np.mean(dd > 0) < 0.01
