@@ -60,8 +60,9 @@ hipError_t sdr_launch_zf(const float* x, const float* c, float gain, int pre, in
                          const double* zi, int64_t zi_stride, double* zf, hipStream_t st);
 hipError_t sdr_launch_combine(const float* mono, const float* side, int64_t n, float* left,
                               float* right, hipStream_t st);
+int sdr_psd_chunks(int64_t nseg);
 hipError_t sdr_launch_psd(const void* x, int f64, int64_t n, int logn, double fs, double* seg_db,
-                          double* out, int* zero_flag, hipStream_t st);
+                          double* part, double* out, int* zero_flag, hipStream_t st);
 hipError_t sdr_launch_dft(const double* x, int64_t n, double* X, hipStream_t st);
 hipError_t sdr_launch_pll(const float* in, int64_t n, int64_t in_stride, int nstreams,
                           const PllCfg& cfg, double* state_dev, double* theta, int64_t th_stride,
@@ -702,13 +703,16 @@ int sdr_psd_dev(sdr_ctx* c, const void* x, int dtype, int64_t n, int nfft, doubl
   TRY(set_dev(c));
   const int64_t nseg = n / nfft;
   const int half = nfft / 2;
+  const int64_t nch = sdr_psd_chunks(nseg);
   void* ws;
-  TRY(scratch(c, S_PSD, sizeof(double) * (size_t)(nseg * half) + 64, &ws));
-  int* flag = reinterpret_cast<int*>(static_cast<char*>(ws) + sizeof(double) * (size_t)(nseg * half));
+  TRY(scratch(c, S_PSD, sizeof(double) * (size_t)((nseg + nch) * half) + 64, &ws));
+  double* seg_db = static_cast<double*>(ws);
+  double* part = seg_db + nseg * half;
+  int* flag = reinterpret_cast<int*>(part + nch * half);
   HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), c->stream));
   int logn = 0;
   while ((1 << logn) < nfft) ++logn;
-  HIP_TRY(sdr_launch_psd(x, dtype == SDR_REAL_F64, n, logn, fs, static_cast<double*>(ws), psd, flag, c->stream));
+  HIP_TRY(sdr_launch_psd(x, dtype == SDR_REAL_F64, n, logn, fs, seg_db, part, psd, flag, c->stream));
   int zero = 0;
   HIP_TRY(hipMemcpyAsync(&zero, flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
