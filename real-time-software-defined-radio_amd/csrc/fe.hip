@@ -716,6 +716,11 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   constexpr int FPF = ((MODE >> 20) & 7) ? ((MODE >> 20) & 7) : 2;
   constexpr int APFX = ((MODE >> 24) & 7) ? ((MODE >> 24) & 7) : 2;
   constexpr bool SAFE = !(MODE & 0x8000);
+  // A/B (tuning): 0x20000000 touches tile t+PFD's new lines (one dword per 128-B line, LDS-DMA
+  // into a 256-B scratch, no VGPR destination) after the FIR of tile t, so its later DMA
+  // finds them in L2 / MALL; PFD = 2, or 3 with 0x40000000
+  constexpr bool PFL2 = MODE & 0x20000000;
+  constexpr int PFD = (MODE & 0x40000000) ? 3 : 2;
   constexpr int SPR = SV == 0 ? RING_SPREAD : (SV == 1 ? 0 : 1);
   constexpr int ST0 = SV == 0 ? RING_SPREAD_T0 : (SV == 3 ? 4 : 2);
   constexpr int SDT = SV == 0 ? RING_SPREAD_DT : (SV == 2 ? 4 : (SV == 3 ? 14 : 8));
@@ -742,6 +747,7 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   __shared__ __attribute__((aligned(16))) f2v ring[2][LS];
   __shared__ __attribute__((aligned(16))) float dh[FUSED ? HA + BD + 4 : 1];
   __shared__ __attribute__((aligned(16))) f4v ptab[FUSED ? NW + 1 : 1];
+  __shared__ __attribute__((aligned(16))) float pfs[PFL2 ? 64 : 1];
 
   const int lane = threadIdx.x;
   // FUSED: balanced tile ranges [g0, g1) over a.total tiles; FE: runs of per_wave tiles
@@ -1109,6 +1115,16 @@ void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
               fe_fir_tile<T, D, R, FM, (T > 127 ? 8 : PFR), SAFE>(buf, lane, tp, ai, aq, spread);
             }
             gn += D * TO * 8;
+            if constexpr (PFL2) {
+              if (i + PFD <= j_int) {        // tile i+PFD's image lies inside the stream
+                // gn now points at tile i+2's new chunks (15 KiB = 120 lines: lanes 0..59)
+                const char* gp = gn + (PFD - 2) * (D * TO * 8);
+                asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1 offset:0\n\t"
+                             "global_load_lds_dword %0, %1 offset:128"
+                             :: "v"(lane < 60 ? 256u * lane : 0u), "s"(gp), "s"(lds_addr_of(pfs)) : "memory", "m0");
+                issued += 2;
+              }
+            }
             lds_wait<0>(h0);
             lds_write_b128(&ring[b ^ 1][0] + 2 * lane, h0);
             if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(&ring[b ^ 1][0] + 128 + 2 * lane, h1); }

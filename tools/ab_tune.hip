@@ -91,11 +91,9 @@ int main(int argc, char** argv) {
 #define SEV(NAME, PF, VST, WPC) v.push_back({NAME, eb, [&](hipStream_t s) { slot_launch<false, PF, VST>(p, taps, nullptr, nullptr, s, WPC); }, {}})
   FV("fused ring", 0x00);
   FV("fused ring DMA only", 0x05);
-  FV("fused ring nospread", 0x10);
-  FV("fused ring spread dt4", 0x20);
-  FV("fused ring noepi noaud nolds", 0x700);
-  FV("fused ring noepi noaud nolds nospread", 0x710);
-  FV("fused ring noepi noaud nolds dt4", 0x720);
+  FV("fused ring pfl2 d2", 0x20000000);
+  FV("fused ring pfl2 d3", 0x60000000);
+  FV("fused ring pfl2 d2 nospread", 0x20000010);
   SFV("fused slot pf4 v w8", 4, true, 8);
   v.push_back({"fused slotdma pf8 w8", fb, [&](hipStream_t s) { slot_launch<true, 8, true, 0, 1>(p, taps, tdev, aud, s, 8); }, {}});
   v.push_back({"fused slotdma pf12 w8", fb, [&](hipStream_t s) { slot_launch<true, 12, true, 0, 1>(p, taps, tdev, aud, s, 8); }, {}});
