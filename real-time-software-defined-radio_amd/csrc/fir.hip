@@ -15,7 +15,7 @@
 // D(R-1)+T input window in LDS (one ds_read_b32 feeds up to R FMAs; taps are
 // compile-time indices -> SGPR operands).  LDS rows are padded by one float every
 // D*R samples so the per-lane stride D*R+1 is odd -> conflict-free ds_read_b32.
-#include "sdr_common.h"
+#include "sdr_launch.h"
 
 enum { PRE_NONE = 0, PRE_SQUARE = 1, PRE_MIX = 2 };
 
@@ -231,11 +231,6 @@ __global__ __launch_bounds__(256) void zf_kernel(const float* x, const float* c,
 }
 
 // ------------------------------------------------------------------------------
-struct FirLaunch {
-  const float* x; const float* c; float gain; int pre; int64_t n; int64_t x_stride; int64_t x_step;
-  int64_t hist; int nstreams; const float* taps_dev; const TapsF32* taps; int T; int D;
-  const double* zi; int64_t zi_stride; float* y; int64_t y_stride;
-};
 
 template <int T, int D, int PRE>
 static hipError_t launch_fir_t(const FirLaunch& a, hipStream_t st) {

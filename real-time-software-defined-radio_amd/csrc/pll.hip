@@ -19,11 +19,8 @@
 //   2. nco_kernel: fully parallel ncoOut[k+1] = cos(th_k*scale + adj),
 //      ncoOutQ[k+1] = sin(th_k*scale + adj) (fmPll.py:36-37).
 // All phase arithmetic is f64 (SURVEY §7 hard part 5: an fp32 NCO drifts).
-#include "sdr_common.h"
+#include "sdr_launch.h"
 
-struct PllCfg {
-  double freq, fs, scale, adj, kp, ki;
-};
 
 namespace {
 

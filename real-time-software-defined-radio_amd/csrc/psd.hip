@@ -15,7 +15,7 @@
 // The PSD reads each sample once and the work is tiny (a diagnostic, off the hot path).
 #include <hip/hip_runtime.h>
 #include <cstdint>
-#include "sdr_common.h"
+#include "sdr_launch.h"
 
 namespace {
 

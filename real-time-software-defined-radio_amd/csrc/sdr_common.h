@@ -240,6 +240,43 @@ __device__ __forceinline__ float fast_atan2f(float y, float x) {
   return (x != x || y != y) ? __builtin_nanf("") : r;
 }
 
+// Deferred per-lane output queue: Q entries of 3 floats held in registers, written to HBM
+// in one burst at the end of a wave's run.  Output stores interleaved with a streaming
+// read lower the read rate far more than their bytes (tools/pipe_probe.hip, r02: one 768-B
+// store per 15-KiB tile 80 -> 96 us, one per 5 tiles -> 86 us, the same bytes written at the
+// end of each run -> 84 us), so the streaming kernels keep their outputs here until the
+// run ends.  Entries are written with a wave-uniform index through a compile-time binary
+// search (scalar branches, static register names: no scratch, no movrel).
+template <int Q>
+struct OutQ3 {
+  float v[Q][3];
+  template <int LO, int HI>
+  __device__ __forceinline__ void put_bs(int k, float a, float b, float c) {
+    if constexpr (LO == HI) {
+      v[LO][0] = a; v[LO][1] = b; v[LO][2] = c;
+      // a distinct marker ends each leaf: the leaves' stores cannot be merged into one
+      // store at a computed index (which would move the queue to scratch memory)
+      asm volatile("; oq leaf %0" :: "n"(LO));
+    } else {
+      constexpr int MID = (LO + HI + 1) / 2;
+      if (k >= MID) put_bs<MID, HI>(k, a, b, c);
+      else put_bs<LO, MID - 1>(k, a, b, c);
+    }
+  }
+  __device__ __forceinline__ void put(int k, float a, float b, float c) {
+    put_bs<0, Q - 1>(__builtin_amdgcn_readfirstlane(k), a, b, c);
+  }
+  // entries [0, cnt) -> p + step * j (one 12-B store per lane each); returns cnt
+  __device__ __forceinline__ int flush(float* p, int64_t step, int cnt) {
+    typedef float f3v __attribute__((ext_vector_type(3)));
+    static_for<0, Q>([&](auto J) {
+      constexpr int j = J;
+      if (j < cnt) *reinterpret_cast<f3v*>(p + step * j) = f3v{v[j][0], v[j][1], v[j][2]};
+    });
+    return cnt;
+  }
+};
+
 // Wave-wide sum over 64 lanes (CDNA wave64: six xor steps).
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

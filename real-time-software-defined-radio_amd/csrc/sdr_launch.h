@@ -1,0 +1,56 @@
+// Internal launcher interface between the C-ABI (capi.hip) and the kernel translation
+// units (fe.hip, fir.hip, pll.hip, psd.hip).  One definition of every struct that crosses a
+// translation-unit boundary: each .hip file includes this header, so a field change is a
+// compile error everywhere instead of a silent ODR mismatch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sdr_common.h"
+
+// RF front end (fe.hip): interleaved IQ -> FIR + decimate -> atan2 discriminator.
+struct FeLaunch {
+  const void* iq; int64_t n; int64_t stride; int64_t hist; int nstreams;
+  const float* taps_dev; const TapsF32* taps; int T; int D; int u8;
+  const double* zi_i; const double* zi_q; int64_t zi_stride; const double* prev_phase;
+  float* demod; int64_t out_stride; float* i_ds; float* q_ds; float* last_phi; int* wraps;
+};
+
+// Real-channel FIR with decimation (fir.hip); `pre` selects a fused pre-op on the input
+// (0 none, 1 x^2, 2 x*c*gain mixer).
+struct FirLaunch {
+  const float* x; const float* c; float gain; int pre; int64_t n; int64_t x_stride; int64_t x_step;
+  int64_t hist; int nstreams; const float* taps_dev; const TapsF32* taps; int T; int D;
+  const double* zi; int64_t zi_stride; float* y; int64_t y_stride;
+};
+
+// fmPll constants (pll.hip): model/fmPll.py:4-10
+struct PllCfg { double freq, fs, scale, adj, kp, ki; };
+
+hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st);
+hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
+                              int64_t audio_stride, hipStream_t st);
+hipError_t sdr_launch_iq_zf(const void* iq, int u8, int64_t n, int64_t stride, int nstreams,
+                            const double* b_dev, int T, const double* zi_i, const double* zi_q,
+                            int64_t zi_stride, double* zf_i, double* zf_q, hipStream_t st);
+hipError_t sdr_launch_demod(const float* I, const float* Q, int64_t n, int64_t stride, int nstreams,
+                            const double* prev_phase, float* out, int64_t out_stride,
+                            float* last_phi, int* wraps, hipStream_t st);
+hipError_t sdr_launch_demod_state(int nstreams, int64_t m, const float* last_phi, const int* wraps,
+                                  double* prev_phase, hipStream_t st);
+hipError_t sdr_launch_fir(const FirLaunch& a, hipStream_t st);
+hipError_t sdr_launch_resample(const float* x, int64_t n, const float* taps_dev, int T, int U, int D,
+                               const double* zi, float* y, hipStream_t st);
+hipError_t sdr_launch_zf(const float* x, const float* c, float gain, int pre, int64_t n,
+                         int64_t x_stride, int nstreams, int U, const double* b_dev, int T,
+                         const double* zi, int64_t zi_stride, double* zf, hipStream_t st);
+hipError_t sdr_launch_combine(const float* mono, const float* side, int64_t n, float* left,
+                              float* right, hipStream_t st);
+int sdr_psd_chunks(int64_t nseg);
+hipError_t sdr_launch_psd(const void* x, int f64, int64_t n, int logn, double fs, double* seg_db,
+                          double* part, double* out, int* zero_flag, hipStream_t st);
+hipError_t sdr_launch_dft(const double* x, int64_t n, double* X, hipStream_t st);
+hipError_t sdr_launch_pll(const float* in, int64_t n, int64_t in_stride, int nstreams,
+                          const PllCfg& cfg, double* state_dev, double* theta, int64_t th_stride,
+                          double* nco0, double* ncoq0, float* nco_i, float* nco_q,
+                          int64_t out_stride, hipStream_t st);
