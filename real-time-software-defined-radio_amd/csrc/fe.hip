@@ -190,12 +190,12 @@ __device__ __forceinline__ float fe_epilogue(const FeParams& p, int s, int64_t M
 // per step, issued by hand PF steps ahead with counted lgkmcnt waits (hipcc would split
 // the 16-B read into ds_read2_b64, 4-8-way bank-conflicted at this lane stride, and read
 // only one pair ahead); taps in VGPR pairs {h[2j], h[2j+1]}, broadcast by op_sel.
-template <int T, int D, int R, int PF>
+template <int T, int D, int R, int PF, int OFF = D>
 __device__ __forceinline__ void fe_fir_tile(const f2v* buf, int lane, const f2v (&tp)[(T + 1) / 2],
                                             float (&ai)[R], float (&aq)[R]) {
-  static_assert((T & 1) == 1, "odd tap counts (the lane window starts 16-B aligned)");
+  static_assert((T & 1) == 1 && (OFF & 1) == 0, "the lane window starts 16-B aligned");
   constexpr int NI = D * (R - 1) + T;
-  const f2v* win = buf + (D * R * lane + D);
+  const f2v* win = buf + (D * R * lane + OFF);
   const float4* win4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(win, 16));
   f2v acc[R], acc2[R];   // even / odd taps: 2R independent FMA chains
 #pragma unroll
@@ -276,7 +276,7 @@ struct Sched {
 template <int v> struct CW { static_assert(v >= 0 && v <= 15, "lgkmcnt field"); static constexpr int value = v; };
 }  // namespace fa
 
-template <int T, int PF, int APF>
+template <int T, int PF, int APF, int OFF>
 __device__ __forceinline__ void fir_audio_tile(const f2v* buf, int lane, const f2v (&tp)[(T + 1) / 2],
                                                float (&ai)[3], float (&aq)[3], const float* aw,
                                                const f4v* ptab, float& o0, float& o1, float& o2) {
@@ -285,7 +285,8 @@ __device__ __forceinline__ void fir_audio_tile(const f2v* buf, int lane, const f
   constexpr int NP = (NI + 1) / 2;                   // FE steps (sample pairs)
   constexpr int NS = 81;                             // audio steps (161-sample window in pairs)
   using S = fa::Sched<NP, NS, PF, APF>;
-  const f2v* win = buf + (D * R * lane + D);
+  static_assert((OFF & 1) == 0, "the lane window starts 16-B aligned");
+  const f2v* win = buf + (D * R * lane + OFF);
   const float4* win4 = reinterpret_cast<const float4*>(__builtin_assume_aligned(win, 16));
   f2v acc[R], acc2[R];
 #pragma unroll
@@ -421,7 +422,12 @@ template <int T, bool FUSED>
 __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, RingArgs a) {
   constexpr int D = 10, R = 3, TO = 64 * R;
   constexpr int NEWC = D * TO / 128;                 // 15 new 1-KiB chunks per tile
-  constexpr int NCH = (D * TO + T + 1 + 127) / 128;  // chunks per tile image
+  // image start n_lo = D*(m0-1) - (T-1) - DELTA, DELTA >= 0 chosen so that every chunk's
+  // source address is 128-B aligned (f32: n_lo % 16 == 0): a 1-KiB LDS-DMA then covers
+  // 8 whole cache lines instead of 9 partial ones
+  constexpr int DELTA = (16 - (D + T - 1) % 16) % 16;
+  constexpr int OFF = D + DELTA;                     // lane 0's window start in the image
+  constexpr int NCH = (D * TO + T + DELTA + 127) / 128;  // chunks per tile image
   constexpr int HCH = NCH - NEWC;                    // halo chunks shared with the next tile
   constexpr int L = NCH * 128;                       // image length (complex samples)
   constexpr int TP = (T + 1) / 2;
@@ -452,10 +458,20 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
 #pragma unroll
   for (int j = 0; j < TP; ++j) asm volatile("" : "+v"(tp[j]));
 
+  // this lane's taps for a run's cooperative predecessor output, loaded (and waited for)
+  // before any LDS-DMA is in flight: the first tile then needs no VMEM of its own
+  constexpr int NK = (T + 63) / 64;
+  float hk[NK];
+#pragma unroll
+  for (int q = 0; q < NK; ++q) hk[q] = (lane + 64 * q < T) ? p.taps_dev[lane + 64 * q] : 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int q = 0; q < NK; ++q) asm volatile("" : "+v"(hk[q]));
+
   const unsigned voff = 16u * lane;
   const float* iqf = reinterpret_cast<const float*>(p.iq);
   // tile i: outputs TO*i ..; image = samples [n_lo, n_lo + L), n_lo = D*(m0-1) - (T-1)
-  auto n_lo_of = [&](int ii) { return (int64_t)(D * TO) * ii - D - (T - 1); };
+  auto n_lo_of = [&](int ii) { return (int64_t)(D * TO) * ii - D - (T - 1) - DELTA; };
   // LDS-DMA needs the image inside [-hist, n) and a 16-B aligned base (the C-ABI passes
   // 16-B aligned IQ and an even stream stride for this kernel)
   auto dma_full = [&](int64_t nl) { return nl >= -p.hist && nl + L <= p.n; };
@@ -477,15 +493,21 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
     return NEWC;
   };
   // guarded image build (stream edges): zeros outside [-hist, n)
+  // every lane's L/64 predicated 8-B loads are issued before the first use (one memory
+  // round trip; a load-use loop here serialised ~32 round trips and made the waves
+  // holding a stream's head or tail the last to finish)
   auto build = [&](int ss, int64_t nl, int sl) {
-    const float* base = iqf + 2 * ((int64_t)ss * p.stride);
+    const f2v* base = reinterpret_cast<const f2v*>(iqf) + (int64_t)ss * p.stride;
     f2v* buf = &ring[sl][0];
-    for (int e = lane; e < L; e += 64) {
-      const int64_t nn = nl + e;
-      f2v x = f2v{0.f, 0.f};
-      if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
-      buf[e] = x;
+    constexpr int NPL = L / 64;
+    f2v v[NPL];
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) {
+      const int64_t nn = nl + 64 * j + lane;
+      v[j] = (nn >= -p.hist && nn < p.n) ? base[nn] : f2v{0.f, 0.f};
     }
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) buf[64 * j + lane] = v[j];
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   };
 
@@ -518,15 +540,29 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
   int wacc = 0;                                    // per-lane 2*pi correction count
 
   // ---- deferred outputs (OutQ3): FE demod tiles / FUSED audio blocks ----
-  constexpr int QN = FUSED ? 8 : 36;
+  constexpr int QN = FUSED ? 12 : 36;
   OutQ3<QN> oq;
   int qn = 0, qs = 0;
   int64_t q0 = 0;                                  // FE: first tile; FUSED: first audio block
+  // FUSED: audio outputs [own_lo(ss), own_hi(ss)) of stream ss are this run's (5 j inside
+  // its tile range): every output is stored by exactly one wave
+  auto own_lo = [&](int ss) {
+    const int64_t lo = max<int64_t>(g0 - (int64_t)ss * a.tps, 0);
+    return (TO * lo + DA - 1) / DA;
+  };
+  auto own_hi = [&](int ss) {
+    const int64_t hi = min<int64_t>(g1 - (int64_t)ss * a.tps, a.tps);
+    return min<int64_t>((TO * hi + DA - 1) / DA, (M + DA - 1) / DA);
+  };
   auto q_flush = [&]() __attribute__((always_inline)) {
     if (qn == 0) return;
-    float* base = FUSED ? a.audio + (int64_t)qs * a.audio_stride + q0 * BO + RA * lane
-                        : p.demod + (int64_t)qs * p.out_stride + q0 * TO + R * lane;
-    issued += oq.flush(base, TO, qn);
+    if constexpr (FUSED) {
+      // masked stores: not counted in `issued` (a smaller count only makes waits longer)
+      oq.flush_owned(a.audio + (int64_t)qs * a.audio_stride + q0 * BO + RA * lane, BO, qn,
+                     q0 * BO + RA * lane, own_lo(qs), own_hi(qs));
+    } else {
+      issued += oq.flush(p.demod + (int64_t)qs * p.out_stride + q0 * TO + R * lane, TO, qn);
+    }
     qn = 0;
   };
   auto q_push = [&](int64_t idx, float x0, float x1, float x2) __attribute__((always_inline)) {
@@ -538,31 +574,10 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
 
   // ---- FUSED audio pieces ----
   const float* aw_lane = dh + (HA - (TA - 1) + DA * RA * lane);   // lane window in dh
-  // outputs [jlo, A) of stream s are this run's (5 j inside its tile range)
-  auto own_lo = [&]() {
-    const int64_t lo = max<int64_t>(g0 - (int64_t)s * a.tps, 0);
-    return (TO * lo + DA - 1) / DA;
-  };
-  auto own_hi = [&]() {
-    const int64_t hi = min<int64_t>(g1 - (int64_t)s * a.tps, a.tps);
-    return min<int64_t>((TO * hi + DA - 1) / DA, (M + DA - 1) / DA);
-  };
-  // block q's outputs: queued when the block is wholly this run's, else stored now (the
-  // owned ones) and drained; returns true if vmcnt was drained
+  // block q's outputs go to the deferred queue (the flush keeps to the owned outputs)
   auto audio_put = [&](int64_t q, float o0, float o1, float o2) __attribute__((always_inline)) -> bool {
-    const int64_t jlo = own_lo(), A = own_hi();
-    if (q * BO >= jlo && q * BO + BO <= A) {
-      q_push(q, o0, o1, o2);
-      return false;
-    }
-    const int64_t j = q * BO + RA * lane;
-    float* ao = a.audio + (int64_t)s * a.audio_stride + j;
-    if (j >= jlo && j < A) ao[0] = o0;
-    if (j + 1 >= jlo && j + 1 < A) ao[1] = o1;
-    if (j + 2 >= jlo && j + 2 < A) ao[2] = o2;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    issued = 0;
-    return true;
+    q_push(q, o0, o1, o2);
+    return false;
   };
   auto dh_shift = [&](bool next_same) {
     asm volatile("" ::: "memory");
@@ -583,7 +598,96 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
   bool pend = false;                               // FUSED: a finished block's audio is due
   int64_t q_pend = 0;
 
+  // interior tile epilogue: phases, predecessor (DPP / carry), np.unwrap wrap
+  auto fast_epi = [&](const float (&ai)[R], const float (&aq)[R], float (&d)[R]) __attribute__((always_inline)) {
+    float phi[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) phi[r] = fast_atan2f(aq[r], ai[r]);
+    const float from_left = __int_as_float(__builtin_amdgcn_update_dpp(
+        0, __float_as_int(phi[R - 1]), 0x138 /*wave_shr:1*/, 0xf, 0xf, false));
+    float prev = (lane == 0) ? carry : from_left;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float dd = phi[r] - prev;
+      if (dd > kPiF) { dd -= k2PiF; wacc -= 1; }
+      else if (dd < -kPiF) { dd += k2PiF; wacc += 1; }
+      d[r] = dd;
+      prev = phi[r];
+    }
+    carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[R - 1]), 63));
+  };
+  // last tile whose image is interior (DMA) and last tile with the fast epilogue, per stream
+  const int64_t jn = p.n + D + (T - 1) + DELTA - L;
+  const int64_t j_int = jn >= 0 ? jn / (D * TO) : -1;
+  const int64_t j_fast = M >= TO + 1 ? (M - TO - 1) / TO : -1;
+
   for (int u = 0; u < U; ++u) {
+    // ---- steady run: consecutive interior tiles of one stream, fixed VMEM pattern ----
+    // Entry: tile i's new chunks are in flight into slot b (its halo written), carry valid.
+    // Per tile: the next tile's 15 chunks -> slot b^1, s_waitcnt vmcnt(15), FIR, halo,
+    // fast epilogue, outputs to the deferred queue.  Exit: the same state for tile i+K.
+    if (kind == K_HALO && have && p.i_ds == nullptr) {
+      int64_t K = min<int64_t>(U - 1 - u, a.tps - 1 - i);
+      K = min<int64_t>(K, j_int - i);
+      K = min<int64_t>(K, j_fast - i + 1);
+      if constexpr (!FUSED) {
+        if (qn > 0 && (qs != s || q0 + qn != i)) q_flush();
+        K = min<int64_t>(K, QN - qn);
+      }
+      if (K > 0) {
+        const char* gn = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)s * p.stride + nl + D * TO)) + 1024 * HCH;
+        const int first_wait = issued - mark + NEWC;
+        for (int k = 0; k < (int)K; ++k) {
+          const unsigned lb = lds_addr_of(&ring[b ^ 1][0]) + 1024 * HCH;
+          static_for<0, (NEWC + 3) / 4>([&](auto Q) {
+            constexpr int c = 4 * Q;
+            constexpr int nc = (NEWC - c) < 4 ? (NEWC - c) : 4;
+            glds16x<nc>(voff, gn + 1024 * c, lb + 1024 * c);
+          });
+          gn += D * TO * 8;
+          issued += NEWC;
+          int mk = issued;
+          // tile i: every VMEM instruction after its DMA is this tile's 15 chunks (k > 0:
+          // stores issued in between only make the wait longer, never short)
+          if (k == 0) wait_vm(first_wait);
+          else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NEWC) : "memory");
+          f2v* buf = &ring[b][0];
+          f2v* nb = &ring[b ^ 1][0];
+          f4v h0 = lds_read_b128<0>(buf + NEWC * 128 + 2 * lane), h1;
+          if constexpr (HCH == 2) h1 = lds_read_b128<0>(buf + (NEWC + 1) * 128 + 2 * lane);
+          float ai[R], aq[R];
+          if constexpr (FUSED) {
+            if (pend) {
+              float o0, o1, o2;
+              fir_audio_tile<T, 2, 2, OFF>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2);
+              if (audio_put(q_pend, o0, o1, o2)) mk = issued;
+              dh_shift(true);
+              pend = false;
+            } else {
+              fe_fir_tile<T, D, R, PF, OFF>(buf, lane, tp, ai, aq);
+            }
+          } else {
+            fe_fir_tile<T, D, R, PF, OFF>(buf, lane, tp, ai, aq);
+          }
+          lds_wait<0>(h0);
+          lds_write_b128(nb + 2 * lane, h0);
+          if constexpr (HCH == 2) { lds_wait<0>(h1); lds_write_b128(nb + 128 + 2 * lane, h1); }
+          float d[R];
+          fast_epi(ai, aq, d);
+          if constexpr (FUSED) {
+            dh_write(i, false, d);
+            if (i % TPB == TPB - 1) { pend = true; q_pend = i / TPB; }
+          } else {
+            q_push(i, d[0], d[1], d[2]);
+          }
+          mark = mk;
+          b ^= 1;
+          ++i;
+          nl += D * TO;
+        }
+        u += (int)K;
+      }
+    }
     // ---- next tile: position, kind, DMA issue (before this tile's wait) ----
     int s1 = s, i1 = i + 1;
     if (i1 == a.tps) { i1 = 0; ++s1; }
@@ -612,15 +716,15 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
     if constexpr (FUSED) {
       if (pend) {                                  // the previous block's audio, interleaved
         float o0, o1, o2;
-        fir_audio_tile<T, 2, 2>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2);
+        fir_audio_tile<T, 2, 2, OFF>(buf, lane, tp, ai, aq, aw_lane, ptab, o0, o1, o2);
         if (audio_put(q_pend, o0, o1, o2)) mark1 = 0;
         dh_shift(true);
         pend = false;
       } else {
-        fe_fir_tile<T, D, R, PF>(buf, lane, tp, ai, aq);
+        fe_fir_tile<T, D, R, PF, OFF>(buf, lane, tp, ai, aq);
       }
     } else {
-      fe_fir_tile<T, D, R, PF>(buf, lane, tp, ai, aq);
+      fe_fir_tile<T, D, R, PF, OFF>(buf, lane, tp, ai, aq);
     }
     if (kind1 == K_HALO) {
       f2v* nb = &ring[b ^ 1][0];
@@ -632,36 +736,33 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
     // ---- epilogue ----
     const int64_t m0 = (int64_t)TO * i;
     float d[R];
-    if (have && i >= 1 && m0 + TO < M && p.i_ds == nullptr) {
-      // interior tile: phases, predecessor (DPP / carry), np.unwrap wrap; output deferred
-      float phi[R];
+    // predecessor output m0-1 of a run's first tile: image samples [0, T), register taps
+    auto pred = [&](float& si, float& sq) {
+      si = 0.f; sq = 0.f;
 #pragma unroll
-      for (int r = 0; r < R; ++r) phi[r] = fast_atan2f(aq[r], ai[r]);
-      const float from_left = __int_as_float(__builtin_amdgcn_update_dpp(
-          0, __float_as_int(phi[R - 1]), 0x138 /*wave_shr:1*/, 0xf, 0xf, false));
-      float prev = (lane == 0) ? carry : from_left;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        float dd = phi[r] - prev;
-        if (dd > kPiF) { dd -= k2PiF; wacc -= 1; }
-        else if (dd < -kPiF) { dd += k2PiF; wacc += 1; }
-        d[r] = dd;
-        prev = phi[r];
+      for (int q = 0; q < NK; ++q) {
+        if (lane + 64 * q < T) {
+          const f2v x = buf[DELTA + (T - 1) - (lane + 64 * q)];
+          si = fmaf(hk[q], x.x, si);
+          sq = fmaf(hk[q], x.y, sq);
+        }
       }
-      carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[R - 1]), 63));
+      si = wave_sum(si);
+      sq = wave_sum(sq);
+    };
+    if (!have && i >= 1 && m0 + TO < M && p.i_ds == nullptr) {
+      // an interior first tile (no zi, no carried phase, no store of its own): the fast path
+      float si, sq;
+      pred(si, sq);
+      carry = fast_atan2f(sq, si);
+      have = true;
+    }
+    if (have && i >= 1 && m0 + TO < M && p.i_ds == nullptr) {
+      fast_epi(ai, aq, d);                         // interior tile; output deferred
       if constexpr (!FUSED) q_push(i, d[0], d[1], d[2]);
     } else {
       float si = 0.f, sq = 0.f;
-      if (m0 > 0 && !have) {                       // output m0-1: image samples [0, T)
-        for (int k = lane; k < T; k += 64) {
-          const f2v x = buf[(T - 1) - k];
-          const float h = p.taps_dev[k];
-          si = fmaf(h, x.x, si);
-          sq = fmaf(h, x.y, sq);
-        }
-        si = wave_sum(si);
-        sq = wave_sum(sq);
-      }
+      if (m0 > 0 && !have) pred(si, sq);           // output m0-1
       carry = fe_epilogue<T, D, R>(p, s, M, m0, lane, ai, aq, si, sq, have, carry, d, !FUSED);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       issued = 0; mark1 = 0;
@@ -832,13 +933,17 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
   auto build_sync = [&](int ss, int64_t nl) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if constexpr (U8) {
-      const uint8_t* base = reinterpret_cast<const uint8_t*>(p.iq) + 2 * ((int64_t)ss * p.stride);
-      for (int e = lane; e < L; e += 64) {
-        const int64_t nn = nl + e;
-        f2v x = f2v{0.f, 0.f};
-        if (nn >= -p.hist && nn < p.n) x = f2v{cvt8(base[2 * nn]), cvt8(base[2 * nn + 1])};
-        slot[e] = x;
+      // all predicated 2-B loads (one complex u8 sample each) in flight before the first use
+      const uint16_t* base = reinterpret_cast<const uint16_t*>(p.iq) + (int64_t)ss * p.stride;
+      constexpr int NPL = L / 64;
+      uint32_t v[NPL];
+#pragma unroll
+      for (int j = 0; j < NPL; ++j) {
+        const int64_t nn = nl + 64 * j + lane;
+        v[j] = (nn >= -p.hist && nn < p.n) ? (uint32_t)base[nn] : 0x8080u;   // 0x80 -> 0.0
       }
+#pragma unroll
+      for (int j = 0; j < NPL; ++j) slot[64 * j + lane] = f2v{cvt8(v[j] & 0xff), cvt8(v[j] >> 8)};
     } else if (interior(nl)) {
       const char* g = reinterpret_cast<const char*>(iqf + 2 * ((int64_t)ss * p.stride + nl));
       const unsigned lb = lds_addr_of(slot);
@@ -848,13 +953,16 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
         glds16x<n>(voff, g + 1024 * c, lb + 1024 * c);
       });
     } else {
-      const float* base = iqf + 2 * ((int64_t)ss * p.stride);
-      for (int e = lane; e < L; e += 64) {
-        const int64_t nn = nl + e;
-        f2v x = f2v{0.f, 0.f};
-        if (nn >= -p.hist && nn < p.n) x = f2v{base[2 * nn], base[2 * nn + 1]};
-        slot[e] = x;
+      const f2v* base = reinterpret_cast<const f2v*>(iqf) + (int64_t)ss * p.stride;
+      constexpr int NPL = L / 64;
+      f2v v[NPL];
+#pragma unroll
+      for (int j = 0; j < NPL; ++j) {
+        const int64_t nn = nl + 64 * j + lane;
+        v[j] = (nn >= -p.hist && nn < p.n) ? base[nn] : f2v{0.f, 0.f};
       }
+#pragma unroll
+      for (int j = 0; j < NPL; ++j) slot[64 * j + lane] = v[j];
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   };

@@ -275,6 +275,25 @@ struct OutQ3 {
     });
     return cnt;
   }
+  // as flush, but element r of entry j (global index e0 + step*j + r) is stored only when
+  // it lies in [lo, hi); whole entries inside the range take one 12-B store
+  __device__ __forceinline__ void flush_owned(float* p, int64_t step, int cnt, int64_t e0, int64_t lo, int64_t hi) {
+    typedef float f3v __attribute__((ext_vector_type(3)));
+    static_for<0, Q>([&](auto J) {
+      constexpr int j = J;
+      if (j < cnt) {
+        const int64_t e = e0 + step * j;
+        float* q = p + step * j;
+        if (e >= lo && e + 2 < hi) {
+          *reinterpret_cast<f3v*>(q) = f3v{v[j][0], v[j][1], v[j][2]};
+        } else {
+          if (e >= lo && e < hi) q[0] = v[j][0];
+          if (e + 1 >= lo && e + 1 < hi) q[1] = v[j][1];
+          if (e + 2 >= lo && e + 2 < hi) q[2] = v[j][2];
+        }
+      }
+    });
+  }
 };
 
 // Wave-wide sum over 64 lanes (CDNA wave64: six xor steps).

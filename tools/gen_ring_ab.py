@@ -93,14 +93,15 @@ int main() {
   vs.push_back({"FUSED r01 (ring)", [=] { CK(r01_launch_fe_mono(la, adev, 151, 5, au, n / 50, st)); }});
   FU("FUSED KN=0", 0) FU("FUSED KN=2 no queue", 2) FU("FUSED KN=8 fixed wait", 8) FU("FUSED KN=32 no audio", 32)
   FU("FUSED KN=64 no dh", 64) FU("FUSED KN=96", 96) FU("FUSED KN=1 trivial epi", 1) FU("FUSED KN=111", 111)
+  const bool quick = getenv("AB_QUICK") != nullptr;   // counter runs: few launches
   for (auto& v : vs) v.go();
   CK(hipStreamSynchronize(st));
-  for (int i = 0; i < 3000; ++i) vs[0].go();
-  for (int pass = 0; pass < 2; ++pass)
+  for (int i = 0; i < (quick ? 0 : 3000); ++i) vs[0].go();
+  for (int pass = quick ? 1 : 0; pass < 2; ++pass)
     for (auto& v : vs) {
-      for (int i = 0; i < 200; ++i) v.go();
+      for (int i = 0; i < (quick ? 5 : 200); ++i) v.go();
       CK(hipEventRecord(a, st));
-      for (int i = 0; i < 50; ++i) v.go();
+      for (int i = 0; i < (quick ? 5 : 50); ++i) v.go();
       CK(hipEventRecord(b, st)); CK(hipEventSynchronize(b)); CK(hipGetLastError());
       float ms; CK(hipEventElapsedTime(&ms, a, b)); ms /= 50;
       printf("pass %d %-36s %8.2f us  %7.1f GB/s (8 B/sample in)\n", pass, v.nm, ms * 1e3, 8.0 * n / ms / 1e6);
