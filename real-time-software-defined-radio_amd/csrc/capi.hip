@@ -18,7 +18,7 @@
 #include <new>
 #include <cstdarg>
 #include <cstdio>
-#include <deque>
+#include <list>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -73,7 +73,10 @@ struct sdr_ctx {
   hipStream_t stream = nullptr;
   void* slot[S_NSLOT] = {};
   size_t cap[S_NSLOT] = {};
-  std::deque<TapSet> taps;  // small cache (deque: stable element addresses) of uploaded tap sets (taps are designed once)
+  // uploaded tap sets (taps are designed once), least recently used first.  A list: a hit
+  // is spliced to the back and an overflow evicts the front, so no pointer handed out by
+  // a lookup is invalidated by the other lookups of the same entry point (<= 4 per call).
+  std::list<TapSet> taps;
 };
 
 namespace {
@@ -106,15 +109,18 @@ int scratch(sdr_ctx* c, Slot s, size_t bytes, void** out) {
 int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T = SDR_MAX_TAPS) {
   if (b == nullptr) return fail(SDR_EINVAL, "taps pointer is NULL");
   if (T < 1 || T > max_T) return fail(SDR_EINVAL, "taps=%d outside [1, %d]", T, max_T);
-  for (const TapSet& t : c->taps)
-    if ((int)t.b.size() == T && std::memcmp(t.b.data(), b, sizeof(double) * T) == 0) {
-      *out = &t;
+  for (auto it = c->taps.begin(); it != c->taps.end(); ++it)
+    if ((int)it->b.size() == T && std::memcmp(it->b.data(), b, sizeof(double) * T) == 0) {
+      c->taps.splice(c->taps.end(), c->taps, it);   // most recently used last; `it` stays valid
+      *out = &*it;
       return SDR_OK;
     }
-  if (c->taps.size() >= 64) {  // bounded cache: drop everything (rare: taps change per block)
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    for (TapSet& t : c->taps) { (void)hipFree(t.dev_f32); (void)hipFree(t.dev_f64); }
-    c->taps.clear();
+  if (c->taps.size() >= 64) {  // bounded cache: evict the least recently used set
+    HIP_TRY(hipStreamSynchronize(c->stream));     // kernels in flight may still read it
+    TapSet& t = c->taps.front();
+    (void)hipFree(t.dev_f32);
+    (void)hipFree(t.dev_f64);
+    c->taps.pop_front();
   }
   TapSet t;
   t.b.assign(b, b + T);
@@ -371,7 +377,6 @@ int sdr_fe_mono_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t
   const TapSet *rts, *ats;
   TRY(get_taps(c, audio_b, audio_taps, &ats));
   TRY(get_taps(c, rf_b, rf_taps, &rts));
-  TRY(get_taps(c, audio_b, audio_taps, &ats));   // again: the second lookup may have reset the cache
   const int u8 = iq_dtype == SDR_IQ_U8;
   const int64_t xs = nstreams > 1 ? stride : ceil_div(n, 2) * 2;
   const int64_t as = nstreams > 1 ? audio_stride : A;
