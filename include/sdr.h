@@ -181,6 +181,57 @@ int sdr_pll_dev(sdr_ctx* ctx, const float* in, int64_t n, int64_t in_stride, int
 int sdr_stereo_combine_dev(sdr_ctx* ctx, const float* mono, const float* side, int64_t n,
                            float* left, float* right);
 
+/* ---- multi-stream block receiver ----------------------------------
+ * The per-block loops of model/fmMonoBlock.py:80-173 (mono, stereo; intended L/R combiner)
+ * and model/fmRDSblock.py:127-204 (RDS up to the RRC output) for `nstreams` independent
+ * streams at once, every filter state, demod phase and PLL state carried in HBM from block
+ * to block (C++: the rf / mono_stereo / rds threads of src/fm_radio.cpp:31-441, 783-792).
+ * One block of all streams is a fixed chain of ~10 launches on the context stream,
+ * whatever nstreams is: the FE, one launch per stage for all filters of that stage (with
+ * their lfilter final states), and one lane per PLL recurrence.
+ *   flags: SDR_RX_AUDIO (mono audio), SDR_RX_STEREO (implies AUDIO), SDR_RX_RDS.
+ *   Filters (taps f64, designed by the caller, <= SDR_MAX_TAPS, set before the first block):
+ *   SDR_RX_F_RF (+ rf_decim), F_AUDIO (+ audio_decim), F_PILOT, F_STEREO_BPF, F_STEREO_LPF
+ *   (decim audio_decim), F_RDS_EXTRACT, F_RDS_SQUARE, F_RDS_LPF, F_RDS_ANTI (on the
+ *   x rds_up zero-stuffed stream, then [::rds_down] x rds_up), F_RDS_RRC.
+ *   PLLs default to the reference's: stereo 19 kHz x2 BW 0.01 (fmMonoBlock.py:119), RDS
+ *   114 kHz x0.5 phase pi/3.3-pi/1.5 BW 0.001 (fmRDSblock.py:167), both at Fs 240 kHz.
+ * Outputs live in receiver-owned device memory, `stride` floats apart per stream, and are
+ * overwritten by the next block: M = ceil(block/rf_decim) demod-rate samples (NCOs: M+1,
+ * index 0 = the carried value), A = ceil(M/audio_decim) audio-rate, R = ceil(M*up/down)
+ * RDS-rate.  Inputs: nstreams rows of `block` interleaved complex samples, iq_stride
+ * complex samples apart (f32 or u8). */
+typedef struct sdr_rx sdr_rx;
+enum { SDR_RX_AUDIO = 1, SDR_RX_STEREO = 2, SDR_RX_RDS = 4 };
+enum {
+  SDR_RX_F_RF, SDR_RX_F_AUDIO, SDR_RX_F_PILOT, SDR_RX_F_STEREO_BPF, SDR_RX_F_STEREO_LPF,
+  SDR_RX_F_RDS_EXTRACT, SDR_RX_F_RDS_SQUARE, SDR_RX_F_RDS_LPF, SDR_RX_F_RDS_ANTI, SDR_RX_F_RDS_RRC,
+  SDR_RX_NFILTERS
+};
+enum {
+  SDR_RX_O_DEMOD, SDR_RX_O_AUDIO,                                   /* fm_demod, audio_block */
+  SDR_RX_O_BPF_RECOVERY, SDR_RX_O_STEREO_NCO, SDR_RX_O_BPF_EXTRACTION, SDR_RX_O_STEREO,
+  SDR_RX_O_LEFT, SDR_RX_O_RIGHT,                                    /* fmMonoBlock.py:115-170 */
+  SDR_RX_O_RDS_EXTRACT, SDR_RX_O_RDS_PRE_PLL, SDR_RX_O_RDS_NCO_I, SDR_RX_O_RDS_NCO_Q,
+  SDR_RX_O_RDS_LPF_I, SDR_RX_O_RDS_LPF_Q, SDR_RX_O_RDS_RES_I, SDR_RX_O_RDS_RES_Q,
+  SDR_RX_O_RDS_RRC_I, SDR_RX_O_RDS_RRC_Q,                           /* fmRDSblock.py:156-204 */
+  SDR_RX_NOUTPUTS
+};
+int sdr_rx_create(sdr_ctx* ctx, int nstreams, int64_t block, int iq_dtype, int flags, sdr_rx** out);
+void sdr_rx_destroy(sdr_rx* rx);
+int sdr_rx_set_filter(sdr_rx* rx, int which, const double* b, int taps);
+int sdr_rx_set_decim(sdr_rx* rx, int rf_decim, int audio_decim, int rds_up, int rds_down);
+int sdr_rx_set_pll(sdr_rx* rx, int which /* 0 stereo, 1 RDS */, double freq, double fs,
+                   double nco_scale, double phase_adj, double norm_bw);
+int sdr_rx_reset(sdr_rx* rx);                       /* all states back to the stream start */
+int sdr_rx_process_dev(sdr_rx* rx, const void* iq, int64_t iq_stride);   /* async, device IQ */
+int sdr_rx_process(sdr_rx* rx, const void* iq, int64_t iq_stride);       /* sync, host IQ */
+int sdr_rx_output(sdr_rx* rx, int which, float** dev, int64_t* stride, int64_t* n);
+int sdr_rx_fetch(sdr_rx* rx, int which, float* host, int64_t host_stride); /* sync, all streams */
+/* carried states (host copies; any may be NULL): demod prev_phase [nstreams], PLL states
+ * [nstreams][6] in fmPll's order (model/fmPll.py:39-44) */
+int sdr_rx_state(sdr_rx* rx, double* phase, double* pll_stereo, double* pll_rds);
+
 /* ---- spectral diagnostics -----------------------------------------
  * Bartlett PSD, model/fmSupportLib.py:66-140 (estimatePSD; the C++ src/fourier.cpp:36-110
  * advances sample and list positions by the same nfft/2 and is not the parity target):

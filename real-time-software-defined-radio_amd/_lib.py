@@ -19,6 +19,13 @@ SDR_OK, SDR_EINVAL, SDR_EHIP, SDR_ENOMEM, SDR_EUNSUPPORTED, SDR_EDOMAIN = 0, -1,
 SDR_REAL_F32, SDR_REAL_F64 = 0, 1
 SDR_IQ_F32, SDR_IQ_U8 = 0, 1
 SDR_PRE_NONE, SDR_PRE_SQUARE, SDR_PRE_MIX = 0, 1, 2
+# multi-stream receiver (include/sdr.h sdr_rx_*)
+SDR_RX_AUDIO, SDR_RX_STEREO, SDR_RX_RDS = 1, 2, 4
+RX_FILTERS = ("rf", "audio", "pilot", "stereo_bpf", "stereo_lpf", "rds_extract", "rds_square", "rds_lpf",
+              "rds_anti", "rds_rrc")
+RX_OUTPUTS = ("demod", "audio", "bpf_recovery", "nco", "bpf_extraction", "stereo", "left", "right",
+              "extract", "pre_pll", "nco_i", "nco_q", "lpf_i", "lpf_q", "resample_i", "resample_q",
+              "rrc_i", "rrc_q")
 
 
 class SdrUnavailable(RuntimeError):
@@ -74,6 +81,17 @@ SIGNATURES = {
     "sdr_psd": (_i32, [_vp, _dp, _i64, _i32, _f64, _dp]),
     "sdr_psd_dev": (_i32, [_vp, _vp, _i32, _i64, _i32, _f64, _vp]),
     "sdr_dft": (_i32, [_vp, _dp, _i64, _dp]),
+    "sdr_rx_create": (_i32, [_vp, _i32, _i64, _i32, _i32, _c.POINTER(_vp)]),
+    "sdr_rx_destroy": (None, [_vp]),
+    "sdr_rx_set_filter": (_i32, [_vp, _i32, _dp, _i32]),
+    "sdr_rx_set_decim": (_i32, [_vp, _i32, _i32, _i32, _i32]),
+    "sdr_rx_set_pll": (_i32, [_vp, _i32, _f64, _f64, _f64, _f64, _f64]),
+    "sdr_rx_reset": (_i32, [_vp]),
+    "sdr_rx_process_dev": (_i32, [_vp, _vp, _i64]),
+    "sdr_rx_process": (_i32, [_vp, _vp, _i64]),
+    "sdr_rx_output": (_i32, [_vp, _i32, _c.POINTER(_vp), _c.POINTER(_i64), _c.POINTER(_i64)]),
+    "sdr_rx_fetch": (_i32, [_vp, _i32, _fp, _i64]),
+    "sdr_rx_state": (_i32, [_vp, _dp, _dp, _dp]),
     "sdr_rds_link_create": (_i32, [_c.POINTER(_vp)]),
     "sdr_rds_link_destroy": (None, [_vp]),
     "sdr_rds_link_block": (_i32, [_vp, _dp, _i64, _vp, _i64, _c.POINTER(_i64), _vp, _i64, _c.POINTER(_i64),

@@ -18,23 +18,21 @@
 #include <new>
 #include <cstdarg>
 #include <cstdio>
-#include <list>
 #include <cstring>
 #include <mutex>
-#include <string>
-#include <vector>
 
-#include "sdr_launch.h"
-#include "../../include/sdr.h"
+#include "sdr_ctx.h"
 
-// launchers implemented in fe.hip / fir.hip / pll.hip / psd.hip: sdr_launch.h
+// launchers implemented in fe.hip / fir.hip / pll.hip / psd.hip: sdr_launch.h;
+// context internals shared with rx.hip: sdr_ctx.h
+using namespace sdrint;
 
-// ---- context ------------------------------------------------------------------
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+namespace sdrint {
+
 int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
@@ -44,42 +42,6 @@ int fail(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
-
-#define HIP_TRY(expr)                                                                   \
-  do {                                                                                  \
-    hipError_t e_ = (expr);                                                             \
-    if (e_ != hipSuccess)                                                               \
-      return fail(SDR_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
-  } while (0)
-
-// scratch slots owned by a context (grown on demand, never shrunk)
-enum Slot {
-  S_IN, S_IN2, S_OUT, S_OUT2, S_OUT3, S_OUT4, S_STATE, S_STATE2, S_MISC, S_THETA, S_PHI, S_WRAP,
-  S_PSD,
-  S_NSLOT
-};
-
-struct TapSet {
-  std::vector<double> b;
-  TapsF32 h;
-  float* dev_f32 = nullptr;
-  double* dev_f64 = nullptr;
-};
-
-}  // namespace
-
-struct sdr_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  void* slot[S_NSLOT] = {};
-  size_t cap[S_NSLOT] = {};
-  // uploaded tap sets (taps are designed once), least recently used first.  A list: a hit
-  // is spliced to the back and an overflow evicts the front, so no pointer handed out by
-  // a lookup is invalidated by the other lookups of the same entry point (<= 4 per call).
-  std::list<TapSet> taps;
-};
-
-namespace {
 
 int set_dev(sdr_ctx* c) {
   HIP_TRY(hipSetDevice(c->device));
@@ -106,7 +68,7 @@ int scratch(sdr_ctx* c, Slot s, size_t bytes, void** out) {
 
 // max_T: SDR_MAX_TAPS for the FIR kernels (taps also passed by value, TapsF32), up to
 // SDR_MAX_RESAMPLE_TAPS for the resampler (device arrays only; h holds the first 256).
-int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T = SDR_MAX_TAPS) {
+int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T) {
   if (b == nullptr) return fail(SDR_EINVAL, "taps pointer is NULL");
   if (T < 1 || T > max_T) return fail(SDR_EINVAL, "taps=%d outside [1, %d]", T, max_T);
   for (auto it = c->taps.begin(); it != c->taps.end(); ++it)
@@ -138,16 +100,9 @@ int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T =
   return SDR_OK;
 }
 
-#define TRY(expr)                 \
-  do {                            \
-    int r_ = (expr);              \
-    if (r_ != SDR_OK) return r_;  \
-  } while (0)
+}  // namespace sdrint
 
-#define CHECK_CTX(c) \
-  if ((c) == nullptr) return fail(SDR_EINVAL, "context is NULL")
-
-int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+namespace {
 
 int h2d(sdr_ctx* c, void* dst, const void* src, size_t bytes) {
   if (bytes) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
@@ -297,7 +252,8 @@ int sdr_rf_frontend_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int
   const int64_t M = ceil_div(n, decim);
   if (n > 0 && (iq == nullptr || demod == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
   if (nstreams > 1 && (out_stride < M || stride < n)) return fail(SDR_EINVAL, "stream strides too small");
-  if (nstreams > 1 && zi_i && zi_stride < taps - 1) return fail(SDR_EINVAL, "zi_stride too small");
+  if (nstreams > 1 && (zi_i || zf_i) && zi_stride < taps - 1)
+    return fail(SDR_EINVAL, "zi_stride %lld < taps-1", (long long)zi_stride);
   TRY(set_dev(c));
   const TapSet* ts;
   TRY(get_taps(c, b, taps, &ts));
@@ -412,6 +368,8 @@ int sdr_fir_dev(sdr_ctx* c, const float* x, const float* mix, float gain, int pr
   const int64_t M = ceil_div(n, decim);
   if (n > 0 && (x == nullptr || y == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
   if (nstreams > 1 && (y_stride < M || x_stride < n)) return fail(SDR_EINVAL, "stream strides too small");
+  if (nstreams > 1 && (zi || zf) && zi_stride < taps - 1)
+    return fail(SDR_EINVAL, "zi_stride %lld < taps-1", (long long)zi_stride);
   TRY(set_dev(c));
   const TapSet* ts;
   TRY(get_taps(c, b, taps, &ts));
@@ -478,14 +436,21 @@ int sdr_pll_dev(sdr_ctx* c, const float* in, int64_t n, int64_t in_stride, int n
   if (state == nullptr || nco_i == nullptr || (n > 0 && in == nullptr)) return fail(SDR_EINVAL, "NULL buffer");
   if (!(fs != 0.0)) return fail(SDR_EINVAL, "Fs must be non-zero");
   TRY(set_dev(c));
-  PllCfg cfg{freq, fs, nco_scale, phase_adj, norm_bw * 2.666, norm_bw * norm_bw * 3.555};
+  if (nstreams > 1 && (in_stride < n || out_stride < n + 1))
+    return fail(SDR_EINVAL, "stream strides too small (in_stride %lld < n or out_stride %lld < n+1)",
+                (long long)in_stride, (long long)out_stride);
+  if (nstreams == 0) return SDR_OK;
+  PllJobs P{};
+  P.njobs = 1;
+  P.nstreams = nstreams;
+  P.n = n;
+  const int64_t ths = (n + 1) / 2 * 2 + 2;          // even: 16-B aligned phase rows
   double* theta;
-  double* misc;
-  const int64_t ths = n > 0 ? n : 1;
   TRY(scratch(c, S_THETA, sizeof(double) * (size_t)ths * nstreams, (void**)&theta));
-  TRY(scratch(c, S_MISC, sizeof(double) * 2 * (size_t)nstreams, (void**)&misc));
-  HIP_TRY(sdr_launch_pll(in, n, nstreams > 1 ? in_stride : n, nstreams, cfg, state, theta, ths, misc,
-                         misc + nstreams, nco_i, nco_q, nstreams > 1 ? out_stride : n + 1, c->stream));
+  P.j[0] = PllJob{in, nstreams > 1 ? in_stride : n, state, theta, ths, nco_i, nco_q,
+                  nstreams > 1 ? out_stride : n + 1,
+                  PllCfg{freq, fs, nco_scale, phase_adj, norm_bw * 2.666, norm_bw * norm_bw * 3.555}};
+  HIP_TRY(sdr_launch_pll_jobs(P, c->stream));
   return SDR_OK;
 }
 

@@ -86,6 +86,12 @@ __device__ inline double unwrap_step_f64(double dd, int* w) {
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, 63] (binary search over the
 // immediate; waiting for more than needed is always safe, so n is clamped down).
+// a sample-index bound relative to a lane's image start, clamped into int range (images
+// are < 2^16 samples): 64-bit compares per chunk would hold 64-bit registers per chunk
+__device__ __forceinline__ int rel_bound(int64_t v) {
+  return (int)max<int64_t>(min<int64_t>(v, 1 << 20), -(1 << 20));
+}
+
 template <int LO, int HI>
 __device__ __forceinline__ void wait_vm_bs(int n) {
   if constexpr (LO == HI) {
@@ -933,15 +939,15 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
   auto build_sync = [&](int ss, int64_t nl) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if constexpr (U8) {
-      // all predicated 2-B loads (one complex u8 sample each) in flight before the first use
-      const uint16_t* base = reinterpret_cast<const uint16_t*>(p.iq) + (int64_t)ss * p.stride;
+      // predicated 2-B loads (one complex u8 sample each), all in flight before the first
+      // use; one per-lane base pointer with immediate offsets and 32-bit bounds (per-chunk
+      // 64-bit addresses next to the tap registers spill to scratch)
+      const uint16_t* bp = reinterpret_cast<const uint16_t*>(p.iq) + ((int64_t)ss * p.stride + nl + lane);
+      const int lo = rel_bound(-p.hist - nl - lane), hi = rel_bound(p.n - nl - lane);
       constexpr int NPL = L / 64;
       uint32_t v[NPL];
 #pragma unroll
-      for (int j = 0; j < NPL; ++j) {
-        const int64_t nn = nl + 64 * j + lane;
-        v[j] = (nn >= -p.hist && nn < p.n) ? (uint32_t)base[nn] : 0x8080u;   // 0x80 -> 0.0
-      }
+      for (int j = 0; j < NPL; ++j) v[j] = (64 * j >= lo && 64 * j < hi) ? (uint32_t)bp[64 * j] : 0x8080u;  // 0x80 -> 0.0
 #pragma unroll
       for (int j = 0; j < NPL; ++j) slot[64 * j + lane] = f2v{cvt8(v[j] & 0xff), cvt8(v[j] >> 8)};
     } else if (interior(nl)) {
@@ -953,14 +959,12 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
         glds16x<n>(voff, g + 1024 * c, lb + 1024 * c);
       });
     } else {
-      const f2v* base = reinterpret_cast<const f2v*>(iqf) + (int64_t)ss * p.stride;
+      const f2v* bp = reinterpret_cast<const f2v*>(iqf) + ((int64_t)ss * p.stride + nl + lane);
+      const int lo = rel_bound(-p.hist - nl - lane), hi = rel_bound(p.n - nl - lane);
       constexpr int NPL = L / 64;
       f2v v[NPL];
 #pragma unroll
-      for (int j = 0; j < NPL; ++j) {
-        const int64_t nn = nl + 64 * j + lane;
-        v[j] = (nn >= -p.hist && nn < p.n) ? base[nn] : f2v{0.f, 0.f};
-      }
+      for (int j = 0; j < NPL; ++j) v[j] = (64 * j >= lo && 64 * j < hi) ? bp[64 * j] : f2v{0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < NPL; ++j) slot[64 * j + lane] = v[j];
     }

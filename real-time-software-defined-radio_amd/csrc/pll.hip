@@ -5,7 +5,10 @@
 // SURVEY §8a row a9.
 //
 // The loop is the only serial stage on the path.  It is split in two launches:
-//   1. pll_loop_kernel: one lane per stream runs the recurrence in f64,
+//   1. pll_lanes_kernel: ONE LANE PER RECURRENCE.  A launch carries a job table (the
+//      stereo pilot PLL and the RDS carrier PLL of every stream); each
+//      wave runs one job for up to 64 streams, lane = stream, so one wave advances 64
+//      independent loops at the cost of one.  Per lane, in f64:
 //        e_k   = atan2(-x_k fQ, x_k fI)                      (fmPll.py:24-27)
 //        integ += Ki e_k ; phaseEst += Kp e_k + integ         (fmPll.py:29-31)
 //        th_k  = 2 pi (freq/Fs) (trigOffset + k + 1) + phaseEst (fmPll.py:33)
@@ -16,11 +19,11 @@
 //      to atan2(-x sin th, x cos th) up to rounding (~1e-16 rad).  x == 0, NaN and
 //      the first sample of a call (whose fI, fQ come from the caller's state)
 //      take the literal sincos + atan2 form, so signed zeros behave as in Python.
-//   2. nco_kernel: fully parallel ncoOut[k+1] = cos(th_k*scale + adj),
+//      The lane also writes ncoOut[0] / ncoOutQ[0] (the carried values) before the loop.
+//   2. nco_jobs_kernel: fully parallel ncoOut[k+1] = cos(th_k*scale + adj),
 //      ncoOutQ[k+1] = sin(th_k*scale + adj) (fmPll.py:36-37).
 // All phase arithmetic is f64 (SURVEY §7 hard part 5: an fp32 NCO drifts).
 #include "sdr_launch.h"
-
 
 namespace {
 
@@ -40,28 +43,35 @@ __device__ inline double reduce_2pi(double a) {
   return r;
 }
 
-// One wave per stream.  Every lane runs the same recurrence (wave-uniform values, no
-// divergence); the inputs come from LDS in chunks of PCH samples, the next chunk's global
-// loads are in flight (in registers) while the current chunk runs, and the phases go out
-// through LDS as coalesced stores.  (A lone lane reading x[k] from global memory per step
-// waits an L2 round trip every sample.)
-constexpr int PCH = 512;
-__global__ __launch_bounds__(64) void pll_loop_kernel(const float* in, int64_t n, int64_t in_stride,
-                                                      int nstreams, PllCfg cfg, double* state,
-                                                      int64_t state_stride, double* theta,
-                                                      int64_t th_stride) {
+// Steps per group: the next group's inputs are loaded (registers) while this one runs,
+// and the group's phases leave as 16-B stores.
+constexpr int PG = 32;
+
+template <bool VEC>
+__global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
 #pragma clang fp contract(off)  // Python evaluates a*b + c with two roundings
-  const int s = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (s >= nstreams) return;
-  __shared__ alignas(16) float xs[2][PCH];
-  __shared__ double ths[PCH];
-  const float* x = in + (int64_t)s * in_stride;
-  double* st = state + (int64_t)s * state_stride;
-  double* th = theta + (int64_t)s * th_stride;
+  // one job per wave (a lane-varying job index into the kernarg table would copy the whole
+  // table to scratch); lane = stream
+  const int wpj = (P.nstreams + 63) / 64;
+  const int q = blockIdx.x / wpj;
+  const int s = (blockIdx.x - q * wpj) * 64 + threadIdx.x;
+  if (s >= P.nstreams) return;  // votes below run over the active lanes only
+  const PllJob& J = P.j[q];
+  struct {
+    const float* in; double* th; float* nco_i; float* nco_q;
+  } L{J.in + (int64_t)s * J.in_stride, J.theta + (int64_t)s * J.th_stride,
+      J.nco_i + (int64_t)s * J.out_stride, J.nco_q ? J.nco_q + (int64_t)s * J.out_stride : nullptr};
+  const PllCfg cfg = J.cfg;
+  double* st = J.state + (int64_t)s * 6;
+  const int64_t n = P.n;
   double integ = st[0], phase = st[1], fI = st[2], fQ = st[3];
   const double off = st[5];
   const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  // ncoOut[0] = the carried value; ncoOutQ[0]: the reference leaves it uninitialised
+  // (np.empty, fmPll.py:13); here sin(th_prev*scale + adj) with th_prev rebuilt from the
+  // carried state (0 at stream start), the quadrature twin of ncoOut[0].
+  L.nco_i[0] = (float)st[4];
+  if (L.nco_q) L.nco_q[0] = (float)((off > 0.0) ? sin((w * off + phase) * cfg.scale + cfg.adj) : 0.0);
   double arg = 0.0;
   // One step of model/fmPll.py:23-41.  General form: the first sample of a call uses the
   // caller's (fI, fQ) literally, and an input of 0 or NaN takes atan2 on the products.
@@ -91,68 +101,61 @@ __global__ __launch_bounds__(64) void pll_loop_kernel(const float* in, int64_t n
     base = base + 1.0;
     arg = w * base + phase;
   };
-  constexpr int PL = PCH / 64;
-  const int64_t nch = (n + PCH - 1) / PCH;
-  for (int j = 0; j < PL; ++j) {
-    const int64_t k = lane + 64 * j;
-    xs[0][lane + 64 * j] = k < n ? x[k] : 0.f;
-  }
-  __syncthreads();
-  for (int64_t c = 0; c < nch; ++c) {
-    const int buf = (int)(c & 1);
-    float pre[PL];
+  auto load_group = [&](float (&v)[PG], int64_t k0) {
+    if constexpr (VEC) {
 #pragma unroll
-    for (int j = 0; j < PL; ++j) {               // next chunk: loads in flight meanwhile
-      const int64_t k = (c + 1) * PCH + lane + 64 * j;
-      pre[j] = k < n ? x[k] : 0.f;
-    }
-    const int kn = (int)min<int64_t>(PCH, n - c * PCH);
-    const float* xc = xs[buf];
-    int kk = 0;
-    if (c == 0) {                                // the literal first sample
-      general(xc[0], 0, true);
-      if (lane == 0) ths[0] = arg;
-      kk = 1;
-    }
-    // wave vote: does the chunk hold a 0 or NaN input (the general form's other case)?
-    bool odd = false;
-#pragma unroll
-    for (int j = 0; j < PL; ++j) {
-      const int e = lane + 64 * j;
-      const float v = xc[e];
-      odd |= e < kn && !(v > 0.f || v < 0.f);
-    }
-    if (__any(odd)) {
-      for (; kk < kn; ++kk) {
-        general(xc[kk], c * PCH + kk, false);
-        if (lane == 0) ths[kk] = arg;
+      for (int i = 0; i < PG; i += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(L.in + k0 + i);
+        v[i] = f.x; v[i + 1] = f.y; v[i + 2] = f.z; v[i + 3] = f.w;
       }
     } else {
-      base = (off + (double)(c * PCH + kk - 1)) + 1.0;
-      // groups of 4: the next group's LDS reads are in flight during this group's steps
-      const int ng = (kn - kk) / 4;
-      float n0 = xc[kk], n1 = xc[kk + 1], n2 = xc[kk + 2], n3 = xc[kk + 3];  // kk+3 < PCH
-      for (int g = 0; g < ng; ++g, kk += 4) {
-        const float c0 = n0, c1 = n1, c2 = n2, c3 = n3;
-        if (g + 1 < ng) { n0 = xc[kk + 4]; n1 = xc[kk + 5]; n2 = xc[kk + 6]; n3 = xc[kk + 7]; }
-        fast(c0); const double a0 = arg;
-        fast(c1); const double a1 = arg;
-        fast(c2); const double a2 = arg;
-        fast(c3);
-        if (lane == 0) { ths[kk] = a0; ths[kk + 1] = a1; ths[kk + 2] = a2; ths[kk + 3] = arg; }
+#pragma unroll
+      for (int i = 0; i < PG; ++i) v[i] = L.in[k0 + i];
+    }
+  };
+  const int64_t ng = n / PG;
+  float cur[PG], nxt[PG];
+  if (ng > 0) load_group(cur, 0);
+  for (int64_t g = 0; g < ng; ++g) {
+    if (g + 1 < ng) load_group(nxt, (g + 1) * PG);
+    // wave vote: does any lane's group hold a 0 or NaN input (the general form's other
+    // case), or is it the call's first group (literal first sample)?
+    bool odd = g == 0;
+#pragma unroll
+    for (int i = 0; i < PG; ++i) odd |= !(cur[i] > 0.f || cur[i] < 0.f);
+    if (__any(odd)) {
+      // rare (first group of a call, zero or NaN inputs): a rolled loop over the inputs
+      // in memory, phases stored one by one (unrolled, its atan2/sincos would spill)
+      for (int i = 0; i < PG; ++i) {
+        const int64_t k = g * PG + i;
+        general(L.in[k], k, k == 0);
+        L.th[k] = arg;
       }
-      for (; kk < kn; ++kk) {
-        fast(xc[kk]);
-        if (lane == 0) ths[kk] = arg;
+    } else {
+      double thv[PG];
+      base = (off + (double)(g * PG - 1)) + 1.0;
+#pragma unroll
+      for (int i = 0; i < PG; ++i) {
+        fast(cur[i]);
+        thv[i] = arg;
+      }
+      double* tp = L.th + g * PG;
+      if constexpr (VEC) {
+#pragma unroll
+        for (int i = 0; i < PG; i += 2) *reinterpret_cast<double2*>(tp + i) = make_double2(thv[i], thv[i + 1]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < PG; ++i) tp[i] = thv[i];
       }
     }
-    __syncthreads();
-    for (int e = lane; e < kn; e += 64) th[c * PCH + e] = ths[e];
 #pragma unroll
-    for (int j = 0; j < PL; ++j) xs[buf ^ 1][lane + 64 * j] = pre[j];
-    __syncthreads();
+    for (int i = 0; i < PG; ++i) cur[i] = nxt[i];
   }
-  if (n > 0 && lane == 0) {
+  for (int64_t k = ng * PG; k < n; ++k) {      // tail (< PG samples)
+    general(L.in[k], k, k == 0);
+    L.th[k] = arg;
+  }
+  if (n > 0) {
     st[0] = integ;
     st[1] = phase;
     st[2] = cos(arg);
@@ -162,58 +165,38 @@ __global__ __launch_bounds__(64) void pll_loop_kernel(const float* in, int64_t n
   }
 }
 
-// nco[0] = carried ncoOut (state[4] before the call, passed as nco0[s]); nco[k+1] from th_k.
-// ncoQ[0]: the reference leaves it uninitialised (np.empty, fmPll.py:13); here it is
-// sin(th_prev*scale + adj) with th_prev rebuilt from the carried state (0 at stream start),
-// the quadrature twin of ncoOut[0] (documented deviation).
-__global__ void nco_kernel(const double* theta, int64_t th_stride, int64_t n, int nstreams,
-                           PllCfg cfg, const double* nco0, const double* ncoq0, float* nco_i,
-                           float* nco_q, int64_t out_stride) {
+// nco[k+1] from th_k for every (job, stream) of the table; nco[0] is the loop kernel's.
+__global__ void nco_jobs_kernel(PllJobs P) {
 #pragma clang fp contract(off)
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int s = blockIdx.y;
-  if (s >= nstreams || gid > n) return;
-  float* oi = nco_i + (int64_t)s * out_stride;
-  float* oq = nco_q ? nco_q + (int64_t)s * out_stride : nullptr;
-  if (gid == 0) {
-    oi[0] = (float)nco0[s];
-    if (oq) oq[0] = (float)ncoq0[s];
-    return;
-  }
-  const double a = theta[(int64_t)s * th_stride + gid - 1] * cfg.scale + cfg.adj;
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= P.n) return;
+  const int g = blockIdx.y;                 // uniform: (job, stream)
+  const int q = g / P.nstreams;
+  const int s = g - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const double a = J.theta[(int64_t)s * J.th_stride + k] * J.cfg.scale + J.cfg.adj;
   double sv, cv;
   sincos(a, &sv, &cv);
-  oi[gid] = (float)cv;
-  if (oq) oq[gid] = (float)sv;
-}
-
-// Before the loop: remember ncoOut[0] and build ncoOutQ[0] from the incoming state.
-__global__ void nco_prologue_kernel(const double* state, int64_t state_stride, int nstreams,
-                                    PllCfg cfg, double* nco0, double* ncoq0) {
-#pragma clang fp contract(off)
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nstreams) return;
-  const double* st = state + (int64_t)s * state_stride;
-  nco0[s] = st[4];
-  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
-  ncoq0[s] = (st[5] > 0.0) ? sin((w * st[5] + st[1]) * cfg.scale + cfg.adj) : 0.0;
+  J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
+  if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
 }
 
 }  // namespace
 
-// scratch: theta (n per stream, th_stride), nco0/ncoq0 (nstreams each).
-hipError_t sdr_launch_pll(const float* in, int64_t n, int64_t in_stride, int nstreams,
-                          const PllCfg& cfg, double* state_dev, double* theta, int64_t th_stride,
-                          double* nco0, double* ncoq0, float* nco_i, float* nco_q,
-                          int64_t out_stride, hipStream_t st) {
-  if (nstreams <= 0) return hipSuccess;
-  const int nb = (nstreams + 63) / 64;
-  hipLaunchKernelGGL(nco_prologue_kernel, dim3(nb), dim3(64), 0, st, state_dev, (int64_t)6,
-                     nstreams, cfg, nco0, ncoq0);
-  hipLaunchKernelGGL(pll_loop_kernel, dim3(nstreams), dim3(64), 0, st, in, n, in_stride, nstreams, cfg,
-                     state_dev, (int64_t)6, theta, th_stride);
-  const int64_t nout = n + 1;
-  hipLaunchKernelGGL(nco_kernel, dim3((unsigned)((nout + 255) / 256), nstreams), dim3(256), 0, st,
-                     theta, th_stride, n, nstreams, cfg, nco0, ncoq0, nco_i, nco_q, out_stride);
+hipError_t sdr_launch_pll_jobs(const PllJobs& P, hipStream_t st) {
+  if (P.njobs < 1 || P.njobs > SDR_PLL_MAXJ || P.nstreams <= 0 || P.n < 0) return hipErrorInvalidValue;
+  // 16-B loads/stores need every lane's input row and phase row 16-B aligned
+  bool vec = true;
+  for (int q = 0; q < P.njobs; ++q) {
+    const PllJob& J = P.j[q];
+    vec = vec && ((uintptr_t)J.in % 16) == 0 && (J.in_stride % 4) == 0 && ((uintptr_t)J.theta % 16) == 0 &&
+          (J.th_stride % 2) == 0;
+  }
+  const int lanes = P.njobs * P.nstreams;
+  const dim3 grid((unsigned)(P.njobs * ((P.nstreams + 63) / 64)));
+  if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, P);
+  else hipLaunchKernelGGL(pll_lanes_kernel<false>, grid, dim3(64), 0, st, P);
+  if (P.n > 0)
+    hipLaunchKernelGGL(nco_jobs_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)lanes), dim3(256), 0, st, P);
   return hipGetLastError();
 }

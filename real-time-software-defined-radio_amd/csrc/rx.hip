@@ -1,0 +1,723 @@
+// Multi-stream block receiver (sdr_rx_*): the per-block loops of model/fmMonoBlock.py:80-173
+// (mono + stereo) and model/fmRDSblock.py:127-204 (RDS up to the RRC output) for S
+// independent streams at once, every state and intermediate resident in HBM.  This is
+// SURVEY §8a C5 (8 streams, mono + stereo + RDS, B = 153 600, src/fm_radio.cpp:783-792 runs
+// the same stages as four threads per stream) and the per-block drop-in path of C3/C4.
+//
+// One block of all S streams is a fixed chain of launches on the context stream:
+//   FE        RF FIR + decimate + atan2 demod (fe.hip; zf and demod state included)
+//   stage A   every filter that reads demod: mono LPF (decim 5), pilot BPF, stereo BPF,
+//             RDS extract BPF -- one launch, one job table (rx_stage_kernel)
+//   stage B   RDS square + BPF (model/fmRDSblock.py:161-164)
+//   PLL       stereo pilot PLL and RDS carrier PLL of every stream: one lane per
+//             recurrence (pll.hip), then the NCO outputs
+//   stage C   stereo mixer + LPF + decimate with the L/R combiner fused into its store;
+//             RDS I and Q mixers + 3 kHz LPF
+//   stage D   RDS rational resamplers (x19 zero-stuff, anti-image LPF, [::80] x19), I and Q
+//   stage E   RDS RRC filters, I and Q
+// Every stage launch also carries its filters' lfilter final states: extra workgroups after
+// the output tiles compute zf (f64) from the block's last inputs.  zi and
+// zf live in two state banks that swap every block, so no zf write races a zi read.
+// Launches per block: 1 FE (+ its zf / phase kernels) + up to 5 stages + 2 PLL = 10 at
+// full C5, whatever S is.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "sdr_ctx.h"
+
+using namespace sdrint;
+
+namespace {
+
+constexpr int RX_MAXJ = 6;          // jobs per stage launch
+constexpr int RX_NT = 128;          // threads per workgroup
+constexpr int RX_R = 4;             // outputs per thread
+constexpr int RX_TO = RX_NT * RX_R;  // outputs per tile
+constexpr int RX_LDS = 3072;        // floats of LDS per workgroup (largest: 151 taps, decim 5)
+
+enum { JK_FIR = 0, JK_RESAMPLE = 1 };
+enum { PRE_NONE = SDR_PRE_NONE, PRE_SQUARE = SDR_PRE_SQUARE, PRE_MIX = SDR_PRE_MIX };
+
+// One filter of a stage, applied to `nstreams` streams.
+struct StageJob {
+  const float* x;        // input rows, x_stride apart
+  const float* c;        // PRE_MIX second operand (same indexing as x)
+  const float* taps;     // f32 taps (device)
+  const double* taps64;  // f64 taps (device, for zf)
+  const double* zi;      // lfilter state in (T-1 per stream, zi_stride apart), nullable
+  double* zf;            // lfilter state out (same layout), nullable
+  float* y;              // outputs, y_stride apart
+  const float* mono;     // combiner: mono audio rows (y_stride apart), or null
+  float* left;
+  float* right;
+  int64_t n, x_stride, zi_stride, y_stride;
+  int64_t b0;            // first workgroup of this job's tiles
+  float gain;
+  int pre, D, U, kind, T, tiles;
+};
+
+struct StageJobs {
+  StageJob j[RX_MAXJ];
+  int njobs, nstreams;
+  int64_t tile_blocks;        // workgroups [0, tile_blocks) compute outputs
+  int zfj[RX_MAXJ], nzf;      // then nzf * nstreams workgroups compute final states
+};
+
+__device__ __forceinline__ float pre_op(int pre, float x, float c, float g) {
+  return pre == PRE_SQUARE ? x * x : pre == PRE_MIX ? (x * c) * g : x;
+}
+
+// The lfilter FIR tile (compile-time T and D): thread t owns R consecutive outputs and slides
+// once over its D(R-1)+T window in LDS; rows padded by one float every D*R samples so the
+// per-lane stride is odd (conflict-free ds_read_b32).  Taps are read through the job's
+// uniform pointer with compile-time indices (scalar loads, SGPR operands).
+template <int T, int D>
+struct FirShape {
+  static constexpr int G = 4, NT = RX_NT, R = RX_R, TO = RX_TO, DR = D * R;
+  static constexpr bool PAD = (DR % 2) == 0;
+  static constexpr int SR = PAD ? DR + 1 : DR;
+  static constexpr int DELTA = (G - ((T - 1) % G)) % G;
+  static constexpr int L = ((D * (TO - 1) + T + DELTA) + G - 1) / G * G;
+  static constexpr int NSLOT = PAD ? L + (L + DR - DELTA) / DR + 1 : L;
+  static constexpr int NCHUNK = L / G;
+  static constexpr int NLOAD = (NCHUNK + NT - 1) / NT;
+  static constexpr int NI = D * (R - 1) + T;
+  static_assert((D * TO) % G == 0, "tile start must stay G-aligned");
+  static_assert(NSLOT <= RX_LDS, "tile image fits the stage LDS");
+};
+
+template <int T, int D>
+__device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile, float* lds) {
+  using S = FirShape<T, D>;
+  constexpr int R = S::R, DR = S::DR, DELTA = S::DELTA, L = S::L;
+  constexpr bool PAD = S::PAD;
+  const int t = threadIdx.x;
+  const int64_t m0 = tile * S::TO;
+  const int64_t M = (J.n + D - 1) / D;
+  const int64_t n_lo = D * m0 - (T - 1) - DELTA;
+  const float* xb = J.x + (int64_t)s * J.x_stride;
+  const float* cb = J.c ? J.c + (int64_t)s * J.x_stride : nullptr;
+  const int pre = J.pre;
+  const float g = J.gain;
+  auto slot = [](int e) { return PAD ? e + (e + DR - DELTA) / DR : e; };
+  if (n_lo >= 0 && n_lo + L <= J.n) {               // interior: 16-B loads (rows are aligned)
+    float4 v[S::NLOAD], cv[S::NLOAD];
+#pragma unroll
+    for (int j = 0; j < S::NLOAD; ++j) {
+      const int q = t + j * S::NT;
+      if (q < S::NCHUNK) {
+        v[j] = reinterpret_cast<const float4*>(xb + n_lo)[q];
+        cv[j] = pre == PRE_MIX ? reinterpret_cast<const float4*>(cb + n_lo)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < S::NLOAD; ++j) {
+      const int q = t + j * S::NT;
+      if (q < S::NCHUNK) {
+        const int e = q * S::G;
+        lds[slot(e + 0)] = pre_op(pre, v[j].x, cv[j].x, g);
+        lds[slot(e + 1)] = pre_op(pre, v[j].y, cv[j].y, g);
+        lds[slot(e + 2)] = pre_op(pre, v[j].z, cv[j].z, g);
+        lds[slot(e + 3)] = pre_op(pre, v[j].w, cv[j].w, g);
+      }
+    }
+  } else {
+    for (int e = t; e < L; e += S::NT) {
+      const int64_t nn = n_lo + e;
+      float x = 0.f;
+      if (nn >= 0 && nn < J.n) x = pre_op(pre, xb[nn], pre == PRE_MIX ? cb[nn] : 0.f, g);
+      lds[slot(e)] = x;
+    }
+  }
+  __syncthreads();
+  const float* h = J.taps;
+  const float* win = lds + (PAD ? (DELTA + 1 + S::SR * t) : (DELTA + DR * t));
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < S::NI; ++i) {
+    const float x = win[PAD ? i + i / DR : i];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int k = D * r + T - 1 - i;
+      if (k >= 0 && k < T) acc[r] = fmaf(h[k], x, acc[r]);
+    }
+  }
+  const int64_t mf = m0 + (int64_t)t * R;
+  if (J.zi != nullptr) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t nn = D * (mf + r);
+      if (nn < T - 1) acc[r] += (float)J.zi[(int64_t)s * J.zi_stride + nn];
+    }
+  }
+  float* yb = J.y + (int64_t)s * J.y_stride;
+  if (mf + R <= M) {
+    *reinterpret_cast<float4*>(yb + mf) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (mf + r < M) yb[mf + r] = acc[r];
+  }
+  if (J.mono != nullptr) {                           // stereo combiner (fmMonoBlock.py:166-170)
+    const float* mb = J.mono + (int64_t)s * J.y_stride;
+    float* lb = J.left + (int64_t)s * J.y_stride;
+    float* rb = J.right + (int64_t)s * J.y_stride;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (mf + r < M) {
+        const float a = mb[mf + r];
+        lb[mf + r] = (a + acc[r]) * 0.5f;
+        rb[mf + r] = (a - acc[r]) * 0.5f;
+      }
+    }
+  }
+}
+
+// Any T (<= SDR_MAX_TAPS) and D: taps in LDS, inputs through the caches; outputs
+// m0 + t + NT*r.  Also the combiner when asked.
+__device__ __forceinline__ void fir_tile_any(const StageJob& J, int s, int64_t tile, float* lds) {
+  const int t = threadIdx.x;
+  for (int k = t; k < J.T; k += RX_NT) lds[k] = J.taps[k];
+  __syncthreads();
+  const int64_t M = (J.n + J.D - 1) / J.D;
+  const float* xb = J.x + (int64_t)s * J.x_stride;
+  const float* cb = J.c ? J.c + (int64_t)s * J.x_stride : nullptr;
+  for (int r = 0; r < RX_R; ++r) {
+    const int64_t m = tile * RX_TO + t + RX_NT * r;
+    if (m >= M) break;
+    const int64_t j0 = (int64_t)J.D * m;
+    float acc = 0.f;
+    const int khi = (int)min<int64_t>(J.T - 1, j0);
+    for (int k = khi; k >= 0; --k)
+      acc = fmaf(lds[k], pre_op(J.pre, xb[j0 - k], J.pre == PRE_MIX ? cb[j0 - k] : 0.f, J.gain), acc);
+    if (J.zi != nullptr && j0 < J.T - 1) acc += (float)J.zi[(int64_t)s * J.zi_stride + j0];
+    J.y[(int64_t)s * J.y_stride + m] = acc;
+    if (J.mono != nullptr) {
+      const float a = J.mono[(int64_t)s * J.y_stride + m];
+      J.left[(int64_t)s * J.y_stride + m] = (a + acc) * 0.5f;
+      J.right[(int64_t)s * J.y_stride + m] = (a - acc) * 0.5f;
+    }
+  }
+}
+
+// Rational resampler (model/fmRDSblock.py:184-199): lfilter on the x U zero-stuffed stream,
+// [::D], times U, without materialising the zero-stuffed stream (only the taps with
+// (D m - k) % U == 0 contribute; the input index walks down by one per term).
+__device__ __forceinline__ void resample_tile(const StageJob& J, int s, int64_t tile, float* lds) {
+  const int t = threadIdx.x;
+  for (int k = t; k < J.T; k += RX_NT) lds[k] = J.taps[k];
+  __syncthreads();
+  const int U = J.U, D = J.D;
+  const int64_t M = (J.n * U + D - 1) / D;
+  const float* xb = J.x + (int64_t)s * J.x_stride;
+  for (int r = 0; r < RX_R; ++r) {
+    const int64_t m = tile * RX_TO + t + RX_NT * r;
+    if (m >= M) break;
+    const int64_t j0 = (int64_t)D * m;
+    const int k0 = (int)(j0 % U);
+    const int khi = (int)min<int64_t>(J.T - 1, j0);
+    int64_t xi = (j0 - k0) / U;
+    float acc = 0.f;
+    for (int k = k0; k <= khi; k += U, --xi) acc = fmaf(lds[k], xb[xi], acc);
+    if (J.zi != nullptr && j0 < J.T - 1) acc += (float)J.zi[(int64_t)s * J.zi_stride + j0];
+    J.y[(int64_t)s * J.y_stride + m] = acc * (float)U;
+  }
+}
+
+// lfilter final state of one (job, stream), f64, on the (zero-stuffed when U > 1) input:
+//   zf[k] = sum_{j=k+1}^{T-1} b[j] u[NU+k-j] + (NU+k < T-1 ? zi[NU+k] : 0),  NU = n*U
+// (the zf_kernel of fir.hip as extra workgroups of the producing stage).
+__device__ __forceinline__ void zf_block(const StageJobs& P, int64_t zb, float* lds) {
+  const int q = P.zfj[zb / P.nstreams];
+  const int s = (int)(zb % P.nstreams);
+  const StageJob& J = P.j[q];
+  const int U = J.kind == JK_RESAMPLE ? J.U : 1;
+  const int T = J.T;
+  const float* x = J.x + (int64_t)s * J.x_stride;
+  const float* c = J.c ? J.c + (int64_t)s * J.x_stride : nullptr;
+  const double* zi = J.zi ? J.zi + (int64_t)s * J.zi_stride : nullptr;
+  double* zf = J.zf + (int64_t)s * J.zi_stride;
+  const int64_t n = J.n, nu = n * U;
+  const int L = (int)min<int64_t>(n, (T - 1) / U);
+  double* bs = reinterpret_cast<double*>(lds);
+  double* us = bs + T;
+  for (int i = threadIdx.x; i < L; i += RX_NT) {
+    const int64_t xi = n - 1 - i;
+    double v = (double)x[xi];
+    if (J.pre == PRE_SQUARE) v = v * v;
+    else if (J.pre == PRE_MIX) v = (double)((x[xi] * c[xi]) * J.gain);
+    us[i] = v;
+  }
+  for (int i = threadIdx.x; i < T; i += RX_NT) bs[i] = J.taps64[i];
+  __syncthreads();
+  for (int k = threadIdx.x; k < T - 1; k += RX_NT) {
+    const int jhi = (int)min<int64_t>(T - 1, nu + k);
+    double acc = 0.0;
+    int i = 0;
+    for (int j = k + U; j <= jhi; j += U, ++i) acc = fma(bs[j], us[i], acc);
+    if (zi != nullptr && nu + k < T - 1) acc += zi[nu + k];
+    zf[k] = acc;
+  }
+}
+
+// One stage launch.  T > 0: every FIR job of the launch has T taps (compile-time tiles for
+// D = 1 and 5); T == 0: any tap count.  Workgroups map to (job, stream, tile) in job order,
+// then to the zf work.
+template <int T>
+__global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
+  __shared__ __attribute__((aligned(16))) float lds[RX_LDS];
+  const int64_t b = blockIdx.x;
+  if (b >= P.tile_blocks) {
+    zf_block(P, b - P.tile_blocks, lds);
+    return;
+  }
+  int q = 0;
+  for (int i = 1; i < P.njobs; ++i)
+    if (b >= P.j[i].b0) q = i;
+  const StageJob& J = P.j[q];
+  const int64_t bl = b - J.b0;
+  const int s = (int)(bl / J.tiles);
+  const int64_t tile = bl - (int64_t)s * J.tiles;
+  if (J.kind == JK_RESAMPLE) {
+    resample_tile(J, s, tile, lds);
+    return;
+  }
+  if constexpr (T > 0) {
+    if (J.D == 1) { fir_tile<T, 1>(J, s, tile, lds); return; }
+    if (J.D == 5) { fir_tile<T, 5>(J, s, tile, lds); return; }
+  }
+  fir_tile_any(J, s, tile, lds);
+}
+
+// Launch the jobs of one stage, one launch per tap-count class.
+hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st) {
+  auto cls = [](const StageJob& j) { return (j.kind == JK_FIR && (j.T == 101 || j.T == 151)) ? j.T : 0; };
+  for (int key : {151, 101, 0}) {
+    StageJobs P{};
+    P.nstreams = S;
+    int64_t blocks = 0;
+    for (const StageJob& j0 : jobs) {
+      if (cls(j0) != key) continue;
+      if (P.njobs == RX_MAXJ) return hipErrorInvalidValue;
+      StageJob j = j0;
+      const int64_t nout = j.kind == JK_RESAMPLE ? (j.n * j.U + j.D - 1) / j.D : (j.n + j.D - 1) / j.D;
+      j.tiles = (int)std::max<int64_t>((nout + RX_TO - 1) / RX_TO, 0);
+      j.b0 = blocks;
+      blocks += (int64_t)j.tiles * S;
+      if (j.zf != nullptr && j.T > 1) P.zfj[P.nzf++] = P.njobs;
+      P.j[P.njobs++] = j;
+    }
+    if (P.njobs == 0) continue;
+    P.tile_blocks = blocks;
+    const int64_t grid = blocks + (int64_t)P.nzf * S;
+    if (grid <= 0) continue;
+    if (grid > 0x7fffffff) return hipErrorInvalidValue;
+    if (key == 151) hipLaunchKernelGGL(rx_stage_kernel<151>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
+    else if (key == 101) hipLaunchKernelGGL(rx_stage_kernel<101>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
+    else hipLaunchKernelGGL(rx_stage_kernel<0>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// state-bank slots (f64 lfilter states, T-1 per stream each)
+enum Zs {
+  Z_FE_I, Z_FE_Q, Z_AUDIO, Z_PILOT, Z_BAND, Z_EXTRACT, Z_SQUARE, Z_SLPF, Z_RLPF_I, Z_RLPF_Q,
+  Z_ANTI_I, Z_ANTI_Q, Z_RRC_I, Z_RRC_Q, Z_N
+};
+
+int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+}  // namespace
+
+struct sdr_rx {
+  sdr_ctx* c = nullptr;
+  int S = 0;
+  int64_t B = 0;
+  int u8 = 0, flags = 0;
+  int rf_decim = 10, audio_decim = 5, rds_up = 19, rds_down = 80;
+  std::vector<double> taps[SDR_RX_NFILTERS];
+  PllCfg pll[2] = {};
+  bool ready = false;
+  int64_t M = 0, A = 0, R = 0;
+  float* out[SDR_RX_NOUTPUTS] = {};
+  int64_t out_n[SDR_RX_NOUTPUTS] = {}, out_stride[SDR_RX_NOUTPUTS] = {};
+  void* mem = nullptr;                 // one allocation for outputs, states and phases
+  double* bank[2] = {};
+  int64_t zoff[Z_N] = {}, zlen[Z_N] = {};
+  int64_t bank_len = 0;
+  double* phase = nullptr;             // demod prev_phase per stream
+  double* pll_state[2] = {};           // 6 per stream (stereo, RDS)
+  double* theta = nullptr;             // PLL phases: 2 x S rows of ths
+  int64_t ths = 0;
+  void* iq_dev = nullptr;              // host-path upload buffer
+  size_t iq_cap = 0;
+  int parity = 0;
+  int64_t blocks = 0;
+};
+
+namespace {
+
+PllCfg pll_cfg(double freq, double fs, double scale, double adj, double bw) {
+  return PllCfg{freq, fs, scale, adj, bw * 2.666, bw * bw * 3.555};   // model/fmPll.py:7-10
+}
+
+bool need_out(const sdr_rx* r, int o) {
+  const bool au = r->flags & (SDR_RX_AUDIO | SDR_RX_STEREO), st = r->flags & SDR_RX_STEREO,
+             rd = r->flags & SDR_RX_RDS;
+  switch (o) {
+    case SDR_RX_O_DEMOD: return true;
+    case SDR_RX_O_AUDIO: return au;
+    case SDR_RX_O_BPF_RECOVERY: case SDR_RX_O_STEREO_NCO: case SDR_RX_O_BPF_EXTRACTION:
+    case SDR_RX_O_STEREO: case SDR_RX_O_LEFT: case SDR_RX_O_RIGHT: return st;
+    default: return rd;
+  }
+}
+
+int filter_of_zs(int z) {
+  switch (z) {
+    case Z_FE_I: case Z_FE_Q: return SDR_RX_F_RF;
+    case Z_AUDIO: return SDR_RX_F_AUDIO;
+    case Z_PILOT: return SDR_RX_F_PILOT;
+    case Z_BAND: return SDR_RX_F_STEREO_BPF;
+    case Z_EXTRACT: return SDR_RX_F_RDS_EXTRACT;
+    case Z_SQUARE: return SDR_RX_F_RDS_SQUARE;
+    case Z_SLPF: return SDR_RX_F_STEREO_LPF;
+    case Z_RLPF_I: case Z_RLPF_Q: return SDR_RX_F_RDS_LPF;
+    case Z_ANTI_I: case Z_ANTI_Q: return SDR_RX_F_RDS_ANTI;
+    default: return SDR_RX_F_RDS_RRC;
+  }
+}
+
+bool filter_used(const sdr_rx* r, int f) {
+  const bool au = r->flags & (SDR_RX_AUDIO | SDR_RX_STEREO), st = r->flags & SDR_RX_STEREO,
+             rd = r->flags & SDR_RX_RDS;
+  switch (f) {
+    case SDR_RX_F_RF: return true;
+    case SDR_RX_F_AUDIO: return au;
+    case SDR_RX_F_PILOT: case SDR_RX_F_STEREO_BPF: case SDR_RX_F_STEREO_LPF: return st;
+    default: return rd;
+  }
+}
+
+const char* kFilterName[SDR_RX_NFILTERS] = {"rf", "audio", "pilot", "stereo_bpf", "stereo_lpf",
+                                            "rds_extract", "rds_square", "rds_lpf", "rds_anti", "rds_rrc"};
+
+// Allocate and zero everything once the configuration is known (first block).
+int rx_finalize(sdr_rx* r) {
+  for (int f = 0; f < SDR_RX_NFILTERS; ++f)
+    if (filter_used(r, f) && r->taps[f].empty())
+      return fail(SDR_EINVAL, "sdr_rx: the %s filter taps are not set", kFilterName[f]);
+  const int64_t M = ceil_div(r->B, r->rf_decim);
+  r->M = M;
+  r->A = ceil_div(M, r->audio_decim);
+  r->R = ceil_div(M * r->rds_up, r->rds_down);
+  const int64_t ms = round_up(M + 1, 64), as = round_up(r->A, 64), rs = round_up(r->R, 64);
+  const int64_t S = r->S;
+  int64_t floats = 0;
+  for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) {
+    if (!need_out(r, o)) continue;
+    int64_t n, st;
+    switch (o) {
+      case SDR_RX_O_AUDIO: case SDR_RX_O_STEREO: case SDR_RX_O_LEFT: case SDR_RX_O_RIGHT:
+        n = r->A; st = as; break;
+      case SDR_RX_O_STEREO_NCO: case SDR_RX_O_RDS_NCO_I: case SDR_RX_O_RDS_NCO_Q:
+        n = M + 1; st = ms; break;
+      case SDR_RX_O_RDS_RES_I: case SDR_RX_O_RDS_RES_Q: case SDR_RX_O_RDS_RRC_I: case SDR_RX_O_RDS_RRC_Q:
+        n = r->R; st = rs; break;
+      default: n = M; st = ms; break;
+    }
+    r->out_n[o] = n;
+    r->out_stride[o] = st;
+    r->out[o] = reinterpret_cast<float*>((intptr_t)floats);   // offset for now
+    floats += st * S + 64;
+  }
+  int64_t zl = 0;
+  for (int z = 0; z < Z_N; ++z) {
+    const int f = filter_of_zs(z);
+    if (!filter_used(r, f)) continue;
+    r->zoff[z] = zl;
+    r->zlen[z] = std::max<int64_t>((int64_t)r->taps[f].size() - 1, 1);
+    zl += round_up(r->zlen[z] * S, 2);
+  }
+  r->bank_len = zl;
+  r->ths = round_up(M, 2) + 2;
+  const int64_t S2 = round_up(S, 2);                 // keeps the phase rows 16-B aligned
+  const int64_t doubles = 2 * zl + S2 + 2 * 6 * S2 + 2 * S * r->ths;
+  const size_t bytes = (size_t)floats * 4 + 64 + (size_t)doubles * 8;
+  TRY(set_dev(r->c));
+  hipError_t e = hipMalloc(&r->mem, bytes);
+  if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx: hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  char* base = static_cast<char*>(r->mem);
+  for (int o = 0; o < SDR_RX_NOUTPUTS; ++o)
+    if (need_out(r, o)) r->out[o] = reinterpret_cast<float*>(base) + (intptr_t)r->out[o];
+  double* d = reinterpret_cast<double*>(base + round_up(floats * 4, 64));
+  r->bank[0] = d;
+  r->bank[1] = d + zl;
+  r->phase = d + 2 * zl;
+  r->pll_state[0] = r->phase + S2;
+  r->pll_state[1] = r->pll_state[0] + 6 * S2;
+  r->theta = r->pll_state[1] + 6 * S2;
+  r->ready = true;
+  return sdr_rx_reset(r);
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdr_rx_create(sdr_ctx* c, int nstreams, int64_t block, int iq_dtype, int flags, sdr_rx** out) {
+  CHECK_CTX(c);
+  if (out == nullptr) return fail(SDR_EINVAL, "sdr_rx_create: out is NULL");
+  *out = nullptr;
+  if (nstreams < 1 || block < 1) return fail(SDR_EINVAL, "sdr_rx_create: nstreams %d, block %lld", nstreams, (long long)block);
+  if (iq_dtype != SDR_IQ_F32 && iq_dtype != SDR_IQ_U8) return fail(SDR_EINVAL, "sdr_rx_create: iq_dtype %d", iq_dtype);
+  if (flags & ~(SDR_RX_AUDIO | SDR_RX_STEREO | SDR_RX_RDS)) return fail(SDR_EINVAL, "sdr_rx_create: flags 0x%x", flags);
+  sdr_rx* r = new (std::nothrow) sdr_rx();
+  if (!r) return fail(SDR_ENOMEM, "sdr_rx_create: out of memory");
+  r->c = c;
+  r->S = nstreams;
+  r->B = block;
+  r->u8 = iq_dtype == SDR_IQ_U8;
+  r->flags = flags;
+  // model/fmMonoBlock.py:119 (19 kHz, x2, BW 0.01); model/fmRDSblock.py:167 (114 kHz, x0.5)
+  r->pll[0] = pll_cfg(19e3, 240e3, 2.0, 0.0, 0.01);
+  r->pll[1] = pll_cfg(114e3, 240e3, 0.5, M_PI / 3.3 - M_PI / 1.5, 0.001);
+  *out = r;
+  return SDR_OK;
+}
+
+void sdr_rx_destroy(sdr_rx* r) {
+  if (r == nullptr) return;
+  if (r->c) {
+    (void)hipSetDevice(r->c->device);
+    (void)hipStreamSynchronize(r->c->stream);
+  }
+  if (r->mem) (void)hipFree(r->mem);
+  if (r->iq_dev) (void)hipFree(r->iq_dev);
+  delete r;
+}
+
+int sdr_rx_set_filter(sdr_rx* r, int which, const double* b, int taps) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (r->ready) return fail(SDR_EINVAL, "sdr_rx_set_filter: the receiver has processed a block");
+  if (which < 0 || which >= SDR_RX_NFILTERS) return fail(SDR_EINVAL, "sdr_rx_set_filter: filter %d", which);
+  if (b == nullptr || taps < 1 || taps > SDR_MAX_TAPS)
+    return fail(SDR_EINVAL, "sdr_rx_set_filter: taps=%d outside [1, %d]", taps, SDR_MAX_TAPS);
+  r->taps[which].assign(b, b + taps);
+  return SDR_OK;
+}
+
+int sdr_rx_set_decim(sdr_rx* r, int rf_decim, int audio_decim, int rds_up, int rds_down) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (r->ready) return fail(SDR_EINVAL, "sdr_rx_set_decim: the receiver has processed a block");
+  if (rf_decim < 1 || audio_decim < 1 || rds_up < 1 || rds_down < 1) return fail(SDR_EINVAL, "sdr_rx_set_decim: factor < 1");
+  r->rf_decim = rf_decim;
+  r->audio_decim = audio_decim;
+  r->rds_up = rds_up;
+  r->rds_down = rds_down;
+  return SDR_OK;
+}
+
+int sdr_rx_set_pll(sdr_rx* r, int which, double freq, double fs, double nco_scale, double phase_adj,
+                   double norm_bw) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (which != 0 && which != 1) return fail(SDR_EINVAL, "sdr_rx_set_pll: which=%d (0 stereo, 1 RDS)", which);
+  if (!(fs != 0.0)) return fail(SDR_EINVAL, "sdr_rx_set_pll: Fs must be non-zero");
+  r->pll[which] = pll_cfg(freq, fs, nco_scale, phase_adj, norm_bw);
+  return SDR_OK;
+}
+
+int sdr_rx_reset(sdr_rx* r) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (!r->ready) return SDR_OK;   // nothing allocated yet: the first block starts from zero
+  TRY(set_dev(r->c));
+  hipStream_t st = r->c->stream;
+  HIP_TRY(hipMemsetAsync(r->bank[0], 0, sizeof(double) * (size_t)(2 * r->bank_len + r->S), st));
+  std::vector<double> ps(6 * (size_t)r->S);
+  for (int s = 0; s < r->S; ++s) {               // model/fmMonoBlock.py:76, model/fmRDSblock.py:96
+    const double init[6] = {0.0, 0.0, 1.0, 0.0, 1.0, 0.0};
+    std::memcpy(&ps[6 * (size_t)s], init, sizeof init);
+  }
+  HIP_TRY(hipMemcpyAsync(r->pll_state[0], ps.data(), sizeof(double) * ps.size(), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(r->pll_state[1], ps.data(), sizeof(double) * ps.size(), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  r->parity = 0;
+  r->blocks = 0;
+  return SDR_OK;
+}
+
+int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (iq == nullptr) return fail(SDR_EINVAL, "sdr_rx_process_dev: iq is NULL");
+  if (r->S > 1 && iq_stride < r->B) return fail(SDR_EINVAL, "sdr_rx_process_dev: iq_stride %lld < block", (long long)iq_stride);
+  if (!r->ready) TRY(rx_finalize(r));
+  sdr_ctx* c = r->c;
+  TRY(set_dev(c));
+  hipStream_t st = c->stream;
+  const int S = r->S;
+  const int64_t M = r->M;
+  double* zi = r->bank[r->parity];
+  double* zf = r->bank[r->parity ^ 1];
+  auto zin = [&](int z) { return zi + r->zoff[z]; };
+  auto zout = [&](int z) { return zf + r->zoff[z]; };
+  // device taps (cached per context; the pointers stay valid for this call)
+  const TapSet* ts[SDR_RX_NFILTERS] = {};
+  for (int f = 0; f < SDR_RX_NFILTERS; ++f)
+    if (filter_used(r, f)) TRY(get_taps(c, r->taps[f].data(), (int)r->taps[f].size(), &ts[f]));
+  float** o = r->out;
+  const int64_t ms = r->out_stride[SDR_RX_O_DEMOD];
+  // FE: RF FIR + decimate + demod, carried zi/zf and phase (fe.hip)
+  const int Trf = (int)r->taps[SDR_RX_F_RF].size();
+  TRY(sdr_rf_frontend_dev(c, iq, r->u8 ? SDR_IQ_U8 : SDR_IQ_F32, r->B, S > 1 ? iq_stride : r->B, 0, S,
+                          r->taps[SDR_RX_F_RF].data(), Trf, r->rf_decim, zin(Z_FE_I), zin(Z_FE_Q), r->zlen[Z_FE_I],
+                          zout(Z_FE_I), zout(Z_FE_Q), r->phase, o[SDR_RX_O_DEMOD], ms, nullptr, nullptr));
+  auto fir = [&](int f, int z, const float* x, int64_t n, int64_t xs, float* y, int64_t ys, int D, int pre = PRE_NONE,
+                 const float* cmix = nullptr) {
+    StageJob j{};
+    j.x = x; j.c = cmix; j.taps = ts[f]->dev_f32; j.taps64 = ts[f]->dev_f64;
+    j.zi = zin(z); j.zf = zout(z); j.zi_stride = r->zlen[z];
+    j.y = y; j.y_stride = ys; j.n = n; j.x_stride = xs;
+    j.gain = 2.0f;                      // the reference's mixer gain (fmMonoBlock.py:156, fmRDSblock.py:173)
+    j.pre = pre; j.D = D; j.U = 1; j.kind = JK_FIR; j.T = (int)r->taps[f].size();
+    return j;
+  };
+  const bool au = r->flags & (SDR_RX_AUDIO | SDR_RX_STEREO), stx = r->flags & SDR_RX_STEREO,
+             rd = r->flags & SDR_RX_RDS;
+  const int64_t as = au ? r->out_stride[SDR_RX_O_AUDIO] : 0;
+  // stage A: every filter of the demodulated signal (model/fmMonoBlock.py:101-105, :117,
+  // :151; model/fmRDSblock.py:156)
+  std::vector<StageJob> A;
+  if (au) A.push_back(fir(SDR_RX_F_AUDIO, Z_AUDIO, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_AUDIO], as, r->audio_decim));
+  if (stx) {
+    A.push_back(fir(SDR_RX_F_PILOT, Z_PILOT, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_BPF_RECOVERY], ms, 1));
+    A.push_back(fir(SDR_RX_F_STEREO_BPF, Z_BAND, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_BPF_EXTRACTION], ms, 1));
+  }
+  if (rd) A.push_back(fir(SDR_RX_F_RDS_EXTRACT, Z_EXTRACT, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_RDS_EXTRACT], ms, 1));
+  HIP_TRY(launch_stage(A, S, st));
+  // stage B: RDS squaring non-linearity + BPF (model/fmRDSblock.py:161-164)
+  if (rd) HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_SQUARE, Z_SQUARE, o[SDR_RX_O_RDS_EXTRACT], M, ms,
+                                    o[SDR_RX_O_RDS_PRE_PLL], ms, 1, PRE_SQUARE)}, S, st));
+  // PLLs (model/fmMonoBlock.py:119, model/fmRDSblock.py:167): one lane per recurrence
+  if (stx || rd) {
+    PllJobs P{};
+    P.nstreams = S;
+    P.n = M;
+    if (stx)
+      P.j[P.njobs++] = PllJob{o[SDR_RX_O_BPF_RECOVERY], ms, r->pll_state[0], r->theta, r->ths,
+                              o[SDR_RX_O_STEREO_NCO], nullptr, ms, r->pll[0]};
+    if (rd)
+      P.j[P.njobs++] = PllJob{o[SDR_RX_O_RDS_PRE_PLL], ms, r->pll_state[1], r->theta + (int64_t)S * r->ths, r->ths,
+                              o[SDR_RX_O_RDS_NCO_I], o[SDR_RX_O_RDS_NCO_Q], ms, r->pll[1]};
+    HIP_TRY(sdr_launch_pll_jobs(P, st));
+  }
+  // stage C: mixers + LPFs; the stereo LPF's store also forms L and R
+  std::vector<StageJob> C;
+  if (stx) {
+    StageJob j = fir(SDR_RX_F_STEREO_LPF, Z_SLPF, o[SDR_RX_O_BPF_EXTRACTION], M, ms, o[SDR_RX_O_STEREO], as,
+                     r->audio_decim, PRE_MIX, o[SDR_RX_O_STEREO_NCO]);          // fmMonoBlock.py:155-162
+    j.mono = o[SDR_RX_O_AUDIO];                                                 // :166-170 (intended)
+    j.left = o[SDR_RX_O_LEFT];
+    j.right = o[SDR_RX_O_RIGHT];
+    C.push_back(j);
+  }
+  if (rd) {                                                                     // fmRDSblock.py:173-182
+    C.push_back(fir(SDR_RX_F_RDS_LPF, Z_RLPF_I, o[SDR_RX_O_RDS_EXTRACT], M, ms, o[SDR_RX_O_RDS_LPF_I], ms, 1, PRE_MIX,
+                    o[SDR_RX_O_RDS_NCO_I]));
+    C.push_back(fir(SDR_RX_F_RDS_LPF, Z_RLPF_Q, o[SDR_RX_O_RDS_EXTRACT], M, ms, o[SDR_RX_O_RDS_LPF_Q], ms, 1, PRE_MIX,
+                    o[SDR_RX_O_RDS_NCO_Q]));
+  }
+  HIP_TRY(launch_stage(C, S, st));
+  if (rd) {
+    // stage D: rational resamplers (fmRDSblock.py:184-199)
+    const int64_t rs = r->out_stride[SDR_RX_O_RDS_RES_I];
+    std::vector<StageJob> Dj;
+    for (int k = 0; k < 2; ++k) {
+      StageJob j = fir(SDR_RX_F_RDS_ANTI, k ? Z_ANTI_Q : Z_ANTI_I, o[k ? SDR_RX_O_RDS_LPF_Q : SDR_RX_O_RDS_LPF_I], M, ms,
+                       o[k ? SDR_RX_O_RDS_RES_Q : SDR_RX_O_RDS_RES_I], rs, r->rds_down);
+      j.kind = JK_RESAMPLE;
+      j.U = r->rds_up;
+      Dj.push_back(j);
+    }
+    HIP_TRY(launch_stage(Dj, S, st));
+    // stage E: RRC (fmRDSblock.py:202-204)
+    HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_RRC, Z_RRC_I, o[SDR_RX_O_RDS_RES_I], r->R, rs, o[SDR_RX_O_RDS_RRC_I], rs, 1),
+                          fir(SDR_RX_F_RDS_RRC, Z_RRC_Q, o[SDR_RX_O_RDS_RES_Q], r->R, rs, o[SDR_RX_O_RDS_RRC_Q], rs, 1)},
+                         S, st));
+  }
+  r->parity ^= 1;
+  ++r->blocks;
+  return SDR_OK;
+}
+
+int sdr_rx_process(sdr_rx* r, const void* iq_host, int64_t iq_stride) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (iq_host == nullptr) return fail(SDR_EINVAL, "sdr_rx_process: iq is NULL");
+  if (r->S > 1 && iq_stride < r->B) return fail(SDR_EINVAL, "sdr_rx_process: iq_stride %lld < block", (long long)iq_stride);
+  TRY(set_dev(r->c));
+  const int64_t es = r->u8 ? 2 : 8;                      // bytes per complex sample
+  const int64_t xs = r->S > 1 ? iq_stride : r->B;
+  const size_t bytes = (size_t)(xs * (r->S - 1) + r->B) * es;
+  if (r->iq_cap < bytes) {
+    if (r->iq_dev) {
+      HIP_TRY(hipStreamSynchronize(r->c->stream));
+      HIP_TRY(hipFree(r->iq_dev));
+      r->iq_dev = nullptr;
+      r->iq_cap = 0;
+    }
+    hipError_t e = hipMalloc(&r->iq_dev, bytes);
+    if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx_process: hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    r->iq_cap = bytes;
+  }
+  HIP_TRY(hipMemcpyAsync(r->iq_dev, iq_host, bytes, hipMemcpyHostToDevice, r->c->stream));
+  TRY(sdr_rx_process_dev(r, r->iq_dev, xs));
+  HIP_TRY(hipStreamSynchronize(r->c->stream));
+  return SDR_OK;
+}
+
+int sdr_rx_output(sdr_rx* r, int which, float** dev, int64_t* stride, int64_t* n) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (which < 0 || which >= SDR_RX_NOUTPUTS) return fail(SDR_EINVAL, "sdr_rx_output: output %d", which);
+  if (!r->ready) TRY(rx_finalize(r));
+  if (!need_out(r, which)) return fail(SDR_EINVAL, "sdr_rx_output: output %d is not produced by flags 0x%x", which, r->flags);
+  if (dev) *dev = r->out[which];
+  if (stride) *stride = r->out_stride[which];
+  if (n) *n = r->out_n[which];
+  return SDR_OK;
+}
+
+int sdr_rx_fetch(sdr_rx* r, int which, float* host, int64_t host_stride) {
+  float* d;
+  int64_t ds, n;
+  TRY(sdr_rx_output(r, which, &d, &ds, &n));
+  if (host == nullptr) return fail(SDR_EINVAL, "sdr_rx_fetch: host is NULL");
+  if (r->S > 1 && host_stride < n) return fail(SDR_EINVAL, "sdr_rx_fetch: host_stride %lld < %lld", (long long)host_stride, (long long)n);
+  TRY(set_dev(r->c));
+  HIP_TRY(hipMemcpy2DAsync(host, sizeof(float) * (size_t)(r->S > 1 ? host_stride : n), d, sizeof(float) * (size_t)ds,
+                           sizeof(float) * (size_t)n, (size_t)r->S, hipMemcpyDeviceToHost, r->c->stream));
+  HIP_TRY(hipStreamSynchronize(r->c->stream));
+  return SDR_OK;
+}
+
+int sdr_rx_state(sdr_rx* r, double* phase, double* pll_stereo, double* pll_rds) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (!r->ready) TRY(rx_finalize(r));
+  TRY(set_dev(r->c));
+  hipStream_t st = r->c->stream;
+  const size_t S = (size_t)r->S;
+  if (phase) HIP_TRY(hipMemcpyAsync(phase, r->phase, sizeof(double) * S, hipMemcpyDeviceToHost, st));
+  if (pll_stereo) HIP_TRY(hipMemcpyAsync(pll_stereo, r->pll_state[0], sizeof(double) * 6 * S, hipMemcpyDeviceToHost, st));
+  if (pll_rds) HIP_TRY(hipMemcpyAsync(pll_rds, r->pll_state[1], sizeof(double) * 6 * S, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return SDR_OK;
+}
+
+}  // extern "C"

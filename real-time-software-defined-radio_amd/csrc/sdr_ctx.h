@@ -1,0 +1,73 @@
+// Host-side internals of a libsdr context, shared by the C-ABI translation units
+// (capi.hip: the per-call entry points; rx.hip: the multi-stream block receiver).
+// Not part of the public ABI (include/sdr.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <list>
+#include <string>
+#include <vector>
+
+#include "sdr_launch.h"
+#include "../../include/sdr.h"
+
+namespace sdrint {
+
+// scratch slots owned by a context (grown on demand, never shrunk)
+enum Slot {
+  S_IN, S_IN2, S_OUT, S_OUT2, S_OUT3, S_OUT4, S_STATE, S_STATE2, S_MISC, S_THETA, S_PHI, S_WRAP,
+  S_PSD,
+  S_NSLOT
+};
+
+struct TapSet {
+  std::vector<double> b;
+  TapsF32 h;
+  float* dev_f32 = nullptr;
+  double* dev_f64 = nullptr;
+};
+
+// the calling thread's last error message; returns `code`
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+}  // namespace sdrint
+
+struct sdr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  void* slot[sdrint::S_NSLOT] = {};
+  size_t cap[sdrint::S_NSLOT] = {};
+  // uploaded tap sets (taps are designed once), least recently used first.  A list: a hit
+  // is spliced to the back and an overflow evicts the front, so no pointer handed out by
+  // a lookup is invalidated by the other lookups of the same entry point (<= 4 per call).
+  std::list<sdrint::TapSet> taps;
+};
+
+namespace sdrint {
+
+int set_dev(sdr_ctx* c);
+// context scratch slot `s` of at least `bytes` (synchronises the stream when it grows)
+int scratch(sdr_ctx* c, Slot s, size_t bytes, void** out);
+// device copies (f32, f64) of the tap set b[0..T) (cached per context).  max_T: SDR_MAX_TAPS
+// for the FIR kernels, up to SDR_MAX_RESAMPLE_TAPS for the resampler.
+int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T = SDR_MAX_TAPS);
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace sdrint
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return sdrint::fail(SDR_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+#define TRY(expr)                 \
+  do {                            \
+    int r_ = (expr);              \
+    if (r_ != SDR_OK) return r_;  \
+  } while (0)
+
+#define CHECK_CTX(c) \
+  if ((c) == nullptr) return sdrint::fail(SDR_EINVAL, "context is NULL")

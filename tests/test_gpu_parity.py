@@ -77,6 +77,8 @@ def test_stereo_processor(sdr, gpu_ctx, golden, iq):
     p = sdr.StereoBlockProcessor(B)
     for k in range(3):
         o = p.process(iq[2 * k * B: 2 * (k + 1) * B], return_intermediates=True)
+        print("stereo errors (max, rms):", k, {key: (f"{maxabs(o[key], g[key][k]):.1e}", f"{rms(o[key], g[key][k]):.1e}")
+                                               for key in ("bpf_recovery", "nco", "bpf_extraction", "stereo")})
         assert maxabs(o["bpf_recovery"], g["bpf_recovery"][k]) < 1e-5
         assert maxabs(o["nco"], g["nco"][k]) < 1e-4
         assert rms(o["nco"], g["nco"][k]) < 1e-5
@@ -92,12 +94,13 @@ def test_rds_processor(sdr, gpu_ctx, golden):
     for k in range(2):
         o = p.process(g["iq"][k * 307200:(k + 1) * 307200], return_intermediates=True)
         assert rms(o["demod"], g["demod"][k]) < DEMOD_RMS
-        for key in ("extract", "pre_pll", "nco_i", "nco_q", "lpf_i", "lpf_q", "resample_i", "resample_q",
-                    "rrc_i", "rrc_q"):
+        from test_receiver import RDS_TOL
+        for key, (tmax, trms) in RDS_TOL.items():
             ref = g[key][k]
             scale = max(float(np.max(np.abs(ref))), 1e-3)
-            assert maxabs(o[key], ref) < 2e-4 * scale, (key, k, maxabs(o[key], ref), scale)
-            assert rms(o[key], ref) < 2e-5 * scale, (key, k, rms(o[key], ref), scale)
+            print("rds", key, k, f"{maxabs(o[key], ref) / scale:.1e} {rms(o[key], ref) / scale:.1e}")
+            assert maxabs(o[key], ref) < tmax * scale, (key, k, maxabs(o[key], ref), scale)
+            assert rms(o[key], ref) < trms * scale, (key, k, rms(o[key], ref), scale)
 
 
 def test_mono_basic_single_pass(sdr, gpu_ctx, golden):
