@@ -15,6 +15,17 @@ each rank processes its own independent stream (seed = rank): weak scaling, no
 data-path collective.  torch.distributed (gloo, CPU) only provides the barrier and
 the max-over-ranks of the timed region.
 
+Other workloads (`--workload`, one JSON line each; BASELINE.json configs):
+  c5  configs[4]: `--streams` (default 8) independent u8 streams per GPU, 153 600-sample
+      blocks (src/fm_radio.cpp:23), mono + stereo + RDS to the RRC output through the
+      multi-stream receiver (sdr_rx), inputs resident in HBM, one step = one block of every
+      stream (>= 256 blocks per stream by default); per-stage GPU times from HIP events.
+  c3 / c4  configs[2] / [3]: the per-block drop-in path at fmMonoBlock.py's 51 200-sample
+      blocks, host buffers in and out (PCIe-inclusive by nature), one stream: mono (c3) or
+      mono + stereo (c4).
+  CPU baselines for these: the reference's own C++ receiver (src/filter.cpp, helper.cpp,
+  rf_module.cpp compiled from its sources, oracle/ref_driver.cpp ref_rx_streams).
+
 Prints ONE JSON line (rank 0).  `value` = complex IQ samples processed by all ranks
 per second (MS/s); `roofline` is for the step's dominant kernel (HIP events on the libsdr stream);
 `cpu_baseline` = the C restatement of the Python model (oracle/fm_oracle.c) on the
@@ -42,7 +53,11 @@ BLOCK = 1_024_000              # complex samples per block (SURVEY §7 hard part
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--workload", choices=["mono", "c3", "c4", "c5"], default="mono",
+                    help="mono: configs[1]+[2] batched (the headline); c3/c4: per-block drop-in path; "
+                         "c5: multi-stream mono+stereo+RDS")
+    ap.add_argument("--streams", type=int, default=8, help="c5: independent streams per GPU")
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 50; c5: 256 blocks)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--settle-ms", type=float, default=250.0,
                     help="untimed warm-up continues past --warmup steps until this much GPU time has "
@@ -58,7 +73,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall time per CPU leg")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "fe_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per FE launch (written by tools/pmc_traffic.py)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 256 if a.workload == "c5" else (200 if a.workload in ("c3", "c4") else 50)
+    return a
 
 
 def dist_setup(args):
@@ -99,8 +117,8 @@ def cpu_baseline(args, rf_b, au_b):
     lib.orc_fe_mono_streams.argtypes = [P(np.float32), ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                         P(np.float64), ctypes.c_int, P(np.float64), ctypes.c_int,
                                         P(np.float64), ctypes.c_int64, ctypes.c_int]
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16, os.cpu_count() or 1))
+    threads = cpu_threads()
+    visible, model = cpu_cores()
     import rtsdr
     n = args.cpu_samples
     # one synthetic stream shared read-only by all threads (bounded memory); each thread
@@ -125,6 +143,7 @@ def cpu_baseline(args, rf_b, au_b):
 
     reps, dt = timed(run_port)
     res = {"value": round(n * threads * reps / dt / 1e6, 3), "unit": "MS/s", "cores": threads, "kind": "port",
+           "cpu": model, "cores_visible": visible,
            "sample": f"{threads} threads x {reps} x {n} complex samples (one stream each), "
                      f"FE({len(rf_b)} taps)+mono({len(au_b)} taps), f64 C restatement of the Python model "
                      f"(oracle/fm_oracle.c, -O3 -march=x86-64-v3, OpenMP), {dt:.2f} s wall"}
@@ -147,8 +166,32 @@ def cpu_baseline(args, rf_b, au_b):
                                    "cores": threads, "kind": "reference",
                                    "sample": f"{threads} threads x {reps} x {nn} complex, src/filter.cpp "
                                              f"convolveWithDecimIQ + src/rf_module.cpp fmDemodArctan (FE only, "
-                                             f"f32, reference -O3 flags), {dt:.2f} s wall"}
+                                             f"f32, reference -O3 flags), {dt:.2f} s wall; {ref_provenance()}"}
+    else:
+        res["reference_cpp_fe"] = {"value": None, "kind": "reference",
+                                   "sample": "not run: oracle/_ref/libref_fe.so absent (built only where "
+                                             "/root/reference exists; make -C oracle ref)"}
     return res
+
+
+def ref_provenance():
+    """Which reference sources oracle/_ref was compiled from (sha256, oracle/Makefile)."""
+    try:
+        with open(os.path.join(ROOT, "oracle", "_ref", "sources.sha256")) as f:
+            got = f.read()
+        with open(os.path.join(ROOT, "oracle", "ref_sources.sha256")) as f:
+            want = f.read()
+        return "sources match oracle/ref_sources.sha256" if got == want else "sources DIFFER from oracle/ref_sources.sha256"
+    except OSError:
+        return "source hashes unavailable"
+
+
+def cpu_threads():
+    """Worker threads for the CPU legs: the lease's CPU share.  OMP_NUM_THREADS when the
+    environment sets it (the GPU box sets it to its per-GPU share), else every core this
+    process may run on."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return env if env > 0 else cpu_cores()[0]
 
 
 def load_traffic(path, taps, blocks, kpath):
@@ -168,6 +211,8 @@ def main():
     args = parse()
     ws, rank, local = dist_setup(args)
     os.environ["SDR_DEVICE"] = str(local)
+    if args.workload != "mono":
+        return run_rx(args, ws, rank, local)
     import rtsdr
     from importlib import import_module
     _lib = import_module("real-time-software-defined-radio_amd._lib")
@@ -296,6 +341,182 @@ def main():
     tm.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def cpu_cores():
+    """Host cores this process may use, and the CPU model (all cores)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return n, model
+
+
+def ref_rx_baseline(args, iq_blocks, B, u8, stereo, rds, rf_taps):
+    """The reference's own C++ receiver (oracle/_ref/libref_fe.so, ref_rx_streams), one stream
+    per thread on all host cores, ~args.cpu_seconds of wall time; None when the library was not
+    built (it needs /root/reference at build time) -- said so in the line."""
+    path = os.path.join(ROOT, "oracle", "_ref", "libref_fe.so")
+    visible, model = cpu_cores()
+    cores = cpu_threads()
+    if not os.path.exists(path):
+        return {"value": None, "unit": "MS/s", "cores": cores, "kind": "reference", "cpu": model,
+                "sample": "not run: oracle/_ref/libref_fe.so absent (built only where /root/reference exists)"}
+    lib = ctypes.CDLL(path)
+    lib.ref_rx_streams.restype = ctypes.c_double
+    lib.ref_rx_streams.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                   ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    x = np.ascontiguousarray(iq_blocks)                 # one stream's blocks, shared read-only by all threads
+    n = x.size // 2
+    n = (n // B) * B
+
+    def run(threads):
+        return lib.ref_rx_streams(x.ctypes.data, int(u8), n, 0, threads, B, rf_taps, int(stereo), int(rds), threads)
+
+    t0 = time.perf_counter()
+    run(1)
+    t1 = max(time.perf_counter() - t0, 1e-6)
+    reps = max(1, int(np.ceil(args.cpu_seconds / t1)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run(cores)
+    dt = time.perf_counter() - t0
+    return {"value": round(n * cores * reps / dt / 1e6, 3), "unit": "MS/s", "cores": cores, "kind": "reference",
+            "cpu": model, "cores_visible": visible,
+            "sample": f"{cores} threads x {reps} x {n // B} blocks of {B} complex (one stream per thread), the "
+                      f"reference's rf/mono_stereo/rds thread bodies (src/fm_radio.cpp mode 0, stereo={int(stereo)}, "
+                      f"rds={int(rds)}) compiled from its sources -O3, {dt:.2f} s wall; {ref_provenance()}"}
+
+
+def run_rx(args, ws, rank, local):
+    """c3 / c4 (per-block drop-in path, host buffers) and c5 (multi-stream, device-resident)."""
+    import rtsdr
+    from importlib import import_module
+    _lib = import_module("real-time-software-defined-radio_amd._lib")
+    ctx = _lib.Context(local)
+    c5 = args.workload == "c5"
+    B = 153_600 if c5 else 51_200
+    S = args.streams if c5 else 1
+    u8 = c5
+    stereo = args.workload in ("c4", "c5")
+    rds = c5
+    rf_taps = 151 if c5 else args.taps
+    rf_b, au_b = rtsdr.design.mono_coeffs(rf_taps, args.audio_taps)
+    rx = rtsdr.Receiver(S, B, stereo=stereo, rds=rds, iq_dtype=np.uint8 if u8 else np.float32,
+                        rf_coeff=rf_b, audio_coeff=au_b, ctx=ctx)
+    nres = 16                                           # distinct blocks per stream, cycled
+    dt = np.uint8 if u8 else np.float32
+    # one synthetic stream per stream index (seed = rank * S + s), nres consecutive blocks
+    host = np.stack([rtsdr.synth.fm_iq(nres * B, seed=rank * S + s, dtype=dt).reshape(nres, 2 * B)
+                     for s in range(S)], axis=1)        # (nres, S, 2B)
+    es = 2 if u8 else 8
+    fetch = ["audio", "left", "right"] if stereo else ["audio"]
+    if c5:
+        d_iq = _lib.DeviceBuffer.from_array(ctx, host)
+        blk_bytes = S * B * es
+
+        def step(k):
+            rx.process_dev(d_iq.ptr + (k % nres) * blk_bytes, B)
+    else:
+        def step(k):
+            o = rx.process(host[k % nres], fetch=fetch)
+            return o
+    for k in range(args.warmup):
+        step(k)
+    ctx.synchronize()
+    t_set = time.perf_counter()
+    settle = 0
+    while (time.perf_counter() - t_set) * 1e3 < args.settle_ms:
+        for _ in range(8):
+            step(settle)
+            settle += 1
+        ctx.synchronize()
+    # per-stage GPU times (events between the receiver's launches), a separate pass
+    rx.set_timing(True)
+    stages = []
+    for k in range(8):
+        step(k)
+        stages.append(rx.stage_ms())
+    rx.set_timing(False)
+    stage_ms = {key: round(float(np.mean([st[key] for st in stages])), 5) for key in stages[0]}
+    barrier(ws)
+    ctx.synchronize()
+    lat = []
+    t0 = time.perf_counter()
+    if c5:
+        tm = _lib.Timer(ctx)
+        e0, e1 = tm.event(), tm.event()
+        tm.record(e0)
+        for k in range(args.steps):
+            step(k)
+        tm.record(e1)
+    else:
+        for k in range(args.steps):
+            t = time.perf_counter()
+            step(k)
+            lat.append(time.perf_counter() - t)
+    ctx.synchronize()
+    barrier(ws)
+    elapsed = max_over_ranks(ws, time.perf_counter() - t0)
+    gpu_ms = tm.elapsed_ms(e0, e1) / args.steps if c5 else None
+    result = None
+    if rank == 0:
+        total = S * B * args.steps * ws
+        M = B // 10
+        dom = max(stage_ms, key=stage_ms.get)
+        # the front end is the HBM-streaming kernel of the chain: IQ in + demod out per launch
+        fe_bytes = S * (B * es + M * 4)
+        fe_gbs = fe_bytes / (stage_ms["fe"] * 1e-3) / 1e9
+        result = {
+            "metric": f"IQ MSamples/s through the {'multi-stream mono+stereo+RDS receiver' if c5 else 'per-block drop-in path'}"
+                      f" ({args.workload}); achieved HBM GB/s vs peak",
+            "value": round(total / elapsed / 1e6, 1), "unit": "MS/s", "n_gpus": ws, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": (f"synthetic FM IQ (seed = rank*streams + stream), interleaved {'u8' if u8 else 'f32'}, "
+                     + ("device-resident, 16 distinct blocks per stream cycled" if c5 else
+                        "host buffers: each step uploads one block and downloads its outputs (PCIe-inclusive)")),
+            "config": {"workload": {"c3": "configs[2]: FE + mono per block, fmMonoBlock.py block size",
+                                    "c4": "configs[3]: FE + mono + stereo per block, fmMonoBlock.py block size",
+                                    "c5": "configs[4]: independent streams, mono + stereo + RDS to the RRC output"}
+                       [args.workload],
+                       "block_complex": B, "streams_per_gpu": S, "rf_taps": rf_taps, "iq": "u8" if u8 else "f32",
+                       "parallelism": f"independent streams x{S * ws}"},
+            "roofline": {"bound": "hbm", "achieved": round(fe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(fe_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": f"FE stage (fe_slot/ring kernel, {rf_taps} taps, + its zf and phase kernels)",
+                         "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": stage_ms["fe"]},
+            "stage_ms": stage_ms,
+            "dominant_stage": {"stage": dom, "ms": stage_ms[dom],
+                               "bound": ("serial f64 PLL recurrence: one lane per stream, ~"
+                                         f"{stage_ms[dom] * 1e6 / M:.0f} ns per sample step") if dom == "pll" else "see roofline"},
+        }
+        if c5:
+            result["gpu_ms_per_block"] = round(gpu_ms, 5)
+        else:
+            la = np.array(lat) * 1e3
+            result["block_latency_ms"] = {"mean": round(float(la.mean()), 4), "p50": round(float(np.median(la)), 4),
+                                          "p99": round(float(np.percentile(la, 99)), 4)}
+            result["realtime_factor"] = round((total / elapsed) / 2.4e6, 1)     # x the 2.4 MS/s input rate
+    if ws == 1 and not args.no_cpu and rank == 0:
+        result["cpu_baseline"] = ref_rx_baseline(args, host[:, 0].reshape(-1), B, u8, stereo, rds, rf_taps)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    rx.close()
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

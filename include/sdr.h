@@ -228,6 +228,14 @@ int sdr_rx_process_dev(sdr_rx* rx, const void* iq, int64_t iq_stride);   /* asyn
 int sdr_rx_process(sdr_rx* rx, const void* iq, int64_t iq_stride);       /* sync, host IQ */
 int sdr_rx_output(sdr_rx* rx, int which, float** dev, int64_t* stride, int64_t* n);
 int sdr_rx_fetch(sdr_rx* rx, int which, float* host, int64_t host_stride); /* sync, all streams */
+/* per-stage timing of the last block (HIP events between the receiver's launches, on the
+ * context stream): FE, stage A (filters of demod), B (RDS square), PLL, C (mixers + LPFs),
+ * D (resamplers), E (RRC); ms: SDR_RX_NSTAGES floats.  Timing adds event records between
+ * launches; keep it off in measured loops. */
+enum { SDR_RX_ST_FE, SDR_RX_ST_A, SDR_RX_ST_B, SDR_RX_ST_PLL, SDR_RX_ST_C, SDR_RX_ST_D, SDR_RX_ST_E,
+       SDR_RX_NSTAGES };
+int sdr_rx_set_timing(sdr_rx* rx, int on);
+int sdr_rx_stage_ms(sdr_rx* rx, float* ms);
 /* carried states (host copies; any may be NULL): demod prev_phase [nstreams], PLL states
  * [nstreams][6] in fmPll's order (model/fmPll.py:39-44) */
 int sdr_rx_state(sdr_rx* rx, double* phase, double* pll_stereo, double* pll_rds);

@@ -26,6 +26,7 @@ RX_FILTERS = ("rf", "audio", "pilot", "stereo_bpf", "stereo_lpf", "rds_extract",
 RX_OUTPUTS = ("demod", "audio", "bpf_recovery", "nco", "bpf_extraction", "stereo", "left", "right",
               "extract", "pre_pll", "nco_i", "nco_q", "lpf_i", "lpf_q", "resample_i", "resample_q",
               "rrc_i", "rrc_q")
+RX_STAGES = ("fe", "filters_of_demod", "rds_square", "pll", "mix_lpf", "resample", "rrc")
 
 
 class SdrUnavailable(RuntimeError):
@@ -92,6 +93,8 @@ SIGNATURES = {
     "sdr_rx_output": (_i32, [_vp, _i32, _c.POINTER(_vp), _c.POINTER(_i64), _c.POINTER(_i64)]),
     "sdr_rx_fetch": (_i32, [_vp, _i32, _fp, _i64]),
     "sdr_rx_state": (_i32, [_vp, _dp, _dp, _dp]),
+    "sdr_rx_set_timing": (_i32, [_vp, _i32]),
+    "sdr_rx_stage_ms": (_i32, [_vp, _fp]),
     "sdr_rds_link_create": (_i32, [_c.POINTER(_vp)]),
     "sdr_rds_link_destroy": (None, [_vp]),
     "sdr_rds_link_block": (_i32, [_vp, _dp, _i64, _vp, _i64, _c.POINTER(_i64), _vp, _i64, _c.POINTER(_i64),

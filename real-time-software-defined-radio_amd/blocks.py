@@ -129,6 +129,16 @@ class Receiver:
     def reset(self):
         check(self.lib.sdr_rx_reset(self.handle), "sdr_rx_reset")
 
+    def set_timing(self, on: bool = True):
+        """Record HIP events between the receiver's launches (stage_ms)."""
+        check(self.lib.sdr_rx_set_timing(self.handle, int(bool(on))), "sdr_rx_set_timing")
+
+    def stage_ms(self) -> dict:
+        """GPU time per stage of the last block (set_timing(True) first): _lib.RX_STAGES."""
+        ms = np.zeros(len(_lib.RX_STAGES), dtype=np.float32)
+        check(self.lib.sdr_rx_stage_ms(self.handle, ms.ctypes.data_as(_lib._fp)), "sdr_rx_stage_ms")
+        return dict(zip(_lib.RX_STAGES, (float(v) for v in ms)))
+
     def close(self):
         if getattr(self, "handle", None):
             self.lib.sdr_rx_destroy(self.handle)

@@ -89,17 +89,24 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
     phase = phase + cfg.kp * e + integ;
     arg = w * ((off + (double)k) + 1.0) + phase;
   };
-  // Fast form for x != 0: atan2(-x sin a, x cos a) = wrap(-a) or wrap(pi - a), branch-free;
-  // `base` = (off + k) + 1 kept as a running exact integer in double (< 2^53).
+  // Fast form for x != 0: atan2(-x sin a, x cos a) = wrap(-a) or wrap(pi - a), branch-free.
+  // The step is issue-bound (one wave issues every instruction of the recurrence; an f64
+  // op holds the SIMD ~8 cycles at wave64), so it is written for the fewest f64 ops (10: 23
+  // instructions per step became 15, tools/pll_probe.hip): the loop filter's updates as
+  // FMAs (one rounding where Python rounds twice: the f32 outputs cannot see the
+  // difference) and a two-constant reduction (the third term is below 1e-22 rad per turn).  `base` = (off + k) + 1 is a running exact integer in double (< 2^53).
   double base = 0.0;
   auto fast = [&](float xf) {
     const double sel = xf > 0.f ? 0.0 : kPi;                 // off the chain: x is known
-    const double r = reduce_2pi(sel - arg);
-    const double e = r <= -kPi ? r + 2.0 * kPi : r;
-    integ = integ + cfg.ki * e;
-    phase = phase + cfg.kp * e + integ;
+    const double d = sel - arg;
+    // n = ceil(d/2pi - 1/2) rounds half-way cases down, so e = d - 2 pi n lies in (-pi, pi]
+    // (atan2's range) without a range fix
+    const double nn = ceil(fma(d, kInv2Pi, -0.5));
+    const double e = fma(-nn, kP2, fma(-nn, kP1, d));
+    integ = fma(cfg.ki, e, integ);
+    phase = fma(cfg.kp, e, phase) + integ;
     base = base + 1.0;
-    arg = w * base + phase;
+    arg = fma(w, base, phase);
   };
   auto load_group = [&](float (&v)[PG], int64_t k0) {
     if constexpr (VEC) {

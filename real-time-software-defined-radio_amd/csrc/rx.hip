@@ -362,6 +362,8 @@ struct sdr_rx {
   size_t iq_cap = 0;
   int parity = 0;
   int64_t blocks = 0;
+  bool timing = false;                 // events between the stages of each block
+  hipEvent_t ev[SDR_RX_NSTAGES + 1] = {};
 };
 
 namespace {
@@ -503,6 +505,8 @@ void sdr_rx_destroy(sdr_rx* r) {
   }
   if (r->mem) (void)hipFree(r->mem);
   if (r->iq_dev) (void)hipFree(r->iq_dev);
+  for (hipEvent_t e : r->ev)
+    if (e) (void)hipEventDestroy(e);
   delete r;
 }
 
@@ -567,6 +571,8 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   const int64_t M = r->M;
   double* zi = r->bank[r->parity];
   double* zf = r->bank[r->parity ^ 1];
+  auto mark = [&](int k) { return r->timing ? hipEventRecord(r->ev[k], st) : hipSuccess; };
+  HIP_TRY(mark(0));
   auto zin = [&](int z) { return zi + r->zoff[z]; };
   auto zout = [&](int z) { return zf + r->zoff[z]; };
   // device taps (cached per context; the pointers stay valid for this call)
@@ -580,6 +586,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   TRY(sdr_rf_frontend_dev(c, iq, r->u8 ? SDR_IQ_U8 : SDR_IQ_F32, r->B, S > 1 ? iq_stride : r->B, 0, S,
                           r->taps[SDR_RX_F_RF].data(), Trf, r->rf_decim, zin(Z_FE_I), zin(Z_FE_Q), r->zlen[Z_FE_I],
                           zout(Z_FE_I), zout(Z_FE_Q), r->phase, o[SDR_RX_O_DEMOD], ms, nullptr, nullptr));
+  HIP_TRY(mark(1 + SDR_RX_ST_FE));
   auto fir = [&](int f, int z, const float* x, int64_t n, int64_t xs, float* y, int64_t ys, int D, int pre = PRE_NONE,
                  const float* cmix = nullptr) {
     StageJob j{};
@@ -603,9 +610,11 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   }
   if (rd) A.push_back(fir(SDR_RX_F_RDS_EXTRACT, Z_EXTRACT, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_RDS_EXTRACT], ms, 1));
   HIP_TRY(launch_stage(A, S, st));
+  HIP_TRY(mark(1 + SDR_RX_ST_A));
   // stage B: RDS squaring non-linearity + BPF (model/fmRDSblock.py:161-164)
   if (rd) HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_SQUARE, Z_SQUARE, o[SDR_RX_O_RDS_EXTRACT], M, ms,
                                     o[SDR_RX_O_RDS_PRE_PLL], ms, 1, PRE_SQUARE)}, S, st));
+  HIP_TRY(mark(1 + SDR_RX_ST_B));
   // PLLs (model/fmMonoBlock.py:119, model/fmRDSblock.py:167): one lane per recurrence
   if (stx || rd) {
     PllJobs P{};
@@ -619,6 +628,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
                               o[SDR_RX_O_RDS_NCO_I], o[SDR_RX_O_RDS_NCO_Q], ms, r->pll[1]};
     HIP_TRY(sdr_launch_pll_jobs(P, st));
   }
+  HIP_TRY(mark(1 + SDR_RX_ST_PLL));
   // stage C: mixers + LPFs; the stereo LPF's store also forms L and R
   std::vector<StageJob> C;
   if (stx) {
@@ -636,6 +646,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
                     o[SDR_RX_O_RDS_NCO_Q]));
   }
   HIP_TRY(launch_stage(C, S, st));
+  HIP_TRY(mark(1 + SDR_RX_ST_C));
   if (rd) {
     // stage D: rational resamplers (fmRDSblock.py:184-199)
     const int64_t rs = r->out_stride[SDR_RX_O_RDS_RES_I];
@@ -648,11 +659,15 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       Dj.push_back(j);
     }
     HIP_TRY(launch_stage(Dj, S, st));
+    HIP_TRY(mark(1 + SDR_RX_ST_D));
     // stage E: RRC (fmRDSblock.py:202-204)
     HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_RRC, Z_RRC_I, o[SDR_RX_O_RDS_RES_I], r->R, rs, o[SDR_RX_O_RDS_RRC_I], rs, 1),
                           fir(SDR_RX_F_RDS_RRC, Z_RRC_Q, o[SDR_RX_O_RDS_RES_Q], r->R, rs, o[SDR_RX_O_RDS_RRC_Q], rs, 1)},
                          S, st));
+  } else {
+    HIP_TRY(mark(1 + SDR_RX_ST_D));
   }
+  HIP_TRY(mark(1 + SDR_RX_ST_E));
   r->parity ^= 1;
   ++r->blocks;
   return SDR_OK;
@@ -704,6 +719,23 @@ int sdr_rx_fetch(sdr_rx* r, int which, float* host, int64_t host_stride) {
   HIP_TRY(hipMemcpy2DAsync(host, sizeof(float) * (size_t)(r->S > 1 ? host_stride : n), d, sizeof(float) * (size_t)ds,
                            sizeof(float) * (size_t)n, (size_t)r->S, hipMemcpyDeviceToHost, r->c->stream));
   HIP_TRY(hipStreamSynchronize(r->c->stream));
+  return SDR_OK;
+}
+
+int sdr_rx_set_timing(sdr_rx* r, int on) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  TRY(set_dev(r->c));
+  if (on && !r->ev[0])
+    for (hipEvent_t& e : r->ev) HIP_TRY(hipEventCreate(&e));
+  r->timing = on != 0;
+  return SDR_OK;
+}
+
+int sdr_rx_stage_ms(sdr_rx* r, float* ms) {
+  if (r == nullptr || ms == nullptr) return fail(SDR_EINVAL, "sdr_rx_stage_ms: NULL argument");
+  if (!r->timing || r->blocks == 0) return fail(SDR_EINVAL, "sdr_rx_stage_ms: no timed block (sdr_rx_set_timing)");
+  HIP_TRY(hipEventSynchronize(r->ev[SDR_RX_NSTAGES]));
+  for (int k = 0; k < SDR_RX_NSTAGES; ++k) HIP_TRY(hipEventElapsedTime(&ms[k], r->ev[k], r->ev[k + 1]));
   return SDR_OK;
 }
 

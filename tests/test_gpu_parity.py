@@ -77,12 +77,11 @@ def test_stereo_processor(sdr, gpu_ctx, golden, iq):
     p = sdr.StereoBlockProcessor(B)
     for k in range(3):
         o = p.process(iq[2 * k * B: 2 * (k + 1) * B], return_intermediates=True)
-        print("stereo errors (max, rms):", k, {key: (f"{maxabs(o[key], g[key][k]):.1e}", f"{rms(o[key], g[key][k]):.1e}")
-                                               for key in ("bpf_recovery", "nco", "bpf_extraction", "stereo")})
-        assert maxabs(o["bpf_recovery"], g["bpf_recovery"][k]) < 1e-5
-        assert maxabs(o["nco"], g["nco"][k]) < 1e-4
-        assert rms(o["nco"], g["nco"][k]) < 1e-5
-        assert maxabs(o["bpf_extraction"], g["bpf_extraction"][k]) < 1e-5
+        # ~3x the errors measured on MI355X (profiles/r02/rx_tolerances.log)
+        assert maxabs(o["bpf_recovery"], g["bpf_recovery"][k]) < 5e-7
+        assert maxabs(o["nco"], g["nco"][k]) < 1e-7
+        assert rms(o["nco"], g["nco"][k]) < 5e-8
+        assert maxabs(o["bpf_extraction"], g["bpf_extraction"][k]) < 2e-6
         for key in ("audio", "stereo", "left", "right"):
             assert rms(o[key], g[key][k]) < AUDIO_RMS, (key, k)
             assert maxabs(o[key], g[key][k]) < AUDIO_MAX, (key, k)
@@ -98,7 +97,6 @@ def test_rds_processor(sdr, gpu_ctx, golden):
         for key, (tmax, trms) in RDS_TOL.items():
             ref = g[key][k]
             scale = max(float(np.max(np.abs(ref))), 1e-3)
-            print("rds", key, k, f"{maxabs(o[key], ref) / scale:.1e} {rms(o[key], ref) / scale:.1e}")
             assert maxabs(o[key], ref) < tmax * scale, (key, k, maxabs(o[key], ref), scale)
             assert rms(o[key], ref) < trms * scale, (key, k, rms(o[key], ref), scale)
 
