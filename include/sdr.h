@@ -226,6 +226,11 @@ int sdr_rx_set_pll(sdr_rx* rx, int which /* 0 stereo, 1 RDS */, double freq, dou
 int sdr_rx_reset(sdr_rx* rx);                       /* all states back to the stream start */
 int sdr_rx_process_dev(sdr_rx* rx, const void* iq, int64_t iq_stride);   /* async, device IQ */
 int sdr_rx_process(sdr_rx* rx, const void* iq, int64_t iq_stride);       /* sync, host IQ */
+/* sync, host IQ in and the `nout` requested outputs (which[i]: SDR_RX_O_*) out into
+ * out[i] (nstreams rows, out_stride[i] floats apart; NULL out_stride = packed), through
+ * pinned staging with one wait: the per-block drop-in call of fmMonoBlock.py's loop */
+int sdr_rx_run(sdr_rx* rx, const void* iq, int64_t iq_stride, int nout, const int* which,
+               float* const* out, const int64_t* out_stride);
 int sdr_rx_output(sdr_rx* rx, int which, float** dev, int64_t* stride, int64_t* n);
 int sdr_rx_fetch(sdr_rx* rx, int which, float* host, int64_t host_stride); /* sync, all streams */
 /* per-stage timing of the last block (HIP events between the receiver's launches, on the

@@ -48,6 +48,7 @@ class Receiver:
         self.u8 = np.dtype(iq_dtype) == np.uint8
         flags = (SDR_RX_AUDIO if mono else 0) | (SDR_RX_STEREO if stereo else 0) | (SDR_RX_RDS if rds else 0)
         self.flags = flags
+        self._lengths = {}
         h = ctypes.c_void_p()
         check(self.lib.sdr_rx_create(self.ctx.handle, self.S, self.B, SDR_IQ_U8 if self.u8 else SDR_IQ_F32,
                                      flags, ctypes.byref(h)), "sdr_rx_create")
@@ -90,15 +91,25 @@ class Receiver:
 
     def process(self, iq, fetch=None):
         """One block of every stream; returns {name: (nstreams, n) float32} for `fetch`
-        (default: the configuration's final outputs)."""
+        (default: the configuration's final outputs).  One C call: IQ up, the chain, the
+        outputs down, one wait (sdr_rx_run)."""
         es = np.uint8 if self.u8 else np.float32
         iq = np.ascontiguousarray(iq, dtype=es)
         if iq.size != self.S * 2 * self.B:
             raise ValueError(f"expected {self.S} x {2 * self.B} interleaved values, got {iq.shape}")
-        check(self.lib.sdr_rx_process(self.handle, iq.ctypes.data, self.B), "sdr_rx_process")
         if fetch is None:
             fetch = [n for n in ("audio", "left", "right", "rrc_i", "rrc_q") if n in self.outputs]
-        return {n: self.output(n) for n in fetch}
+        outs = {n: np.empty((self.S, self._length(n)), dtype=np.float32) for n in fetch}
+        k = len(fetch)
+        which = (ctypes.c_int * k)(*[RX_OUTPUTS.index(n) for n in fetch])
+        ptrs = (ctypes.c_void_p * k)(*[outs[n].ctypes.data for n in fetch])
+        check(self.lib.sdr_rx_run(self.handle, iq.ctypes.data, self.B, k, which, ptrs, None), "sdr_rx_run")
+        return outs
+
+    def _length(self, name):
+        if name not in self._lengths:
+            self._lengths[name] = self.output_ptr(name)[2]
+        return self._lengths[name]
 
     def process_dev(self, iq_ptr: int, iq_stride: int):
         """One block from device memory (async on the context stream); outputs stay on the

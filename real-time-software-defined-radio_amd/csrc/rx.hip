@@ -61,11 +61,31 @@ struct StageJob {
   int pre, D, U, kind, T, tiles;
 };
 
+// The front end's carried state, finished by the first stage launch after the FE kernel:
+// the I/Q lfilter final states (f64, from the block's last T-1 IQ samples) and the demod
+// phase prev = phi_last + 2 pi W (W = the block's wrap count, which is reset for the next
+// block).  One workgroup per stream.
+struct FeState {
+  const void* iq;
+  int64_t n, stride;          // complex samples per block / between streams
+  const double* b;            // f64 taps
+  const double* zi_i;
+  const double* zi_q;
+  double* zf_i;
+  double* zf_q;
+  int64_t zs;                 // state stride
+  const float* last_phi;
+  int* wraps;
+  double* phase;
+  int T, u8, on;
+};
+
 struct StageJobs {
   StageJob j[RX_MAXJ];
   int njobs, nstreams;
   int64_t tile_blocks;        // workgroups [0, tile_blocks) compute outputs
   int zfj[RX_MAXJ], nzf;      // then nzf * nstreams workgroups compute final states
+  FeState fe;                 // then (fe.on ? nstreams : 0) workgroups finish the FE state
 };
 
 __device__ __forceinline__ float pre_op(int pre, float x, float c, float g) {
@@ -100,10 +120,21 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
   const int64_t m0 = tile * S::TO;
   const int64_t M = (J.n + D - 1) / D;
   const int64_t n_lo = D * m0 - (T - 1) - DELTA;
+  const int64_t mf = m0 + (int64_t)t * R;
   const float* xb = J.x + (int64_t)s * J.x_stride;
   const float* cb = J.c ? J.c + (int64_t)s * J.x_stride : nullptr;
   const int pre = J.pre;
   const float g = J.gain;
+  // the zi terms and the combiner inputs are loaded up front, not after the FIR: at the
+  // reference's block sizes a stage is a handful of workgroups whose time is the number of
+  // dependent memory round trips
+  float zr[R], mr[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t nn = D * (mf + r);
+    zr[r] = (J.zi != nullptr && nn < T - 1) ? (float)J.zi[(int64_t)s * J.zi_stride + nn] : 0.f;
+    mr[r] = (J.mono != nullptr && mf + r < M) ? J.mono[(int64_t)s * J.y_stride + mf + r] : 0.f;
+  }
   auto slot = [](int e) { return PAD ? e + (e + DR - DELTA) / DR : e; };
   if (n_lo >= 0 && n_lo + L <= J.n) {               // interior: 16-B loads (rows are aligned)
     float4 v[S::NLOAD], cv[S::NLOAD];
@@ -149,14 +180,8 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
       if (k >= 0 && k < T) acc[r] = fmaf(h[k], x, acc[r]);
     }
   }
-  const int64_t mf = m0 + (int64_t)t * R;
-  if (J.zi != nullptr) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int64_t nn = D * (mf + r);
-      if (nn < T - 1) acc[r] += (float)J.zi[(int64_t)s * J.zi_stride + nn];
-    }
-  }
+  for (int r = 0; r < R; ++r) acc[r] += zr[r];
   float* yb = J.y + (int64_t)s * J.y_stride;
   if (mf + R <= M) {
     *reinterpret_cast<float4*>(yb + mf) = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -166,15 +191,13 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
       if (mf + r < M) yb[mf + r] = acc[r];
   }
   if (J.mono != nullptr) {                           // stereo combiner (fmMonoBlock.py:166-170)
-    const float* mb = J.mono + (int64_t)s * J.y_stride;
     float* lb = J.left + (int64_t)s * J.y_stride;
     float* rb = J.right + (int64_t)s * J.y_stride;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (mf + r < M) {
-        const float a = mb[mf + r];
-        lb[mf + r] = (a + acc[r]) * 0.5f;
-        rb[mf + r] = (a - acc[r]) * 0.5f;
+        lb[mf + r] = (mr[r] + acc[r]) * 0.5f;
+        rb[mf + r] = (mr[r] - acc[r]) * 0.5f;
       }
     }
   }
@@ -259,11 +282,72 @@ __device__ __forceinline__ void zf_block(const StageJobs& P, int64_t zb, float* 
   __syncthreads();
   for (int k = threadIdx.x; k < T - 1; k += RX_NT) {
     const int jhi = (int)min<int64_t>(T - 1, nu + k);
-    double acc = 0.0;
-    int i = 0;
-    for (int j = k + U; j <= jhi; j += U, ++i) acc = fma(bs[j], us[i], acc);
+    // four independent partial sums: a single accumulator is a chain of up to T-1
+    // dependent f64 FMAs, each behind an LDS read (~7 us per launch at T = 151)
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int j = k + U, i = 0;
+    for (; j + 3 * U <= jhi; j += 4 * U, i += 4) {
+      a0 = fma(bs[j], us[i], a0);
+      a1 = fma(bs[j + U], us[i + 1], a1);
+      a2 = fma(bs[j + 2 * U], us[i + 2], a2);
+      a3 = fma(bs[j + 3 * U], us[i + 3], a3);
+    }
+    for (; j <= jhi; j += U, ++i) a0 = fma(bs[j], us[i], a0);
+    double acc = (a0 + a1) + (a2 + a3);
     if (zi != nullptr && nu + k < T - 1) acc += zi[nu + k];
     zf[k] = acc;
+  }
+}
+
+// I/Q final states of one stream (the iq_zf_kernel of fe.hip as workgroups of stage A):
+//   zf[k] = sum_{j=k+1}^{T-1} b[j] x[n-1-(j-k-1)] + (n+k < T-1 ? zi[n+k] : 0)
+// and the demod phase state.
+__device__ __forceinline__ void fe_state_block(const FeState& F, int s, float* lds) {
+  float2* xs = reinterpret_cast<float2*>(lds);                  // xs[i] = x[n-1-i]
+  double* bs = reinterpret_cast<double*>(lds + 2 * SDR_MAX_TAPS);
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)s * F.stride;
+  const int L = (int)min<int64_t>(F.n, F.T - 1);
+  for (int i = t; i < L; i += RX_NT) {
+    const int64_t k = base + F.n - 1 - i;
+    if (F.u8) {
+      const uint8_t* q = static_cast<const uint8_t*>(F.iq) + 2 * k;
+      xs[i] = make_float2(((float)q[0] - 128.f) / 128.f, ((float)q[1] - 128.f) / 128.f);
+    } else {
+      xs[i] = static_cast<const float2*>(F.iq)[k];
+    }
+  }
+  for (int i = t; i < F.T; i += RX_NT) bs[i] = F.b[i];
+  __syncthreads();
+  const double* zii = F.zi_i + (int64_t)s * F.zs;
+  const double* ziq = F.zi_q + (int64_t)s * F.zs;
+  for (int k = t; k < F.T - 1; k += RX_NT) {
+    const int jhi = (int)min<int64_t>(F.T - 1, F.n + k);
+    double si0 = 0.0, sq0 = 0.0, si1 = 0.0, sq1 = 0.0;   // two partial sums per channel
+    int j = k + 1;
+    for (; j + 1 <= jhi; j += 2) {
+      const float2 v0 = xs[j - k - 1], v1 = xs[j - k];
+      si0 = fma(bs[j], (double)v0.x, si0);
+      sq0 = fma(bs[j], (double)v0.y, sq0);
+      si1 = fma(bs[j + 1], (double)v1.x, si1);
+      sq1 = fma(bs[j + 1], (double)v1.y, sq1);
+    }
+    if (j <= jhi) {
+      const float2 v = xs[j - k - 1];
+      si0 = fma(bs[j], (double)v.x, si0);
+      sq0 = fma(bs[j], (double)v.y, sq0);
+    }
+    double si = si0 + si1, sq = sq0 + sq1;
+    if (F.n + k < F.T - 1) {
+      si += zii[F.n + k];
+      sq += ziq[F.n + k];
+    }
+    F.zf_i[(int64_t)s * F.zs + k] = si;
+    F.zf_q[(int64_t)s * F.zs + k] = sq;
+  }
+  if (t == 0 && F.n > 0) {                     // model/fmSupportLib.py:40-44: accumulated phase
+    F.phase[s] = (double)F.last_phi[s] + 6.28318530717958647692 * (double)F.wraps[s];
+    F.wraps[s] = 0;
   }
 }
 
@@ -275,7 +359,9 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
   __shared__ __attribute__((aligned(16))) float lds[RX_LDS];
   const int64_t b = blockIdx.x;
   if (b >= P.tile_blocks) {
-    zf_block(P, b - P.tile_blocks, lds);
+    const int64_t zb = b - P.tile_blocks;
+    if (zb < (int64_t)P.nzf * P.nstreams) zf_block(P, zb, lds);
+    else fe_state_block(P.fe, (int)(zb - (int64_t)P.nzf * P.nstreams), lds);
     return;
   }
   int q = 0;
@@ -297,8 +383,9 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
 }
 
 // Launch the jobs of one stage, one launch per tap-count class.
-hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st) {
+hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const FeState* fe = nullptr) {
   auto cls = [](const StageJob& j) { return (j.kind == JK_FIR && (j.T == 101 || j.T == 151)) ? j.T : 0; };
+  bool fe_done = fe == nullptr || !fe->on;
   for (int key : {151, 101, 0}) {
     StageJobs P{};
     P.nstreams = S;
@@ -314,9 +401,13 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st) {
       if (j.zf != nullptr && j.T > 1) P.zfj[P.nzf++] = P.njobs;
       P.j[P.njobs++] = j;
     }
-    if (P.njobs == 0) continue;
+    if (P.njobs == 0 && (fe_done || key != 0)) continue;
+    if (!fe_done) {                       // the FE state rides on the first launch
+      P.fe = *fe;
+      fe_done = true;
+    }
     P.tile_blocks = blocks;
-    const int64_t grid = blocks + (int64_t)P.nzf * S;
+    const int64_t grid = blocks + (int64_t)P.nzf * S + (P.fe.on ? S : 0);
     if (grid <= 0) continue;
     if (grid > 0x7fffffff) return hipErrorInvalidValue;
     if (key == 151) hipLaunchKernelGGL(rx_stage_kernel<151>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
@@ -355,11 +446,17 @@ struct sdr_rx {
   int64_t zoff[Z_N] = {}, zlen[Z_N] = {};
   int64_t bank_len = 0;
   double* phase = nullptr;             // demod prev_phase per stream
+  int* wraps = nullptr;                // FE kernel scratch: per-block wrap count, last phase
+  float* last_phi = nullptr;
   double* pll_state[2] = {};           // 6 per stream (stereo, RDS)
   double* theta = nullptr;             // PLL phases: 2 x S rows of ths
   int64_t ths = 0;
   void* iq_dev = nullptr;              // host-path upload buffer
   size_t iq_cap = 0;
+  void* pin_in = nullptr;              // pinned host staging (sdr_rx_run)
+  size_t pin_in_cap = 0;
+  float* pin_out = nullptr;
+  size_t pin_out_cap = 0;
   int parity = 0;
   int64_t blocks = 0;
   bool timing = false;                 // events between the stages of each block
@@ -453,7 +550,7 @@ int rx_finalize(sdr_rx* r) {
   r->bank_len = zl;
   r->ths = round_up(M, 2) + 2;
   const int64_t S2 = round_up(S, 2);                 // keeps the phase rows 16-B aligned
-  const int64_t doubles = 2 * zl + S2 + 2 * 6 * S2 + 2 * S * r->ths;
+  const int64_t doubles = 2 * zl + 3 * S2 + 2 * 6 * S2 + 2 * S * r->ths;
   const size_t bytes = (size_t)floats * 4 + 64 + (size_t)doubles * 8;
   TRY(set_dev(r->c));
   hipError_t e = hipMalloc(&r->mem, bytes);
@@ -465,7 +562,9 @@ int rx_finalize(sdr_rx* r) {
   r->bank[0] = d;
   r->bank[1] = d + zl;
   r->phase = d + 2 * zl;
-  r->pll_state[0] = r->phase + S2;
+  r->wraps = reinterpret_cast<int*>(r->phase + S2);
+  r->last_phi = reinterpret_cast<float*>(r->phase + 2 * S2);
+  r->pll_state[0] = r->phase + 3 * S2;
   r->pll_state[1] = r->pll_state[0] + 6 * S2;
   r->theta = r->pll_state[1] + 6 * S2;
   r->ready = true;
@@ -505,6 +604,8 @@ void sdr_rx_destroy(sdr_rx* r) {
   }
   if (r->mem) (void)hipFree(r->mem);
   if (r->iq_dev) (void)hipFree(r->iq_dev);
+  if (r->pin_in) (void)hipHostFree(r->pin_in);
+  if (r->pin_out) (void)hipHostFree(r->pin_out);
   for (hipEvent_t e : r->ev)
     if (e) (void)hipEventDestroy(e);
   delete r;
@@ -545,7 +646,8 @@ int sdr_rx_reset(sdr_rx* r) {
   if (!r->ready) return SDR_OK;   // nothing allocated yet: the first block starts from zero
   TRY(set_dev(r->c));
   hipStream_t st = r->c->stream;
-  HIP_TRY(hipMemsetAsync(r->bank[0], 0, sizeof(double) * (size_t)(2 * r->bank_len + r->S), st));
+  // state banks, phases and wrap counters (contiguous)
+  HIP_TRY(hipMemsetAsync(r->bank[0], 0, sizeof(double) * (size_t)(2 * r->bank_len + 2 * round_up(r->S, 2)), st));
   std::vector<double> ps(6 * (size_t)r->S);
   for (int s = 0; s < r->S; ++s) {               // model/fmMonoBlock.py:76, model/fmRDSblock.py:96
     const double init[6] = {0.0, 0.0, 1.0, 0.0, 1.0, 0.0};
@@ -581,11 +683,28 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     if (filter_used(r, f)) TRY(get_taps(c, r->taps[f].data(), (int)r->taps[f].size(), &ts[f]));
   float** o = r->out;
   const int64_t ms = r->out_stride[SDR_RX_O_DEMOD];
-  // FE: RF FIR + decimate + demod, carried zi/zf and phase (fe.hip)
+  // FE: RF FIR + decimate + demod (fe.hip).  The tiled kernels take the reference's RF
+  // configurations; their carried state (I/Q zf, demod phase) is finished by workgroups of
+  // the stage-A launch.  Other configurations run sdr_rf_frontend_dev's generic path.
   const int Trf = (int)r->taps[SDR_RX_F_RF].size();
-  TRY(sdr_rf_frontend_dev(c, iq, r->u8 ? SDR_IQ_U8 : SDR_IQ_F32, r->B, S > 1 ? iq_stride : r->B, 0, S,
-                          r->taps[SDR_RX_F_RF].data(), Trf, r->rf_decim, zin(Z_FE_I), zin(Z_FE_Q), r->zlen[Z_FE_I],
-                          zout(Z_FE_I), zout(Z_FE_Q), r->phase, o[SDR_RX_O_DEMOD], ms, nullptr, nullptr));
+  const int64_t xs = S > 1 ? iq_stride : r->B;
+  const int G = r->u8 ? 8 : 2;
+  const bool fast = (Trf == 101 || Trf == 151) && r->rf_decim == 10 && (S <= 1 || r->u8 || xs % G == 0) &&
+                    ((uintptr_t)iq % (r->u8 ? 4 : 16)) == 0;
+  FeState fst{};
+  if (fast) {
+    const int64_t fstride = S > 1 ? xs : ceil_div(r->B, G) * G;
+    FeLaunch a{iq, r->B, fstride, 0, S, ts[SDR_RX_F_RF]->dev_f32, &ts[SDR_RX_F_RF]->h, Trf, r->rf_decim, r->u8,
+               zin(Z_FE_I), zin(Z_FE_Q), r->zlen[Z_FE_I], r->phase, o[SDR_RX_O_DEMOD], ms, nullptr, nullptr,
+               r->last_phi, r->wraps};
+    HIP_TRY(sdr_launch_fe(a, st));
+    fst = FeState{iq, r->B, xs, ts[SDR_RX_F_RF]->dev_f64, zin(Z_FE_I), zin(Z_FE_Q), zout(Z_FE_I), zout(Z_FE_Q),
+                  r->zlen[Z_FE_I], r->last_phi, r->wraps, r->phase, Trf, r->u8, 1};
+  } else {
+    TRY(sdr_rf_frontend_dev(c, iq, r->u8 ? SDR_IQ_U8 : SDR_IQ_F32, r->B, xs, 0, S, r->taps[SDR_RX_F_RF].data(),
+                            Trf, r->rf_decim, zin(Z_FE_I), zin(Z_FE_Q), r->zlen[Z_FE_I], zout(Z_FE_I), zout(Z_FE_Q),
+                            r->phase, o[SDR_RX_O_DEMOD], ms, nullptr, nullptr));
+  }
   HIP_TRY(mark(1 + SDR_RX_ST_FE));
   auto fir = [&](int f, int z, const float* x, int64_t n, int64_t xs, float* y, int64_t ys, int D, int pre = PRE_NONE,
                  const float* cmix = nullptr) {
@@ -609,7 +728,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     A.push_back(fir(SDR_RX_F_STEREO_BPF, Z_BAND, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_BPF_EXTRACTION], ms, 1));
   }
   if (rd) A.push_back(fir(SDR_RX_F_RDS_EXTRACT, Z_EXTRACT, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_RDS_EXTRACT], ms, 1));
-  HIP_TRY(launch_stage(A, S, st));
+  HIP_TRY(launch_stage(A, S, st, &fst));
   HIP_TRY(mark(1 + SDR_RX_ST_A));
   // stage B: RDS squaring non-linearity + BPF (model/fmRDSblock.py:161-164)
   if (rd) HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_SQUARE, Z_SQUARE, o[SDR_RX_O_RDS_EXTRACT], M, ms,
@@ -673,28 +792,86 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   return SDR_OK;
 }
 
+namespace {
+// grow a device buffer / a pinned host buffer (synchronising first: work in flight may use it)
+int grow_dev(sdr_rx* r, void** p, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return SDR_OK;
+  if (*p) {
+    HIP_TRY(hipStreamSynchronize(r->c->stream));
+    HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+  }
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx: hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  *cap = bytes;
+  return SDR_OK;
+}
+int grow_pinned(sdr_rx* r, void** p, size_t* cap, size_t bytes) {
+  if (*cap >= bytes) return SDR_OK;
+  if (*p) {
+    HIP_TRY(hipStreamSynchronize(r->c->stream));
+    HIP_TRY(hipHostFree(*p));
+    *p = nullptr;
+    *cap = 0;
+  }
+  hipError_t e = hipHostMalloc(p, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx: hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  *cap = bytes;
+  return SDR_OK;
+}
+}  // namespace
+
 int sdr_rx_process(sdr_rx* r, const void* iq_host, int64_t iq_stride) {
+  return sdr_rx_run(r, iq_host, iq_stride, 0, nullptr, nullptr, nullptr);
+}
+
+// One block from host memory: the IQ goes through pinned staging to the device, the chain
+// runs, every requested output comes back through pinned staging, and the call waits once.
+int sdr_rx_run(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, const int* which, float* const* out,
+               const int64_t* out_stride) {
   if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
-  if (iq_host == nullptr) return fail(SDR_EINVAL, "sdr_rx_process: iq is NULL");
-  if (r->S > 1 && iq_stride < r->B) return fail(SDR_EINVAL, "sdr_rx_process: iq_stride %lld < block", (long long)iq_stride);
+  if (iq_host == nullptr) return fail(SDR_EINVAL, "sdr_rx_run: iq is NULL");
+  if (r->S > 1 && iq_stride < r->B) return fail(SDR_EINVAL, "sdr_rx_run: iq_stride %lld < block", (long long)iq_stride);
+  if (nout < 0 || (nout > 0 && (which == nullptr || out == nullptr))) return fail(SDR_EINVAL, "sdr_rx_run: outputs");
+  if (!r->ready) TRY(rx_finalize(r));
+  for (int i = 0; i < nout; ++i) {
+    if (which[i] < 0 || which[i] >= SDR_RX_NOUTPUTS || !need_out(r, which[i]))
+      return fail(SDR_EINVAL, "sdr_rx_run: output %d is not produced by flags 0x%x", which[i], r->flags);
+    if (out[i] == nullptr) return fail(SDR_EINVAL, "sdr_rx_run: output buffer %d is NULL", i);
+    if (r->S > 1 && out_stride && out_stride[i] < r->out_n[which[i]])
+      return fail(SDR_EINVAL, "sdr_rx_run: out_stride[%d] too small", i);
+  }
   TRY(set_dev(r->c));
+  hipStream_t st = r->c->stream;
   const int64_t es = r->u8 ? 2 : 8;                      // bytes per complex sample
   const int64_t xs = r->S > 1 ? iq_stride : r->B;
   const size_t bytes = (size_t)(xs * (r->S - 1) + r->B) * es;
-  if (r->iq_cap < bytes) {
-    if (r->iq_dev) {
-      HIP_TRY(hipStreamSynchronize(r->c->stream));
-      HIP_TRY(hipFree(r->iq_dev));
-      r->iq_dev = nullptr;
-      r->iq_cap = 0;
-    }
-    hipError_t e = hipMalloc(&r->iq_dev, bytes);
-    if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx_process: hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
-    r->iq_cap = bytes;
-  }
-  HIP_TRY(hipMemcpyAsync(r->iq_dev, iq_host, bytes, hipMemcpyHostToDevice, r->c->stream));
+  size_t obytes = 0;
+  for (int i = 0; i < nout; ++i) obytes += sizeof(float) * (size_t)(r->out_n[which[i]] * r->S);
+  TRY(grow_dev(r, &r->iq_dev, &r->iq_cap, bytes));
+  TRY(grow_pinned(r, &r->pin_in, &r->pin_in_cap, bytes));
+  TRY(grow_pinned(r, reinterpret_cast<void**>(&r->pin_out), &r->pin_out_cap, std::max<size_t>(obytes, 16)));
+  // (one DMA: a chunked copy overlapping the host memcpy turns into per-chunk blit kernels)
+  std::memcpy(r->pin_in, iq_host, bytes);
+  HIP_TRY(hipMemcpyAsync(r->iq_dev, r->pin_in, bytes, hipMemcpyHostToDevice, st));
   TRY(sdr_rx_process_dev(r, r->iq_dev, xs));
-  HIP_TRY(hipStreamSynchronize(r->c->stream));
+  size_t off = 0;
+  for (int i = 0; i < nout; ++i) {
+    const int o = which[i];
+    const int64_t n = r->out_n[o];
+    HIP_TRY(hipMemcpy2DAsync(r->pin_out + off, sizeof(float) * (size_t)n, r->out[o], sizeof(float) * (size_t)r->out_stride[o],
+                             sizeof(float) * (size_t)n, (size_t)r->S, hipMemcpyDeviceToHost, st));
+    off += (size_t)(n * r->S);
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  off = 0;
+  for (int i = 0; i < nout; ++i) {
+    const int64_t n = r->out_n[which[i]];
+    const int64_t os = (r->S > 1 && out_stride) ? out_stride[i] : n;
+    for (int s = 0; s < r->S; ++s) std::memcpy(out[i] + s * os, r->pin_out + off + s * n, sizeof(float) * (size_t)n);
+    off += (size_t)(n * r->S);
+  }
   return SDR_OK;
 }
 
