@@ -275,8 +275,15 @@ int sdr_dft(sdr_ctx* ctx, const double* x, int64_t n, double* X);
  * The state (offset, start position, lone symbol, previous bit, carried bits, positions)
  * lives in the sdr_rds_link object; one object per stream.  No GPU is used. */
 typedef struct sdr_rds_link sdr_rds_link;
+enum { SDR_RDS_RESYNC = 4 };   /* event type of a re-sync (only with sdr_rds_link_set_resync) */
 int sdr_rds_link_create(sdr_rds_link** out);
 void sdr_rds_link_destroy(sdr_rds_link* link);
+/* The C++ frame_thread's re-sync rule (src/fm_radio.cpp:697-704): after more than
+ * `after_bad_syncs` false-positive syndromes since the last accepted one, forget the frame
+ * position (the next syndrome is accepted) and emit an SDR_RDS_RESYNC event.  0 (default):
+ * off, as the Python model (model/fmRDSblock.py:299-341), which has no such rule; the C++
+ * uses 10. */
+int sdr_rds_link_set_resync(sdr_rds_link* link, int after_bad_syncs);
 int sdr_rds_link_block(sdr_rds_link* link, const double* rrc_i, int64_t n, int64_t* events,
                        int64_t max_events, int64_t* n_events, double* symbols, int64_t max_symbols,
                        int64_t* n_symbols, uint8_t* bits, int64_t max_bits, int64_t* n_bits,

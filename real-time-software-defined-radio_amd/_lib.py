@@ -98,6 +98,7 @@ SIGNATURES = {
     "sdr_rx_stage_ms": (_i32, [_vp, _fp]),
     "sdr_rds_link_create": (_i32, [_c.POINTER(_vp)]),
     "sdr_rds_link_destroy": (None, [_vp]),
+    "sdr_rds_link_set_resync": (_i32, [_vp, _i32]),
     "sdr_rds_link_block": (_i32, [_vp, _dp, _i64, _vp, _i64, _c.POINTER(_i64), _vp, _i64, _c.POINTER(_i64),
                                   _vp, _i64, _c.POINTER(_i64), _vp, _i64, _c.POINTER(_i64)]),
 }

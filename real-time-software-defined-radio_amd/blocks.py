@@ -238,14 +238,20 @@ class RdsLinkLayer:
     prints (1) or its "False positive" prints (0); the state carries across calls."""
 
     TYPES = "ABCD"
+    RESYNC = 4
 
-    def __init__(self):
+    def __init__(self, resync_after: int = 0):
+        """resync_after > 0: the C++ frame_thread's rule (src/fm_radio.cpp:697-704; it uses
+        10) -- after that many false positives in a row the frame position is forgotten and a
+        (RESYNC, position, 0) event is reported.  0: the Python model's behaviour."""
         import ctypes
         self._c = ctypes
         self.lib = _lib.load_library()
         h = ctypes.c_void_p()
         check(self.lib.sdr_rds_link_create(ctypes.byref(h)), "sdr_rds_link_create")
         self.handle = h
+        if resync_after:
+            check(self.lib.sdr_rds_link_set_resync(h, int(resync_after)), "sdr_rds_link_set_resync")
 
     def process(self, rrc_i):
         c = self._c

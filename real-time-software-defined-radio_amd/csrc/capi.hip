@@ -748,6 +748,7 @@ int sdr_mono_block(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, const do
 struct sdr_rds_link {
   int64_t block_count = 0, int_offset = 0, printposition = 0, last_position = -1;
   int start_pos = 0, front_bit = 0, prebit = 0;
+  int resync_after = 0, bad_sync = 0;     // C++ frame_thread re-sync rule (0: off, as the Python model)
   double lonely_bit = 0.0;
   std::vector<uint8_t> prev_sync_bits;
 };
@@ -776,6 +777,12 @@ int sdr_rds_link_create(sdr_rds_link** out) {
 }
 
 void sdr_rds_link_destroy(sdr_rds_link* l) { delete l; }
+
+int sdr_rds_link_set_resync(sdr_rds_link* l, int after_bad_syncs) {
+  if (!l || after_bad_syncs < 0) return fail(SDR_EINVAL, "sdr_rds_link_set_resync: bad arguments");
+  l->resync_after = after_bad_syncs;
+  return SDR_OK;
+}
 
 int sdr_rds_link_block(sdr_rds_link* l, const double* rrc_i, int64_t n, int64_t* events,
                        int64_t max_events, int64_t* n_events, double* symbols, int64_t max_symbols,
@@ -856,7 +863,18 @@ int sdr_rds_link_block(sdr_rds_link* l, const double* rrc_i, int64_t n, int64_t*
         events[3 * ne + 2] = ok ? 1 : 0;
       }
       ++ne;
+      l->bad_sync = ok ? 0 : l->bad_sync + 1;
       break;
+    }
+    if (l->resync_after > 0 && l->bad_sync > l->resync_after) {   // src/fm_radio.cpp:697-704
+      if (events && ne < max_events) {
+        events[3 * ne] = SDR_RDS_RESYNC;
+        events[3 * ne + 1] = l->printposition;
+        events[3 * ne + 2] = 0;
+      }
+      ++ne;
+      l->bad_sync = 0;
+      l->last_position = -1;
     }
     ++position;
     if (position + 26 > (int64_t)d.size() - 1) break;

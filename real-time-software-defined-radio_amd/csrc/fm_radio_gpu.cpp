@@ -12,11 +12,18 @@
 //
 // Runtime: instead of four threads and a mutex/condvar queue, one host thread and the
 // context's HIP stream with a two-slot pinned ring: while the GPU processes block k
-// (async H2D, kernels, async D2H), the host writes block k-1's audio and reads block k+1.
-// All filter / demod / PLL state stays in device memory between blocks.
+// (async H2D, the receiver's launches, async D2H), the host writes block k-1's audio (and
+// runs its RDS link layer) and reads block k+1.  Mode 0 runs on libsdr's block receiver
+// (sdr_rx: FE, mono, stereo, RDS; every filter / demod / PLL state stays in device memory).
 //
-// Options: --mono (mono only, both channels = mono), --rf-taps N (default 151, the
-// reference's), --blocks N (stop after N blocks), --mode 1 (2.5 MS/s IQ,
+// Options: --mono (mono only, both channels = mono), --rds (also the RDS chain,
+// model/fmRDSblock.py:156-204 on the GPU, and its link layer, :207-346, on the host:
+// clock/data recovery, Manchester and differential decoding and the syndrome frame sync,
+// printing the reference's lines to stderr -- "Syndrome A at position N", "False positive
+// Syndrome A at position N", src/fm_radio.cpp:649-695), --resync (with --rds: the C++
+// frame_thread's re-sync after more than 10 false positives, "~~~~~Re-Sync~~~~~",
+// :697-704; the Python model has no such rule, so it is off by default), --rf-taps N
+// (default 151, the reference's), --blocks N (stop after N blocks), --mode 1 (2.5 MS/s IQ,
 // src/fm_radio.cpp:36; the 250 kS/s IF goes to 48 kHz through the 24/125 resampler with a
 // 6 MHz, 16 kHz filter, :174-180, :228, whose up-gain the reference applies at the int16
 // write, :229, :297; mono only: the reference designs its mode-1 pilot/stereo band-passes
@@ -31,6 +38,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "../../include/sdr.h"
@@ -75,6 +83,27 @@ std::vector<double> firwin(int n, double lo, double hi) {   // lo = 0: low-pass 
   return h;
 }
 
+// model/fmRRC.py:12-47 (impulseResponseRootRaisedCosine): roll-off 0.90 at 2375 symbols/s,
+// t = (k - N/2)/Fs, the reference's three cases (t = 0, |t| = Ts/(4 beta), general).
+std::vector<double> rrc(double fs, int n) {
+  const double ts = 1.0 / 2375.0, beta = 0.90;
+  std::vector<double> h(n);
+  for (int k = 0; k < n; ++k) {
+    const double t = (k - n / 2.0) / fs;
+    if (t == 0.0) {
+      h[k] = 1.0 + beta * (4 / M_PI - 1);
+    } else if (t == -ts / (4 * beta) || t == ts / (4 * beta)) {
+      const double q = M_PI / (4 * beta);
+      h[k] = beta / std::sqrt(2.0) * ((1 + 2 / M_PI) * std::sin(q) + (1 - 2 / M_PI) * std::cos(q));
+    } else {
+      const double x = 4 * beta * t / ts;
+      h[k] = (std::sin(M_PI * t * (1 - beta) / ts) + x * std::cos(M_PI * t * (1 + beta) / ts)) /
+             (M_PI * t * (1 - x * x) / ts);
+    }
+  }
+  return h;
+}
+
 struct Dev {
   sdr_ctx* c;
   void* alloc(int64_t bytes) {
@@ -88,17 +117,19 @@ struct Dev {
 }  // namespace
 
 int main(int argc, char** argv) {
-  bool mono = false, print_taps = false;
+  bool mono = false, print_taps = false, rds = false, resync = false;
   int rf_taps = 151, mode = 0;
   long long max_blocks = -1;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--mono")) mono = true;
+    else if (!std::strcmp(argv[i], "--rds")) rds = true;
+    else if (!std::strcmp(argv[i], "--resync")) resync = true;
     else if (!std::strcmp(argv[i], "--print-taps")) print_taps = true;
     else if (!std::strcmp(argv[i], "--rf-taps") && i + 1 < argc) rf_taps = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--blocks") && i + 1 < argc) max_blocks = std::atoll(argv[++i]);
     else if (!std::strcmp(argv[i], "--mode") && i + 1 < argc) mode = std::atoi(argv[++i]);
     else {
-      std::fprintf(stderr, "usage: fm_radio_gpu [--mode 0|1] [--mono] [--rf-taps N] [--blocks N] "
+      std::fprintf(stderr, "usage: fm_radio_gpu [--mode 0|1] [--mono] [--rds [--resync]] [--rf-taps N] [--blocks N] "
                            "[--print-taps] < iq_u8 > pcm_s16le_stereo\n");
       return 2;
     }
@@ -108,6 +139,10 @@ int main(int argc, char** argv) {
     return 2;
   }
   if (mode == 1) mono = true;
+  if (mode == 1 && rds) {
+    std::fprintf(stderr, "fm_radio_gpu: --rds is a mode-0 feature (src/fm_radio.cpp:321-324)\n");
+    return 2;
+  }
   if (rf_taps < 3 || rf_taps > SDR_MAX_TAPS_ABI) {
     std::fprintf(stderr, "fm_radio_gpu: --rf-taps %d out of range\n", rf_taps);
     return 2;
@@ -122,8 +157,14 @@ int main(int argc, char** argv) {
   const std::vector<double> pil_b = firwin(151, 18.5e3 / 120e3, 19.5e3 / 120e3);
   const std::vector<double> ext_b = firwin(151, 22e3 / 120e3, 54e3 / 120e3);
   const std::vector<double> ste_b = firwin(151, 0.0, 16e3 / 120e3);
+  // RDS (model/fmRDSblock.py:88-111)
+  const std::vector<double> rex_b = firwin(151, 54e3 / 120e3, 60e3 / 120e3);
+  const std::vector<double> rsq_b = firwin(151, 113.5e3 / 120e3, 114.5e3 / 120e3);
+  const std::vector<double> rlp_b = firwin(151, 0.0, 3e3 / 120e3);
+  const std::vector<double> ran_b = firwin(151, 0.0, (57000.0 / 2) / ((240000.0 * 19) / 2));
+  const std::vector<double> rrc_b = rrc(57000.0, 151);
   if (print_taps) {                    // (no GPU) one line per filter, for the design test
-    for (const auto* t : {&rf_b, &au_b, &pil_b, &ext_b, &ste_b, &m1_b}) {
+    for (const auto* t : {&rf_b, &au_b, &pil_b, &ext_b, &ste_b, &m1_b, &rex_b, &rsq_b, &rlp_b, &ran_b, &rrc_b}) {
       for (size_t k = 0; k < t->size(); ++k) std::printf(k ? " %.17g" : "%.17g", (*t)[k]);
       std::printf("\n");
     }
@@ -138,24 +179,12 @@ int main(int argc, char** argv) {
   const int64_t A = mode == 1 ? M * kUp / kDown : M / 5;     // audio samples written per block
   const int64_t AY = mode == 1 ? (M * kUp + kDown - 1) / kDown : A;   // resampler outputs
 
-  // device state and intermediates (persist across blocks)
+  // device buffers of mode 1 (mode 0 runs on the receiver's own)
   auto* d_iq = static_cast<uint8_t*>(d.alloc(2 * kBlock));
   auto* rf_st = static_cast<double*>(d.alloc(8 * (2 * Z + 1)));    // zi_i | zi_q | phase
   auto* d_dm = static_cast<float*>(d.alloc(4 * M + 16));
   auto* d_au = static_cast<float*>(d.alloc(4 * AY + 16));
-  auto* zi_au = static_cast<double*>(d.alloc(8 * (mode == 1 ? kM1Taps - 1 : 150)));
-  auto* zi_pil = static_cast<double*>(d.alloc(8 * 150));
-  auto* zi_ext = static_cast<double*>(d.alloc(8 * 150));
-  auto* zi_ste = static_cast<double*>(d.alloc(8 * 150));
-  auto* d_bpr = static_cast<float*>(d.alloc(4 * M + 16));
-  auto* d_bpe = static_cast<float*>(d.alloc(4 * M + 16));
-  auto* d_nco = static_cast<float*>(d.alloc(4 * (M + 1) + 16));
-  auto* d_st = static_cast<float*>(d.alloc(4 * A + 16));
-  auto* d_l = static_cast<float*>(d.alloc(4 * A + 16));
-  auto* d_r = static_cast<float*>(d.alloc(4 * A + 16));
-  auto* pll = static_cast<double*>(d.alloc(8 * 6));
-  const double pll0[6] = {0.0, 0.0, 1.0, 0.0, 1.0, 0.0};             // model/fmMonoBlock.py:76
-  hk(hipMemcpyAsync(pll, pll0, sizeof pll0, hipMemcpyHostToDevice, st), "pll state");   // after the memsets
+  auto* zi_au = static_cast<double*>(d.alloc(8 * (kM1Taps - 1)));  // mode 1
   hk(hipStreamSynchronize(st), "hipStreamSynchronize");
 
   // two-slot pinned ring
@@ -188,45 +217,91 @@ int main(int argc, char** argv) {
     return true;
   };
 
+  // mode 0: the block receiver (sdr_rx)
+  sdr_rx* rx = nullptr;
+  sdr_rds_link* link = nullptr;
+  const float *o_l = nullptr, *o_r = nullptr, *o_rrc = nullptr;
+  int64_t nrrc = 0;
+  if (mode == 0) {
+    const int flags = SDR_RX_AUDIO | (mono ? 0 : SDR_RX_STEREO) | (rds ? SDR_RX_RDS : 0);
+    ck(sdr_rx_create(c, 1, kBlock, SDR_IQ_U8, flags, &rx), "sdr_rx_create");
+    const std::pair<int, const std::vector<double>*> taps[] = {
+        {SDR_RX_F_RF, &rf_b}, {SDR_RX_F_AUDIO, &au_b}, {SDR_RX_F_PILOT, &pil_b}, {SDR_RX_F_STEREO_BPF, &ext_b},
+        {SDR_RX_F_STEREO_LPF, &ste_b}, {SDR_RX_F_RDS_EXTRACT, &rex_b}, {SDR_RX_F_RDS_SQUARE, &rsq_b},
+        {SDR_RX_F_RDS_LPF, &rlp_b}, {SDR_RX_F_RDS_ANTI, &ran_b}, {SDR_RX_F_RDS_RRC, &rrc_b}};
+    for (const auto& f : taps) ck(sdr_rx_set_filter(rx, f.first, f.second->data(), (int)f.second->size()), "taps");
+    float* p;
+    int64_t stride, n;
+    ck(sdr_rx_output(rx, mono ? SDR_RX_O_AUDIO : SDR_RX_O_LEFT, &p, &stride, &n), "output");
+    o_l = p;
+    ck(sdr_rx_output(rx, mono ? SDR_RX_O_AUDIO : SDR_RX_O_RIGHT, &p, &stride, &n), "output");
+    o_r = p;
+    if (rds) {
+      ck(sdr_rx_output(rx, SDR_RX_O_RDS_RRC_I, &p, &stride, &nrrc), "output");
+      o_rrc = p;
+      ck(sdr_rds_link_create(&link), "sdr_rds_link_create");
+      if (resync) ck(sdr_rds_link_set_resync(link, 10), "sdr_rds_link_set_resync");   // :697
+    }
+  }
+  float* h_rrc[2] = {nullptr, nullptr};
+  std::vector<double> rrc_d(nrrc);
+  std::vector<int64_t> ev(3 * (nrrc / 24 + 128));
+  if (rds)
+    for (int s2 = 0; s2 < 2; ++s2)
+      hk(hipHostMalloc(reinterpret_cast<void**>(&h_rrc[s2]), 4 * nrrc, hipHostMallocDefault), "hipHostMalloc");
+  // the RDS link layer of the block in slot `slot` (host, after its D2H landed): the
+  // reference's stderr lines (src/fm_radio.cpp:649-704)
+  auto link_block = [&](int slot) {
+    for (int64_t i = 0; i < nrrc; ++i) rrc_d[i] = h_rrc[slot][i];
+    int64_t ne = 0;
+    ck(sdr_rds_link_block(link, rrc_d.data(), nrrc, ev.data(), (int64_t)ev.size() / 3, &ne, nullptr, 0, nullptr,
+                          nullptr, 0, nullptr, nullptr, 0, nullptr), "RDS link layer");
+    for (int64_t e = 0; e < ne; ++e) {
+      const int64_t typ = ev[3 * e], pos = ev[3 * e + 1], ok = ev[3 * e + 2];
+      if (typ == SDR_RDS_RESYNC) std::fprintf(stderr, "~~~~~Re-Sync~~~~~\n");
+      else std::fprintf(stderr, "%sSyndrome %c at position %lld\n", ok ? "" : "False positive ", (char)('A' + typ),
+                        (long long)pos);
+    }
+  };
+
   long long k = 0;
   int pending = -1;                    // slot whose audio is still to be written
+  auto finish = [&](int slot) {
+    emit(slot);
+    if (link) link_block(slot);
+  };
   while ((max_blocks < 0 || k < max_blocks) && read_block(h_in[k & 1])) {
     const int slot = (int)(k & 1);
     hk(hipMemcpyAsync(d_iq, h_in[slot], 2 * kBlock, hipMemcpyHostToDevice, st), "H2D");
-    ck(sdr_rf_frontend_dev(c, d_iq, SDR_IQ_U8, kBlock, kBlock, 0, 1, rf_b.data(), rf_taps, 10, rf_st,
-                           rf_st + Z, Z, rf_st, rf_st + Z, rf_st + 2 * Z, d_dm, M, nullptr, nullptr),
-       "front end");                                                  // :86-98
-    if (mode == 1)                                                    // src/fm_radio.cpp:228
-      ck(sdr_resample_dev(c, d_dm, M, m1_b.data(), kM1Taps, kUp, kDown, zi_au, zi_au, d_au), "mode-1 resampler");
-    else
-      ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, au_b.data(), 151, 5, zi_au, 150, zi_au,
-                     d_au, A), "mono");                               // :101-109
     const float* out_l = d_au;
     const float* out_r = d_au;
-    if (!mono) {
-      ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, pil_b.data(), 151, 1, zi_pil, 150,
-                     zi_pil, d_bpr, M), "pilot BPF");                 // :115-117
-      ck(sdr_pll_dev(c, d_bpr, M, M, 1, 19e3, 240e3, 2.0, 0.0, 0.01, pll, d_nco, nullptr, M + 1), "PLL");  // :119
-      ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, ext_b.data(), 151, 1, zi_ext, 150,
-                     zi_ext, d_bpe, M), "stereo BPF");                // :150-151
-      ck(sdr_fir_dev(c, d_bpe, d_nco, 2.f, SDR_PRE_MIX, M, M, 0, 1, ste_b.data(), 151, 5, zi_ste, 150,
-                     zi_ste, d_st, A), "stereo LPF");                 // :155-162
-      ck(sdr_stereo_combine_dev(c, d_au, d_st, A, d_l, d_r), "combine");   // :166-170
-      out_l = d_l;
-      out_r = d_r;
+    if (mode == 0) {
+      ck(sdr_rx_process_dev(rx, d_iq, kBlock), "receiver");           // fmMonoBlock.py:86-173 (+ RDS)
+      out_l = o_l;
+      out_r = o_r;
+    } else {
+      ck(sdr_rf_frontend_dev(c, d_iq, SDR_IQ_U8, kBlock, kBlock, 0, 1, rf_b.data(), rf_taps, 10, rf_st,
+                             rf_st + Z, Z, rf_st, rf_st + Z, rf_st + 2 * Z, d_dm, M, nullptr, nullptr),
+         "front end");
+      ck(sdr_resample_dev(c, d_dm, M, m1_b.data(), kM1Taps, kUp, kDown, zi_au, zi_au, d_au), "mode-1 resampler");
     }
     if (pending >= 0) {                // before reusing this slot's output buffer
-      emit(pending);
+      finish(pending);
       pending = -1;
     }
     hk(hipMemcpyAsync(h_out[slot], out_l, 4 * A, hipMemcpyDeviceToHost, st), "D2H");
     hk(hipMemcpyAsync(h_out[slot] + A, out_r, 4 * A, hipMemcpyDeviceToHost, st), "D2H");
+    if (rds) hk(hipMemcpyAsync(h_rrc[slot], o_rrc, 4 * nrrc, hipMemcpyDeviceToHost, st), "D2H");
     hk(hipEventRecord(done[slot], st), "hipEventRecord");
     pending = slot;
     ++k;
   }
-  if (pending >= 0) emit(pending);
+  if (pending >= 0) finish(pending);
   std::fflush(stdout);
+  if (link) sdr_rds_link_destroy(link);
+  if (rx) sdr_rx_destroy(rx);
+  for (float* p : h_rrc)
+    if (p) (void)hipHostFree(p);
   for (int s = 0; s < 2; ++s) {
     (void)hipHostFree(h_in[s]);
     (void)hipHostFree(h_out[s]);

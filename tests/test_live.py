@@ -30,9 +30,11 @@ def test_taps_match_firwin(sdr):
     pil, ext, ste = sdr.design.stereo_coeffs(151)
     from scipy import signal
     m1 = signal.firwin(3623, 16e3 / 3e6, window="hann")          # mode-1 resampler filter
-    assert len(rows) == 6
-    for got, ref in zip(rows, (rf, au, pil, ext, ste, m1)):
-        assert got.shape == ref.shape and np.max(np.abs(got - ref)) < 1e-15
+    co = sdr.design.rds_coeffs(151)                                # model/fmRDSblock.py:88-111
+    assert len(rows) == 11
+    for got, ref in zip(rows, (rf, au, pil, ext, ste, m1, co["extract"], co["square"], co["lpf"], co["anti_img"],
+                               co["rrc"])):
+        assert got.shape == ref.shape and np.max(np.abs(got - ref)) < 1e-14 * max(1.0, np.max(np.abs(ref)))
 
 
 def test_usage_error_exit_code():
@@ -110,3 +112,66 @@ def test_live_pipeline_mode1(sdr, gpu_ctx, oracle):
     o = np.concatenate(ora)
     dd = np.abs(pcm.astype(np.int32) - to_pcm(o, o))
     assert dd.max() <= 1 and np.mean(dd > 0) < 0.01
+
+
+def _syndrome_lines(stderr):
+    import re
+    out = []
+    for line in stderr.decode().splitlines():
+        m = re.fullmatch(r"(False positive )?Syndrome ([ABCD]) at position (\d+)", line)
+        if m:
+            out.append(("ABCD".index(m.group(2)), int(m.group(3)), 0 if m.group(1) else 1))
+        elif line == "~~~~~Re-Sync~~~~~":
+            out.append((4, -1, 0))
+    return out
+
+
+@pytest.mark.gpu
+def test_live_pipeline_rds_prints_reference_syndromes(sdr, gpu_ctx, golden):
+    """--rds: the rds_link.npz IQ (synthetic, coded RDS groups) piped through the binary;
+    its stderr syndrome lines == the reference script's own prints (make_rds_link_golden.py,
+    model/fmRDSblock.py run as __main__), in the C++ frame_thread's wording
+    (src/fm_radio.cpp:649-695).  The audio is unchanged by the RDS chain."""
+    z = golden("rds_link.npz")
+    iq = sdr.synth.fm_iq(int(z["n_complex"]), seed=int(z["seed"]), dtype=np.uint8, rds_groups=True)
+    nb = len(z["rrc_i"])
+    res = subprocess.run([BIN, "--rds", "--blocks", str(nb)], input=iq.tobytes(), capture_output=True, check=True,
+                         timeout=120)
+    assert _syndrome_lines(res.stderr) == [tuple(int(v) for v in e) for e in z["events"]]
+    plain = subprocess.run([BIN, "--blocks", str(nb)], input=iq.tobytes(), capture_output=True, check=True,
+                           timeout=120)
+    assert res.stdout == plain.stdout
+
+
+@pytest.mark.gpu
+def test_live_pipeline_rds_resync(sdr, gpu_ctx):
+    """--resync: the C++ re-sync rule (src/fm_radio.cpp:697-704) on a stream without RDS
+    groups, where every syndrome match is noise: a "~~~~~Re-Sync~~~~~" line after every
+    11th consecutive false positive, after which the next match is accepted.  Random windows
+    match a syndrome ~0.3 times per block, so 120 blocks (7.7 s of radio) re-sync a few times."""
+    nb = 120
+    iq = sdr.synth.fm_iq(nb * B, seed=21, dtype=np.uint8)
+    res = subprocess.run([BIN, "--rds", "--resync", "--mono"], input=iq.tobytes(), capture_output=True, check=True,
+                         timeout=120)
+    ev = _syndrome_lines(res.stderr)
+    bad = 0
+    expect_accept = True
+    for typ, pos, ok in ev:
+        if typ == 4:
+            assert bad == 11
+            bad = 0
+            expect_accept = True
+            continue
+        if expect_accept:
+            assert ok == 1
+            expect_accept = False
+        bad = 0 if ok else bad + 1
+        assert bad <= 11
+    assert any(e[0] == 4 for e in ev)
+    link = sdr.RdsLinkLayer(resync_after=10)
+    proc = sdr.RdsBlockProcessor(B)
+    ref = []
+    for k in range(nb):
+        for typ, pos, ok in link.process(proc.process(iq[2 * k * B:2 * (k + 1) * B])["rrc_i"])["events"]:
+            ref.append((typ, -1 if typ == 4 else pos, ok))
+    assert ev == ref
