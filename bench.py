@@ -290,12 +290,18 @@ def main():
         stage_ms = [tm.elapsed_ms(ev[0][0], ev[0][1]) / args.steps]
     k_avg = stage_ms[0]                              # the dominant (first) kernel of the step
     bpc = 2 if args.iq == "u8" else 8
-    if args.path == "fused":
+    if args.path == "fused" and lib.sdr_fe_mono_fused(T, 10, TA, 5):
         # compulsory HBM bytes of the fused kernel: IQ in + audio out
         k_bytes = n * bpc + A * 4
         kname = (f"fe_slot_kernel<{args.taps},fused,u8>" if args.iq == "u8" else f"fe_ring_kernel<{args.taps},fused>") + \
             f" (sdr_fe_mono_dev: FE {args.taps} taps + audio {args.audio_taps} taps)"
         kernels = {"fe_mono": round(k_avg, 5)}
+    elif args.path == "fused":
+        # sdr_fe_mono_dev runs its two-kernel path here (sdr_fe_mono_fused == 0): the timed
+        # launch pair moves the demod through HBM too
+        k_bytes = n * bpc + 2 * M * 4 + A * 4
+        kname = f"sdr_fe_mono_dev two-kernel path (FE {args.taps} taps -> demod in HBM -> audio {args.audio_taps} taps)"
+        kernels = {"fe_mono_pair": round(k_avg, 5)}
     else:
         k_bytes = n * bpc + M * 4                    # IQ in + demod out
         kname = f"fe_slot_kernel<{args.taps}{',u8' if args.iq == 'u8' else ''}> (sdr_rf_frontend_dev)"

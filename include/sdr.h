@@ -158,6 +158,9 @@ int sdr_rf_frontend_dev(sdr_ctx* ctx, const void* iq, int iq_dtype, int64_t n, i
  * stream stays on chip (f32 IQ, rf_taps 101/151 at decim 10, audio 151 taps at decim 5);
  * other configurations run the front end into scratch HBM, then the audio filter.
  * audio: nstreams x audio_stride floats, ceil(ceil(n/rf_decim)/audio_decim) per stream. */
+/* 1 if sdr_fe_mono_dev runs the single fused kernel for this configuration (16-B aligned f32
+ * / 4-B aligned u8 IQ rows, even stride), 0 if it runs the front end + audio FIR pair. */
+int sdr_fe_mono_fused(int rf_taps, int rf_decim, int audio_taps, int audio_decim);
 int sdr_fe_mono_dev(sdr_ctx* ctx, const void* iq, int iq_dtype, int64_t n, int64_t stride, int nstreams,
                     const double* rf_b, int rf_taps, int rf_decim, const double* audio_b, int audio_taps,
                     int audio_decim, float* audio, int64_t audio_stride);

@@ -70,6 +70,7 @@ SIGNATURES = {
                               _dp, _fp, _fp]),
     "sdr_rf_frontend_dev": (_i32, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _dp, _i32, _i32, _vp, _vp,
                                    _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "sdr_fe_mono_fused": (_i32, [_i32, _i32, _i32, _i32]),
     "sdr_fe_mono_dev": (_i32, [_vp, _vp, _i32, _i64, _i64, _i32, _dp, _i32, _i32, _dp, _i32, _i32, _vp,
                                _i64]),
     "sdr_fir_dev": (_i32, [_vp, _vp, _vp, _f32, _i32, _i64, _i64, _i64, _i32, _dp, _i32, _i32, _vp,

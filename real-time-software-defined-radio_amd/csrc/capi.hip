@@ -318,6 +318,10 @@ int sdr_rf_frontend_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int
   return SDR_OK;
 }
 
+int sdr_fe_mono_fused(int rf_taps, int rf_decim, int audio_taps, int audio_decim) {
+  return rf_decim == 10 && rf_taps == 101 && audio_taps == 151 && audio_decim == 5;
+}
+
 int sdr_fe_mono_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t stride, int nstreams,
                     const double* rf_b, int rf_taps, int rf_decim, const double* audio_b, int audio_taps,
                     int audio_decim, float* audio, int64_t audio_stride) {
@@ -336,9 +340,8 @@ int sdr_fe_mono_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t
   const int u8 = iq_dtype == SDR_IQ_U8;
   const int64_t xs = nstreams > 1 ? stride : ceil_div(n, 2) * 2;
   const int64_t as = nstreams > 1 ? audio_stride : A;
-  const bool fused = rf_decim == 10 && rf_taps == 101 && audio_taps == 151 &&
-                     audio_decim == 5 && xs % 2 == 0 && ((uintptr_t)iq % (u8 ? 4 : 16)) == 0 &&
-                     ((uintptr_t)audio % 4) == 0;
+  const bool fused = sdr_fe_mono_fused(rf_taps, rf_decim, audio_taps, audio_decim) && xs % 2 == 0 &&
+                     ((uintptr_t)iq % (u8 ? 4 : 16)) == 0 && ((uintptr_t)audio % 4) == 0;
   if (fused) {
     FeLaunch a{iq, n, xs, 0, nstreams, rts->dev_f32, &rts->h, rf_taps, rf_decim, u8, nullptr, nullptr, 0,
                nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr};

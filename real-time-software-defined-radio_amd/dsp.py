@@ -165,16 +165,22 @@ def my_convoloution(x, h, N_taps, my_zi=None, ctx=None):
     zi = np.zeros(10) if my_zi is None else np.asarray(my_zi, dtype=np.float64)
     T = len(h)
     L = len(zi)
-    hist = history_from_my_zi(zi, T)
-    full = np.concatenate([hist, np.asarray(x, dtype=np.float64)]).astype(np.float32)
-    c = _ctx(ctx)
     n = len(x)
+    xd = np.asarray(x, dtype=np.float64)
+    # the new state is x[-len(my_zi):] (:175); for an empty my_zi that is x[-0:], the whole block
+    new_zi = xd[-L:] if L else xd[0:]
+    if n == 0:                       # no output sample reads the history
+        return np.zeros(0), new_zi
+    if L == 0 and T > 1:             # y[0] reads my_zi[len(my_zi)-1-0] = my_zi[-1] (:169)
+        raise IndexError("index -1 is out of bounds for axis 0 with size 0")
+    hist = history_from_my_zi(zi, T)
+    full = np.concatenate([hist, xd]).astype(np.float32)
+    c = _ctx(ctx)
     buf = _lib.DeviceBuffer.from_array(c, full)
     out = _lib.DeviceBuffer(c, max(4 * n, 16))
     check(c.lib.sdr_fir_dev(c.handle, buf.ptr + 4 * (T - 1), None, 1.0, SDR_PRE_NONE, n, n, T - 1, 1,
                             f64p(h), T, 1, None, 0, None, out.ptr, n), "sdr_fir_dev")
     y = out.download(n).astype(np.float64)
-    new_zi = np.asarray(x, dtype=np.float64)[-L:] if L else np.asarray(x, dtype=np.float64)[len(x):]
     return y, new_zi
 
 

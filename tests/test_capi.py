@@ -122,3 +122,16 @@ def test_product_never_imports_oracle():
     for f in list(pkg.rglob("*.py")) + list(pkg.rglob("*.hip")) + list(pkg.rglob("*.h")) + [pkg / "csrc" / "Makefile"]:
         text = f.read_text()
         assert "oracle" not in text.replace("never imports oracle", ""), f
+
+
+def test_my_convoloution_empty_history_as_reference(sdr):
+    """model/fmSupportLib.py:157-176 with my_zi = []: y[0] reads my_zi[-1] -> IndexError (any
+    filter longer than one tap, non-empty block); an empty block reads nothing and returns
+    x[-0:], i.e. the whole (empty) block, as the new state.  Both before any GPU work."""
+    h = np.ones(5) / 5
+    with pytest.raises(IndexError):
+        sdr.my_convoloution(np.ones(8), h, 5, np.zeros(0))
+    y, z = sdr.my_convoloution(np.zeros(0), h, 5, np.zeros(0))
+    assert y.shape == (0,) and z.shape == (0,)
+    y, z = sdr.my_convoloution(np.zeros(0), h, 5, np.arange(3.0))
+    assert y.shape == (0,) and z.shape == (0,)          # x[-3:] of an empty block
