@@ -86,7 +86,16 @@ def dist_setup(args):
     if ws > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        # gloo prints its connection messages on fd 1: keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=ws)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     return ws, rank, local
 
 
@@ -207,9 +216,18 @@ def load_traffic(path, taps, blocks, kpath):
     return None
 
 
+def device_for(local: int) -> int:
+    """GPU of this rank: LOCAL_RANK (one process per GPU); ranks beyond the visible devices
+    wrap around (a multi-process rehearsal on a one-GPU box)."""
+    import rtsdr
+    n = rtsdr.device_count()
+    return local % n if n > 0 else local
+
+
 def main():
     args = parse()
     ws, rank, local = dist_setup(args)
+    local = device_for(local)
     os.environ["SDR_DEVICE"] = str(local)
     if args.workload != "mono":
         return run_rx(args, ws, rank, local)
@@ -304,7 +322,8 @@ def main():
         kernels = {"fe_mono_pair": round(k_avg, 5)}
     else:
         k_bytes = n * bpc + M * 4                    # IQ in + demod out
-        kname = f"fe_slot_kernel<{args.taps}{',u8' if args.iq == 'u8' else ''}> (sdr_rf_frontend_dev)"
+        kname = (f"fe_slot_kernel<{args.taps},u8>" if args.iq == "u8" else f"fe_ring_kernel<{args.taps}>") + \
+            " (sdr_rf_frontend_dev)"
         mono_bytes = M * 4 + A * 4
         kernels = {"fe": round(k_avg, 5), "mono": round(stage_ms[1], 5),
                    "mono_gbs": round(mono_bytes / (stage_ms[1] * 1e-3) / 1e9, 1)}

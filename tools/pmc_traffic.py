@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"split": "fe_slot_kernel<101, false", "fused": "fe_ring_kernel<101, true"}
+KERNELS = {"split": "fe_ring_kernel<101, false", "fused": "fe_ring_kernel<101, true"}
 
 
 def per_kernel(path, counter):
