@@ -447,12 +447,14 @@ int sdr_pll_dev(sdr_ctx* c, const float* in, int64_t n, int64_t in_stride, int n
   P.njobs = 1;
   P.nstreams = nstreams;
   P.n = n;
-  const int64_t ths = (n + 1) / 2 * 2 + 2;          // even: 16-B aligned phase rows
-  double* theta;
+  const int64_t ths = (n + 1) / 2 * 2 + 2;          // even: 16-B aligned rows
+  const int64_t cst = (n + n / 32 + 1) / 2 * 2 + 2;
+  double *theta, *cbuf;
   TRY(scratch(c, S_THETA, sizeof(double) * (size_t)ths * nstreams, (void**)&theta));
+  TRY(scratch(c, S_MISC, sizeof(double) * (size_t)cst * nstreams, (void**)&cbuf));
   P.j[0] = PllJob{in, nstreams > 1 ? in_stride : n, state, theta, ths, nco_i, nco_q,
                   nstreams > 1 ? out_stride : n + 1,
-                  PllCfg{freq, fs, nco_scale, phase_adj, norm_bw * 2.666, norm_bw * norm_bw * 3.555}};
+                  PllCfg{freq, fs, nco_scale, phase_adj, norm_bw * 2.666, norm_bw * norm_bw * 3.555}, cbuf, cst};
   HIP_TRY(sdr_launch_pll_jobs(P, c->stream));
   return SDR_OK;
 }

@@ -4,23 +4,26 @@
 // feedbackQ, ncoOut[0], trigOffset]) and src/helper.cpp:13-57 (fmPLL).
 // SURVEY §8a row a9.
 //
-// The loop is the only serial stage on the path.  It is split in two launches:
-//   1. pll_lanes_kernel: ONE LANE PER RECURRENCE.  A launch carries a job table (the
+// The loop is the only serial stage on the path, and one wave issues every instruction of
+// it (an f64 op holds the SIMD ~8 cycles at wave64), so the step is issue-bound: what is
+// not a function of the loop state is taken out of the loop.  Three launches per call:
+//   1. pll_prep_kernel (parallel over samples): c_k = sel_k - w*(trigOffset + k), where
+//      sel_k = 0 for x_k > 0 and pi for x_k < 0, and per 32-sample group a flag for a 0 or
+//      NaN input (the general form's case).  For x != 0, atan2(-x sin th, x cos th) of the
+//      previous step's angle th_{k-1} = w (trigOffset + k) + phaseEst_{k-1} is
+//      wrap(sel_k - th_{k-1}) = wrap(c_k - phaseEst_{k-1}), reduced by a two-constant
+//      Cody-Waite step.
+//   2. pll_lanes_kernel: ONE LANE PER RECURRENCE.  A launch carries a job table (the
 //      stereo pilot PLL and the RDS carrier PLL of every stream); each
-//      wave runs one job for up to 64 streams, lane = stream, so one wave advances 64
-//      independent loops at the cost of one.  Per lane, in f64:
-//        e_k   = atan2(-x_k fQ, x_k fI)                      (fmPll.py:24-27)
+//      wave runs one job for up to 64 streams, lane = stream.  Per step, in f64:
+//        e_k   = wrap(c_k - phaseEst)                        (fmPll.py:24-27)
 //        integ += Ki e_k ; phaseEst += Kp e_k + integ         (fmPll.py:29-31)
-//        th_k  = 2 pi (freq/Fs) (trigOffset + k + 1) + phaseEst (fmPll.py:33)
-//        fI, fQ = cos th_k, sin th_k                          (fmPll.py:34-35)
-//      and stores th_k.  Because (fI, fQ) = (cos, sin) of the previous th, the
-//      phase detector is evaluated as the exactly reduced angle -th (x > 0) or
-//      pi - th (x < 0): a three-constant Cody-Waite reduction by 2 pi, identical
-//      to atan2(-x sin th, x cos th) up to rounding (~1e-16 rad).  x == 0, NaN and
-//      the first sample of a call (whose fI, fQ come from the caller's state)
-//      take the literal sincos + atan2 form, so signed zeros behave as in Python.
-//      The lane also writes ncoOut[0] / ncoOutQ[0] (the carried values) before the loop.
-//   2. nco_jobs_kernel: fully parallel ncoOut[k+1] = cos(th_k*scale + adj),
+//      (8 f64 ops) and the lane stores phaseEst_k.  The first sample of a call (whose fI, fQ
+//      come from the caller's state) and groups holding a 0 or NaN input take the literal
+//      sincos + atan2 form, so signed zeros behave as in Python.  The lane also writes
+//      ncoOut[0] / ncoOutQ[0] (the carried values) before the loop.
+//   3. nco_jobs_kernel (parallel): th_k = 2 pi (freq/Fs) (trigOffset + k + 1) + phaseEst_k
+//      (fmPll.py:33, Python's rounding), ncoOut[k+1] = cos(th_k*scale + adj),
 //      ncoOutQ[k+1] = sin(th_k*scale + adj) (fmPll.py:36-37).
 // All phase arithmetic is f64 (SURVEY §7 hard part 5: an fp32 NCO drifts).
 #include "sdr_launch.h"
@@ -58,8 +61,8 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
   if (s >= P.nstreams) return;  // votes below run over the active lanes only
   const PllJob& J = P.j[q];
   struct {
-    const float* in; double* th; float* nco_i; float* nco_q;
-  } L{J.in + (int64_t)s * J.in_stride, J.theta + (int64_t)s * J.th_stride,
+    const float* in; double* th; const double* c; float* nco_i; float* nco_q;
+  } L{J.in + (int64_t)s * J.in_stride, J.theta + (int64_t)s * J.th_stride, J.cbuf + (int64_t)s * J.c_stride,
       J.nco_i + (int64_t)s * J.out_stride, J.nco_q ? J.nco_q + (int64_t)s * J.out_stride : nullptr};
   const PllCfg cfg = J.cfg;
   double* st = J.state + (int64_t)s * 6;
@@ -89,79 +92,71 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
     phase = phase + cfg.kp * e + integ;
     arg = w * ((off + (double)k) + 1.0) + phase;
   };
-  // Fast form for x != 0: atan2(-x sin a, x cos a) = wrap(-a) or wrap(pi - a), branch-free.
-  // The step is issue-bound (one wave issues every instruction of the recurrence; an f64
-  // op holds the SIMD ~8 cycles at wave64), so it is written for the fewest f64 ops (10: 23
-  // instructions per step became 15, tools/pll_probe.hip): the loop filter's updates as
-  // FMAs (one rounding where Python rounds twice: the f32 outputs cannot see the
-  // difference) and a two-constant reduction (the third term is below 1e-22 rad per turn).  `base` = (off + k) + 1 is a running exact integer in double (< 2^53).
-  double base = 0.0;
-  auto fast = [&](float xf) {
-    const double sel = xf > 0.f ? 0.0 : kPi;                 // off the chain: x is known
-    const double d = sel - arg;
-    // n = ceil(d/2pi - 1/2) rounds half-way cases down, so e = d - 2 pi n lies in (-pi, pi]
-    // (atan2's range) without a range fix
+  // Fast step (x != 0): e = wrap(c_k - phaseEst) by n = ceil(d/2pi - 1/2), which rounds
+  // half-way cases down so e lies in (-pi, pi] (atan2's range) without a range fix; the loop
+  // filter's updates as FMAs (one rounding where Python rounds twice: the f32 outputs cannot
+  // see it).  8 f64 ops per step (tools/pll_probe.hip).
+  auto fast = [&](double c) {
+    const double d = c - phase;
     const double nn = ceil(fma(d, kInv2Pi, -0.5));
     const double e = fma(-nn, kP2, fma(-nn, kP1, d));
     integ = fma(cfg.ki, e, integ);
     phase = fma(cfg.kp, e, phase) + integ;
-    base = base + 1.0;
-    arg = fma(w, base, phase);
   };
-  auto load_group = [&](float (&v)[PG], int64_t k0) {
+  const double* cr = L.c;
+  auto load_group = [&](double (&v)[PG], int64_t k0) {
     if constexpr (VEC) {
 #pragma unroll
-      for (int i = 0; i < PG; i += 4) {
-        const float4 f = *reinterpret_cast<const float4*>(L.in + k0 + i);
-        v[i] = f.x; v[i + 1] = f.y; v[i + 2] = f.z; v[i + 3] = f.w;
+      for (int i = 0; i < PG; i += 2) {
+        const double2 f = *reinterpret_cast<const double2*>(cr + k0 + i);
+        v[i] = f.x;
+        v[i + 1] = f.y;
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < PG; ++i) v[i] = L.in[k0 + i];
+      for (int i = 0; i < PG; ++i) v[i] = cr[k0 + i];
     }
   };
   const int64_t ng = n / PG;
-  float cur[PG], nxt[PG];
-  if (ng > 0) load_group(cur, 0);
+  double cur[PG], nxt[PG];
+  double flag = 0.0, flag_n = 0.0;                 // group flags: 1.0 = a 0 / NaN input
+  if (ng > 0) { load_group(cur, 0); flag = cr[n]; }
   for (int64_t g = 0; g < ng; ++g) {
-    if (g + 1 < ng) load_group(nxt, (g + 1) * PG);
-    // wave vote: does any lane's group hold a 0 or NaN input (the general form's other
-    // case), or is it the call's first group (literal first sample)?
-    bool odd = g == 0;
-#pragma unroll
-    for (int i = 0; i < PG; ++i) odd |= !(cur[i] > 0.f || cur[i] < 0.f);
-    if (__any(odd)) {
-      // rare (first group of a call, zero or NaN inputs): a rolled loop over the inputs
-      // in memory, phases stored one by one (unrolled, its atan2/sincos would spill)
+    if (g + 1 < ng) { load_group(nxt, (g + 1) * PG); flag_n = cr[n + g + 1]; }
+    // wave vote: the call's first group (literal first sample), or a 0 / NaN input
+    if (__any(g == 0 || flag != 0.0)) {
+      // rare: a rolled loop over the inputs in memory (unrolled, its atan2/sincos would spill)
       for (int i = 0; i < PG; ++i) {
         const int64_t k = g * PG + i;
         general(L.in[k], k, k == 0);
-        L.th[k] = arg;
+        L.th[k] = phase;
       }
     } else {
-      double thv[PG];
-      base = (off + (double)(g * PG - 1)) + 1.0;
+      double ph[PG];
 #pragma unroll
       for (int i = 0; i < PG; ++i) {
         fast(cur[i]);
-        thv[i] = arg;
+        ph[i] = phase;
       }
+      arg = w * ((off + (double)(g * PG + PG - 1)) + 1.0) + phase;   // for a later general step
       double* tp = L.th + g * PG;
       if constexpr (VEC) {
 #pragma unroll
-        for (int i = 0; i < PG; i += 2) *reinterpret_cast<double2*>(tp + i) = make_double2(thv[i], thv[i + 1]);
+        for (int i = 0; i < PG; i += 2) *reinterpret_cast<double2*>(tp + i) = make_double2(ph[i], ph[i + 1]);
       } else {
 #pragma unroll
-        for (int i = 0; i < PG; ++i) tp[i] = thv[i];
+        for (int i = 0; i < PG; ++i) tp[i] = ph[i];
       }
     }
 #pragma unroll
     for (int i = 0; i < PG; ++i) cur[i] = nxt[i];
+    flag = flag_n;
   }
   for (int64_t k = ng * PG; k < n; ++k) {      // tail (< PG samples)
     general(L.in[k], k, k == 0);
-    L.th[k] = arg;
+    L.th[k] = phase;
   }
+  L.th[n] = off;                                // the NCO kernel's trigOffset (st[5] changes below)
   if (n > 0) {
     st[0] = integ;
     st[1] = phase;
@@ -172,7 +167,34 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
   }
 }
 
-// nco[k+1] from th_k for every (job, stream) of the table; nco[0] is the loop kernel's.
+// Per-sample constants of the loop (parallel): c_k = sel_k - w (off + k) and one flag per
+// PG-sample group holding a 0 or NaN input; c row layout: c[0..n) | flags[0..n/PG).
+__global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
+#pragma clang fp contract(off)
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int g = blockIdx.y;                 // uniform: (job, stream)
+  const int q = g / P.nstreams;
+  const int s = g - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const double off = J.state[(int64_t)s * 6 + 5];
+  const double w = 2.0 * kPi * (J.cfg.freq / J.cfg.fs);
+  double* c = J.cbuf + (int64_t)s * J.c_stride;
+  bool odd = false;
+  if (k < P.n) {
+    const float x = J.in[(int64_t)s * J.in_stride + k];
+    odd = !(x > 0.f || x < 0.f);
+    c[k] = (x > 0.f ? 0.0 : kPi) - w * (off + (double)k);      // the previous step's w (off + k)
+  }
+  // groups of PG = 32 lanes: the low and high half of each wave
+  const uint64_t m = __ballot(odd);
+  const int lane = threadIdx.x & 63;
+  const int64_t grp = k / PG;
+  if ((lane == 0 || lane == 32) && grp < P.n / PG)
+    c[P.n + grp] = ((lane == 0 ? (m & 0xffffffffull) : (m >> 32)) != 0) ? 1.0 : 0.0;
+}
+
+// nco[k+1] from phaseEst_k for every (job, stream) of the table (th_k by the reference's
+// formula, fmPll.py:33); nco[0] is the loop kernel's.
 __global__ void nco_jobs_kernel(PllJobs P) {
 #pragma clang fp contract(off)
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -181,7 +203,11 @@ __global__ void nco_jobs_kernel(PllJobs P) {
   const int q = g / P.nstreams;
   const int s = g - q * P.nstreams;
   const PllJob& J = P.j[q];
-  const double a = J.theta[(int64_t)s * J.th_stride + k] * J.cfg.scale + J.cfg.adj;
+  const double* ph = J.theta + (int64_t)s * J.th_stride;
+  const double off = ph[P.n];
+  const double w = 2.0 * kPi * (J.cfg.freq / J.cfg.fs);
+  const double th = w * ((off + (double)k) + 1.0) + ph[k];
+  const double a = th * J.cfg.scale + J.cfg.adj;
   double sv, cv;
   sincos(a, &sv, &cv);
   J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
@@ -192,14 +218,17 @@ __global__ void nco_jobs_kernel(PllJobs P) {
 
 hipError_t sdr_launch_pll_jobs(const PllJobs& P, hipStream_t st) {
   if (P.njobs < 1 || P.njobs > SDR_PLL_MAXJ || P.nstreams <= 0 || P.n < 0) return hipErrorInvalidValue;
-  // 16-B loads/stores need every lane's input row and phase row 16-B aligned
+  // 16-B loads / stores need every lane's constants row and phase row 16-B aligned
   bool vec = true;
   for (int q = 0; q < P.njobs; ++q) {
     const PllJob& J = P.j[q];
-    vec = vec && ((uintptr_t)J.in % 16) == 0 && (J.in_stride % 4) == 0 && ((uintptr_t)J.theta % 16) == 0 &&
+    if (J.th_stride < P.n + 1 || J.c_stride < P.n + P.n / PG) return hipErrorInvalidValue;
+    vec = vec && ((uintptr_t)J.cbuf % 16) == 0 && (J.c_stride % 2) == 0 && ((uintptr_t)J.theta % 16) == 0 &&
           (J.th_stride % 2) == 0;
   }
   const int lanes = P.njobs * P.nstreams;
+  if (P.n > 0)
+    hipLaunchKernelGGL(pll_prep_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)lanes), dim3(256), 0, st, P);
   const dim3 grid((unsigned)(P.njobs * ((P.nstreams + 63) / 64)));
   if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, P);
   else hipLaunchKernelGGL(pll_lanes_kernel<false>, grid, dim3(64), 0, st, P);

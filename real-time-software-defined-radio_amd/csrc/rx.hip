@@ -451,6 +451,8 @@ struct sdr_rx {
   double* pll_state[2] = {};           // 6 per stream (stereo, RDS)
   double* theta = nullptr;             // PLL phases: 2 x S rows of ths
   int64_t ths = 0;
+  double* pllc = nullptr;              // PLL per-sample constants: 2 x S rows of cst
+  int64_t cst = 0;
   void* iq_dev = nullptr;              // host-path upload buffer
   size_t iq_cap = 0;
   void* pin_in = nullptr;              // pinned host staging (sdr_rx_run)
@@ -549,8 +551,9 @@ int rx_finalize(sdr_rx* r) {
   }
   r->bank_len = zl;
   r->ths = round_up(M, 2) + 2;
+  r->cst = round_up(M + M / 32, 2) + 2;
   const int64_t S2 = round_up(S, 2);                 // keeps the phase rows 16-B aligned
-  const int64_t doubles = 2 * zl + 3 * S2 + 2 * 6 * S2 + 2 * S * r->ths;
+  const int64_t doubles = 2 * zl + 3 * S2 + 2 * 6 * S2 + 2 * S * r->ths + 2 * S * r->cst;
   const size_t bytes = (size_t)floats * 4 + 64 + (size_t)doubles * 8;
   TRY(set_dev(r->c));
   hipError_t e = hipMalloc(&r->mem, bytes);
@@ -567,6 +570,7 @@ int rx_finalize(sdr_rx* r) {
   r->pll_state[0] = r->phase + 3 * S2;
   r->pll_state[1] = r->pll_state[0] + 6 * S2;
   r->theta = r->pll_state[1] + 6 * S2;
+  r->pllc = r->theta + 2 * S * r->ths;
   r->ready = true;
   return sdr_rx_reset(r);
 }
@@ -741,10 +745,11 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     P.n = M;
     if (stx)
       P.j[P.njobs++] = PllJob{o[SDR_RX_O_BPF_RECOVERY], ms, r->pll_state[0], r->theta, r->ths,
-                              o[SDR_RX_O_STEREO_NCO], nullptr, ms, r->pll[0]};
+                              o[SDR_RX_O_STEREO_NCO], nullptr, ms, r->pll[0], r->pllc, r->cst};
     if (rd)
       P.j[P.njobs++] = PllJob{o[SDR_RX_O_RDS_PRE_PLL], ms, r->pll_state[1], r->theta + (int64_t)S * r->ths, r->ths,
-                              o[SDR_RX_O_RDS_NCO_I], o[SDR_RX_O_RDS_NCO_Q], ms, r->pll[1]};
+                              o[SDR_RX_O_RDS_NCO_I], o[SDR_RX_O_RDS_NCO_Q], ms, r->pll[1],
+                              r->pllc + (int64_t)S * r->cst, r->cst};
     HIP_TRY(sdr_launch_pll_jobs(P, st));
   }
   HIP_TRY(mark(1 + SDR_RX_ST_PLL));

@@ -51,12 +51,13 @@ hipError_t sdr_launch_psd(const void* x, int f64, int64_t n, int logn, double fs
                           double* part, double* out, int* zero_flag, hipStream_t st);
 hipError_t sdr_launch_dft(const double* x, int64_t n, double* X, hipStream_t st);
 // PLL job table (pll.hip): one lane per (job, stream) recurrence.  Per stream: state 6
-// doubles (stride 6), in[n] (in_stride), theta[n] scratch (th_stride), nco_i / nco_q
-// (optional) n+1 floats (out_stride).
+// doubles (stride 6), in[n] (in_stride), nco_i / nco_q (optional) n+1 floats (out_stride),
+// and two f64 scratch rows: theta (th_stride >= n+1: the phase estimates, then the call's
+// trigOffset) and cbuf (c_stride >= n + n/32: per-sample loop constants, then group flags).
 #define SDR_PLL_MAXJ 4
 struct PllJob {
   const float* in; int64_t in_stride; double* state; double* theta; int64_t th_stride;
-  float* nco_i; float* nco_q; int64_t out_stride; PllCfg cfg;
+  float* nco_i; float* nco_q; int64_t out_stride; PllCfg cfg; double* cbuf; int64_t c_stride;
 };
 struct PllJobs { PllJob j[SDR_PLL_MAXJ]; int njobs; int nstreams; int64_t n; };
 hipError_t sdr_launch_pll_jobs(const PllJobs& jobs, hipStream_t st);

@@ -93,12 +93,15 @@ int main() {
   float* din;
   double *dst, *dth, *dth2;
   float *nco_i, *nco_q;
+  double* cb;
   CK(hipMalloc(&din, sizeof(float) * S * n));
   CK(hipMalloc(&dst, sizeof(double) * 6 * S));
   CK(hipMalloc(&dth, sizeof(double) * S * (n + 2)));
   CK(hipMalloc(&dth2, sizeof(double) * S * (n + 2)));
   CK(hipMalloc(&nco_i, sizeof(float) * S * (n + 1)));
   CK(hipMalloc(&nco_q, sizeof(float) * S * (n + 1)));
+  const int64_t cst = n + n / 32 + 2;
+  CK(hipMalloc(&cb, sizeof(double) * S * cst));
   CK(hipMemcpy(din, h.data(), sizeof(float) * S * n, hipMemcpyHostToDevice));
   const double bw = 0.001;
   PllCfg cfg{114e3, 240e3, 0.5, M_PI / 3.3 - M_PI / 1.5, bw * 2.666, bw * bw * 3.555};
@@ -112,7 +115,7 @@ int main() {
   // product
   PllJobs P{};
   P.njobs = 1; P.nstreams = S; P.n = n;
-  P.j[0] = PllJob{din, n, dst, dth, n + 2, nco_i, nco_q, n + 1, cfg};
+  P.j[0] = PllJob{din, n, dst, dth, n + 2, nco_i, nco_q, n + 1, cfg, cb, cst};
   float ms = 0;
   for (int r = 0; r < 3; ++r) { reset(); CK(sdr_launch_pll_jobs(P, 0)); }
   CK(hipDeviceSynchronize());
@@ -127,8 +130,12 @@ int main() {
     best = std::min(best, ms);
   }
   printf("product  : %8.1f us  %6.1f ns/step (incl. nco kernel)\n", best * 1e3, best * 1e6 / n);
+  // the product's theta rows now hold the phase estimates: rebuild th_k = w (k + 1) + phase_k
   std::vector<double> t_ref(S * (n + 2)), t_v(S * (n + 2));
   CK(hipMemcpy(t_ref.data(), dth, sizeof(double) * S * (n + 2), hipMemcpyDeviceToHost));
+  for (int s = 0; s < S; ++s)
+    for (int64_t k = 0; k < n; ++k)
+      t_ref[s * (n + 2) + k] = 2.0 * M_PI * (cfg.freq / cfg.fs) * ((0.0 + (double)k) + 1.0) + t_ref[s * (n + 2) + k];
   auto run_v = [&](auto kern, const char* name) {
     float b = 1e9;
     for (int r = 0; r < reps + 3; ++r) {
