@@ -18,7 +18,8 @@
 //      wave runs one job for up to 64 streams, lane = stream.  Per step, in f64:
 //        e_k   = wrap(c_k - phaseEst)                        (fmPll.py:24-27)
 //        integ += Ki e_k ; phaseEst += Kp e_k + integ         (fmPll.py:29-31)
-//      (8 f64 ops) and the lane stores phaseEst_k.  The first sample of a call (whose fI, fQ
+//      (6 f64 ops: the wrap is 2 pi (fract(c'_k - phaseEst/2pi) - 1/2) with c'_k = c_k/2pi +
+//      1/2 from the prep kernel) and the lane stores phaseEst_k.  The first sample of a call (whose fI, fQ
 //      come from the caller's state) and groups holding a 0 or NaN input take the literal
 //      sincos + atan2 form, so signed zeros behave as in Python.  The lane also writes
 //      ncoOut[0] / ncoOutQ[0] (the carried values) before the loop.
@@ -36,6 +37,7 @@ constexpr double kP2 = -1.748455600074497e-07;    // double(2 pi - kP1)
 constexpr double kP3 = -1.0687562935444062e-23;   // remainder
 constexpr double kInv2Pi = 0.15915494309189535;
 constexpr double kPi = 3.14159265358979323846;
+constexpr double k2Pi = 6.28318530717958647692;
 
 // r = a - 2*pi*n, n = rint(a / 2pi), |r| <= pi (up to one ulp at the boundary).
 __device__ inline double reduce_2pi(double a) {
@@ -92,14 +94,15 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
     phase = phase + cfg.kp * e + integ;
     arg = w * ((off + (double)k) + 1.0) + phase;
   };
-  // Fast step (x != 0): e = wrap(c_k - phaseEst) by n = ceil(d/2pi - 1/2), which rounds
-  // half-way cases down so e lies in (-pi, pi] (atan2's range) without a range fix; the loop
-  // filter's updates as FMAs (one rounding where Python rounds twice: the f32 outputs cannot
-  // see it).  8 f64 ops per step (tools/pll_probe.hip).
+  // Fast step (x != 0): e = wrap(c_k - phaseEst) (atan2's (-pi, pi] differs only at e = -pi
+  // exactly); the loop filter's updates as FMAs (one rounding where Python rounds twice: the
+  // f32 outputs cannot see it).  6 f64 ops per step (tools/pll_probe.hip).
   auto fast = [&](double c) {
-    const double d = c - phase;
-    const double nn = ceil(fma(d, kInv2Pi, -0.5));
-    const double e = fma(-nn, kP2, fma(-nn, kP1, d));
+    // c = (sel - w (off + k)) / 2pi + 1/2: t = d/2pi + 1/2, e = 2pi (fract(t) - 1/2) = d - 2pi
+    // round(d/2pi), in [-pi, pi); t's rounding (ulp of the accumulated angle) is the same
+    // order as the rounding of the reference's own th = w (off + k + 1) + phaseEst
+    const double t = fma(-kInv2Pi, phase, c);
+    const double e = fma(__builtin_amdgcn_fract(t), k2Pi, -kPi);
     integ = fma(cfg.ki, e, integ);
     phase = fma(cfg.kp, e, phase) + integ;
   };
@@ -167,7 +170,7 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
   }
 }
 
-// Per-sample constants of the loop (parallel): c_k = sel_k - w (off + k) and one flag per
+// Per-sample constants of the loop (parallel): c_k = (sel_k - w (off + k)) / 2pi + 1/2 and one flag per
 // PG-sample group holding a 0 or NaN input; c row layout: c[0..n) | flags[0..n/PG).
 __global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
 #pragma clang fp contract(off)
@@ -183,7 +186,8 @@ __global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
   if (k < P.n) {
     const float x = J.in[(int64_t)s * J.in_stride + k];
     odd = !(x > 0.f || x < 0.f);
-    c[k] = (x > 0.f ? 0.0 : kPi) - w * (off + (double)k);      // the previous step's w (off + k)
+    const double cc = (x > 0.f ? 0.0 : kPi) - w * (off + (double)k);   // the previous step's w (off + k)
+    c[k] = fma(cc, kInv2Pi, 0.5);
   }
   // groups of PG = 32 lanes: the low and high half of each wave
   const uint64_t m = __ballot(odd);
