@@ -18,8 +18,9 @@
 //      wave runs one job for up to 64 streams, lane = stream.  Per step, in f64:
 //        e_k   = wrap(c_k - phaseEst)                        (fmPll.py:24-27)
 //        integ += Ki e_k ; phaseEst += Kp e_k + integ         (fmPll.py:29-31)
-//      (6 f64 ops: the wrap is 2 pi (fract(c'_k - phaseEst/2pi) - 1/2) with c'_k = c_k/2pi +
-//      1/2 from the prep kernel) and the lane stores phaseEst_k.  The first sample of a call (whose fI, fQ
+//      (6 f64 ops, 3 of them dependent: the wrap is 2 pi (fract(c'_k - phaseEst/2pi) - 1/2)
+//      with c'_k = c_k/2pi + 1/2 from the prep kernel, and the loop filter is rewritten on
+//      fract's output) and the lane stores phaseEst_k.  The first sample of a call (whose fI, fQ
 //      come from the caller's state) and groups holding a 0 or NaN input take the literal
 //      sincos + atan2 form, so signed zeros behave as in Python.  The lane also writes
 //      ncoOut[0] / ncoOutQ[0] (the carried values) before the loop.
@@ -95,16 +96,24 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
     arg = w * ((off + (double)k) + 1.0) + phase;
   };
   // Fast step (x != 0): e = wrap(c_k - phaseEst) (atan2's (-pi, pi] differs only at e = -pi
-  // exactly); the loop filter's updates as FMAs (one rounding where Python rounds twice: the
-  // f32 outputs cannot see it).  6 f64 ops per step (tools/pll_probe.hip).
+  // exactly); the loop filter's updates as FMAs (fewer roundings than Python's: the f32
+  // outputs cannot see the difference).  tools/pll_probe.hip, DESIGN.md §4.
+  // c = (sel - w (off + k)) / 2pi + 1/2: t = d/2pi + 1/2 and e = 2pi (fract(t) - 1/2) = d -
+  // 2pi round(d/2pi), in [-pi, pi); t's rounding (ulp of the accumulated angle) is the same
+  // order as the rounding of the reference's own th = w (off + k + 1) + phaseEst.  With
+  // f = fract(t): integ' = integ + Ki e and phaseEst' = phaseEst + integ + (Kp + Ki) e, so
+  // phaseEst' = fma(2pi (Kp+Ki), f, S) with S = phaseEst + integ - pi (Kp+Ki) formed off the
+  // chain: three dependent ops per step (t, fract, phaseEst'), six f64 ops in all.  V tracks
+  // integ - pi (Kp+Ki).
+  const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
+  const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
+  double V = 0.0;
   auto fast = [&](double c) {
-    // c = (sel - w (off + k)) / 2pi + 1/2: t = d/2pi + 1/2, e = 2pi (fract(t) - 1/2) = d - 2pi
-    // round(d/2pi), in [-pi, pi); t's rounding (ulp of the accumulated angle) is the same
-    // order as the rounding of the reference's own th = w (off + k + 1) + phaseEst
     const double t = fma(-kInv2Pi, phase, c);
-    const double e = fma(__builtin_amdgcn_fract(t), k2Pi, -kPi);
-    integ = fma(cfg.ki, e, integ);
-    phase = fma(cfg.kp, e, phase) + integ;
+    const double f = __builtin_amdgcn_fract(t);
+    const double S = phase + V;
+    V = fma(kA, f, V - kB);
+    phase = fma(kC, f, S);
   };
   const double* cr = L.c;
   auto load_group = [&](double (&v)[PG], int64_t k0) {
@@ -136,11 +145,13 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
       }
     } else {
       double ph[PG];
+      V = integ - kD;
 #pragma unroll
       for (int i = 0; i < PG; ++i) {
         fast(cur[i]);
         ph[i] = phase;
       }
+      integ = V + kD;
       arg = w * ((off + (double)(g * PG + PG - 1)) + 1.0) + phase;   // for a later general step
       double* tp = L.th + g * PG;
       if constexpr (VEC) {
