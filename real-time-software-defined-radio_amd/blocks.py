@@ -49,6 +49,7 @@ class Receiver:
         flags = (SDR_RX_AUDIO if mono else 0) | (SDR_RX_STEREO if stereo else 0) | (SDR_RX_RDS if rds else 0)
         self.flags = flags
         self._lengths = {}
+        self._plans = {}
         h = ctypes.c_void_p()
         check(self.lib.sdr_rx_create(self.ctx.handle, self.S, self.B, SDR_IQ_U8 if self.u8 else SDR_IQ_F32,
                                      flags, ctypes.byref(h)), "sdr_rx_create")
@@ -97,13 +98,18 @@ class Receiver:
         iq = np.ascontiguousarray(iq, dtype=es)
         if iq.size != self.S * 2 * self.B:
             raise ValueError(f"expected {self.S} x {2 * self.B} interleaved values, got {iq.shape}")
-        if fetch is None:
-            fetch = [n for n in ("audio", "left", "right", "rrc_i", "rrc_q") if n in self.outputs]
-        outs = {n: np.empty((self.S, self._length(n)), dtype=np.float32) for n in fetch}
-        k = len(fetch)
-        which = (ctypes.c_int * k)(*[RX_OUTPUTS.index(n) for n in fetch])
-        ptrs = (ctypes.c_void_p * k)(*[outs[n].ctypes.data for n in fetch])
-        check(self.lib.sdr_rx_run(self.handle, iq.ctypes.data, self.B, k, which, ptrs, None), "sdr_rx_run")
+        key = tuple(fetch) if fetch is not None else None
+        plan = self._plans.get(key)
+        if plan is None:                      # output names -> (which[], lengths), built once
+            names = list(fetch) if fetch is not None else \
+                [n for n in ("audio", "left", "right", "rrc_i", "rrc_q") if n in self.outputs]
+            which = (ctypes.c_int * len(names))(*[RX_OUTPUTS.index(n) for n in names])
+            plan = self._plans[key] = (names, which, [self._length(n) for n in names])
+        names, which, lengths = plan
+        outs = {n: np.empty((self.S, m), dtype=np.float32) for n, m in zip(names, lengths)}
+        ptrs = (ctypes.c_void_p * len(names))(*[outs[n].ctypes.data for n in names])
+        check(self.lib.sdr_rx_run(self.handle, iq.ctypes.data, self.B, len(names), which, ptrs, None),
+              "sdr_rx_run")
         return outs
 
     def _length(self, name):
