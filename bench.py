@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--path", choices=["fused", "split"], default="fused",
                     help="fused: one fe_mono_kernel (demod stays on chip); split: FE kernel + FIR kernel")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--split-stream", action="store_true",
+                    help="mono: ONE stream of --blocks blocks split over the ranks, each range with a read-only "
+                         "halo (SURVEY §8e; strong scaling) instead of one stream per rank")
     ap.add_argument("--cpu-samples", type=int, default=4_096_000, help="complex samples per CPU stream")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall time per CPU leg")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "fe_pmc_traffic.json"),
@@ -238,10 +241,21 @@ def main():
     ctx = _lib.Context(local)
     lib, h = ctx.lib, ctx.handle
     rf_b, au_b = rtsdr.design.mono_coeffs(args.taps, args.audio_taps)
-    n = args.blocks * BLOCK
-    M = n // 10
-    A = M // 5
-    iq = rtsdr.synth.fm_iq(n, seed=rank, dtype=np.uint8 if args.iq == "u8" else np.float32)
+    n_total = args.blocks * BLOCK
+    n = n_total
+    dt = np.uint8 if args.iq == "u8" else np.float32
+    if args.split_stream:
+        # rank r: IQ [s0, s1) of the one stream plus the halo before s0 (no exchange)
+        step = 50
+        s0 = (rank * n_total // ws) // step * step
+        s1 = n_total if rank == ws - 1 else ((rank + 1) * n_total // ws) // step * step
+        w0 = max(0, s0 - rtsdr.split_halo(len(rf_b), len(au_b)))
+        iq = rtsdr.synth.fm_iq(n_total, seed=0, dtype=dt)[2 * w0:2 * s1].copy()
+        n = s1 - w0
+    else:
+        iq = rtsdr.synth.fm_iq(n, seed=rank, dtype=dt)
+    M = (n + 9) // 10
+    A = (M + 4) // 5
     dtype_code = _lib.SDR_IQ_U8 if args.iq == "u8" else _lib.SDR_IQ_F32
     d_iq = _lib.DeviceBuffer.from_array(ctx, iq)
     del iq
@@ -332,7 +346,7 @@ def main():
 
     result = None
     if rank == 0:
-        total = n * args.steps * ws
+        total = n_total * args.steps * (1 if args.split_stream else ws)
         result = {
             "metric": METRIC,
             "value": round(total / elapsed / 1e6, 1),
@@ -342,14 +356,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.split_stream else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic FM IQ (seed=rank), interleaved {args.iq}, device-resident",
+            "data": f"synthetic FM IQ ({'one stream split over the ranks with halos' if args.split_stream else 'seed=rank'})"
+                    f", interleaved {args.iq}, device-resident",
             "config": {"workload": f"RF front end ({args.taps}-tap LPF, decim 10, atan2 demod) + mono "
                                    f"({args.audio_taps}-tap LPF, decim 5): configs[1]+[2], one stream per GPU",
-                       "block_complex": BLOCK, "blocks_per_step": args.blocks, "complex_per_step": n,
-                       "iq": args.iq, "path": args.path, "parallelism": f"independent streams x{ws}"},
+                       "block_complex": BLOCK, "blocks_per_step": args.blocks, "complex_per_step": n_total,
+                       "iq": args.iq, "path": args.path,
+                       "parallelism": f"one stream in {ws} ranges + halo" if args.split_stream else
+                       f"independent streams x{ws}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,

@@ -19,7 +19,7 @@ from ._lib import (SDR_IQ_F32, SDR_IQ_U8, SDR_PRE_MIX, SDR_PRE_NONE, SDR_PRE_SQU
                    DeviceBuffer, SdrError, SdrUnavailable, Timer, device_count, get_context, load_library)
 from .blocks import MonoBlockProcessor, RdsBlockProcessor, RdsLinkLayer, Receiver, StereoBlockProcessor  # noqa: F401
 from .design import impulseResponseRootRaisedCosine, my_filterImpulseResponse  # noqa: F401
-from .dsp import (DFT, MonoState, estimatePSD, fm_mono_streams, fmDemodArctan, fmPll, lfilter, lfilter_decim,  # noqa: F401
+from .dsp import (DFT, MonoState, estimatePSD, fm_mono_range, fm_mono_streams, split_halo, fmDemodArctan, fmPll, lfilter, lfilter_decim,  # noqa: F401
                   mono_block, my_convoloution, resample, rf_frontend_block)
 
 __version__ = "0.1.0"

@@ -305,6 +305,35 @@ def fm_mono_streams(iq, rf_coeff, audio_coeff, rf_decim=10, audio_decim=5, ctx=N
     return out[0] if one else out
 
 
+def split_halo(rf_taps: int, audio_taps: int, rf_decim: int = 10, audio_decim: int = 5) -> int:
+    """IQ samples a range of one stream reads before its start when the stream is split
+    (SURVEY §8e): audio sample j depends on IQ [D*A*j - ((rf_taps-1) + rf_decim*audio_taps),
+    D*A*j], so (rf_taps-1) + rf_decim*audio_taps, rounded up to a whole audio sample
+    (rf_decim*audio_decim IQ samples)."""
+    step = rf_decim * audio_decim
+    need = (rf_taps - 1) + rf_decim * audio_taps
+    return (need + step - 1) // step * step
+
+
+def fm_mono_range(iq, start, end, rf_coeff, audio_coeff, rf_decim=10, audio_decim=5, ctx=None):
+    """The audio of IQ samples [start, end) of one stream, identical to those samples'
+    outputs of fm_mono_streams(iq) (the whole-stream pass), computed from the range plus a
+    read-only halo of split_halo(...) samples before it: one range per GPU, no exchange
+    (SURVEY §8e).  start must be a multiple of rf_decim*audio_decim; the outputs are those
+    audio samples j whose IQ position rf_decim*audio_decim*j lies in [start, end)."""
+    step = rf_decim * audio_decim
+    iq = np.asarray(iq)
+    n = iq.shape[0] // 2
+    if start % step or not (0 <= start <= end <= n):
+        raise ValueError(f"range [{start}, {end}) of {n}: start must be a multiple of {step}")
+    h = split_halo(len(_taps(rf_coeff)), len(_taps(audio_coeff)), rf_decim, audio_decim)
+    w0 = max(0, start - h)
+    a = fm_mono_streams(iq[2 * w0:2 * end], rf_coeff, audio_coeff, rf_decim, audio_decim, ctx=ctx)
+    j0 = (start - w0) // step
+    j1 = (end - w0 + step - 1) // step
+    return a[j0:j1]
+
+
 def estimatePSD(samples, NFFT, Fs, ctx=None):
     """(freq, psd_est) of model/fmSupportLib.py:66-140: Bartlett estimate over
     floor(len/NFFT) non-overlapping Hann-windowed segments, per-segment dB averaged.

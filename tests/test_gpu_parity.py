@@ -363,3 +363,28 @@ def test_fm_mono_streams_u8_ragged(sdr, gpu_ctx, oracle, n):
         ref, _ = oracle.mono_basic_coeffs((iq[s].astype(np.float64) - 128.0) / 128.0, rf_b, au_b)
         assert got[s].shape == ref.shape
         assert rms(got[s], ref) < AUDIO_RMS and maxabs(got[s], ref) < AUDIO_MAX, (s, rms(got[s], ref))
+
+
+# ---------------------------------------------------------------------------- split stream
+@pytest.mark.parametrize("taps", [101, 151])
+def test_split_stream_ranges_equal_single_pass(sdr, gpu_ctx, taps):
+    """one long stream split into ranges (one per GPU), each computed from its
+    samples plus a read-only halo of split_halo() samples, no exchange.  101 taps (the fused
+    kernel): bit-identical to the whole-stream pass, every output being the same sequence of
+    f32 operations on the same samples.  151 taps (FE kernel + audio FIR): a wave's first
+    tile takes its predecessor phase from a cross-lane sum, and the waves' run boundaries
+    fall elsewhere in a range than in the whole pass, so the last bits can differ there."""
+    rf_b, au_b = sdr.design.mono_coeffs(taps, 151)
+    n = 3 * 1_024_000 + 777
+    iq = sdr.synth.fm_iq(n, seed=31)
+    whole = sdr.fm_mono_streams(iq, rf_b, au_b)
+    cuts = [0, 1_000_000, 1_000_050, 2_048_000, n]          # ragged ranges, one of 50 samples
+    parts = [sdr.fm_mono_range(iq, a, b, rf_b, au_b) for a, b in zip(cuts[:-1], cuts[1:])]
+    assert sum(len(p) for p in parts) == len(whole)
+    got = np.concatenate(parts)
+    if taps == 101:
+        assert np.array_equal(got, whole)
+    else:
+        assert maxabs(got, whole) < 1e-6 and rms(got, whole) < 1e-8
+    with pytest.raises(ValueError):
+        sdr.fm_mono_range(iq, 1_000_001, n, rf_b, au_b)     # not on an audio-sample boundary

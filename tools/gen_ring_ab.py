@@ -5,7 +5,8 @@ from git into tools/_fe_r01.hip with renamed entry points).
 
 KN bits: 1 trivial fast epilogue, 2 no deferred-output queue (outputs dropped), 4 no halo
 copy, 8 fixed steady vmcnt wait, 16 taps from constants, 32 FUSED: no audio FIR,
-64 FUSED: no history writes, 128 FUSED: no warm-up tile (wrong audio at run starts; timing).
+64 FUSED: no history writes, 128 FUSED: no warm-up tile (wrong audio at run starts; timing), 256 FUSED: no run-end
+audio block (timing).
 
 build:  python3 tools/gen_ring_ab.py && cd tools && \
         hipcc --offload-arch=gfx950 -O3 -std=c++17 -Wno-inline-asm _ring_ab.hip _fe_r01.hip -o ring_ab
@@ -39,6 +40,8 @@ reps = [
      "      if constexpr (!(KN & 2)) q_push(q, o0, o1, o2);\n      return false;"),
     ("      dh_write(i, warm, d);", "      if constexpr (!(KN & 64)) dh_write(i, warm, d);"),
     ("    mid = i > 0;\n", "    mid = (KN & 128) ? false : i > 0;\n"),
+    ("          audio_block3(aw_lane, ptab, o0, o1, o2);",
+     "          if constexpr (KN & 256) { o0 = o1 = o2 = aw_lane[0]; } else audio_block3(aw_lane, ptab, o0, o1, o2);"),
     ("      wait_vm(issued - mark);",
      "      if constexpr (KN & 8) { if (issued - mark == 15) asm volatile(\"s_waitcnt vmcnt(15)\" ::: \"memory\");"
      " else asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\"); }\n      else wait_vm(issued - mark);"),
@@ -95,6 +98,7 @@ int main() {
   FU("FUSED KN=0", 0) FU("FUSED KN=2 no queue", 2) FU("FUSED KN=8 fixed wait", 8) FU("FUSED KN=32 no audio", 32)
   FU("FUSED KN=64 no dh", 64) FU("FUSED KN=96", 96) FU("FUSED KN=1 trivial epi", 1) FU("FUSED KN=111", 111)
   FU("FUSED KN=128 no warm-up", 128) FU("FUSED KN=224 no warm/audio/dh", 224) FU("FUSED KN=239", 239)
+  FU("FUSED KN=256 no run-end audio", 256) FU("FUSED KN=384 no warm-up/run-end", 384)
   const bool quick = getenv("AB_QUICK") != nullptr;   // counter runs: few launches
   for (auto& v : vs) v.go();
   CK(hipStreamSynchronize(st));
