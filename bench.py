@@ -3,7 +3,7 @@
 
 One step = one pass of RF front end (101-tap IQ LPF, decimate by 10, atan2 demod;
 configs[1]) + mono (151-tap audio LPF, decimate by 5; configs[2]) over a batch of
-`--blocks` x 1 024 000-complex-sample blocks of one synthetic 2.4 MS/s stream, input
+`--blocks` (default 128) x 1 024 000-complex-sample blocks of one synthetic 2.4 MS/s stream, input
 resident in HBM (block boundaries are carried-state continuations, so the batch is
 one continuous stream; SURVEY §5 "long-context").  Kernel: libsdr.so's fused
 FE + mono kernel (sdr_fe_mono_dev: the demodulated signal never leaves the CU);
@@ -62,7 +62,9 @@ def parse():
     ap.add_argument("--settle-ms", type=float, default=250.0,
                     help="untimed warm-up continues past --warmup steps until this much GPU time has "
                          "run, so the clocks have ramped before the timed region (DESIGN.md §5)")
-    ap.add_argument("--blocks", type=int, default=64, help="1 024 000-sample blocks per step")
+    ap.add_argument("--blocks", type=int, default=128,
+                    help="1 024 000-sample blocks per step (>= 64, SURVEY §8d; the launch has ~6 us of fixed cost, "
+                         "DESIGN.md §5)")
     ap.add_argument("--taps", type=int, default=101)
     ap.add_argument("--audio-taps", type=int, default=151)
     ap.add_argument("--iq", choices=["f32", "u8"], default="f32")

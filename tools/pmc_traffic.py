@@ -31,7 +31,7 @@ def per_kernel(path, counter):
 
 def main():
     tag = sys.argv[1]
-    blocks = int(sys.argv[sys.argv.index("--blocks") + 1]) if "--blocks" in sys.argv else 64
+    blocks = int(sys.argv[sys.argv.index("--blocks") + 1]) if "--blocks" in sys.argv else 128
     taps = int(sys.argv[sys.argv.index("--taps") + 1]) if "--taps" in sys.argv else 101
     n = blocks * 1_024_000
     entries = []
