@@ -55,7 +55,10 @@ struct StageJob {
   const float* mono;     // combiner: mono audio rows (y_stride apart), or null
   float* left;
   float* right;
-  int64_t n, x_stride, zi_stride, y_stride;
+  float* yh;             // host mirrors (pinned, rows yh_stride apart) of y / left / right, nullable:
+  float* lh;             //   sdr_rx_run's outputs are stored straight into pinned host memory
+  float* rh;             //   by the producing tile instead of coming back by a copy
+  int64_t n, x_stride, zi_stride, y_stride, yh_stride;
   int64_t b0;            // first workgroup of this job's tiles
   float gain;
   int pre, D, U, kind, T, tiles;
@@ -190,14 +193,25 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
     for (int r = 0; r < R; ++r)
       if (mf + r < M) yb[mf + r] = acc[r];
   }
+  if (J.yh != nullptr) {                             // host rows are packed: scalar stores
+    float* hb = J.yh + (int64_t)s * J.yh_stride;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (mf + r < M) hb[mf + r] = acc[r];
+  }
   if (J.mono != nullptr) {                           // stereo combiner (fmMonoBlock.py:166-170)
     float* lb = J.left + (int64_t)s * J.y_stride;
     float* rb = J.right + (int64_t)s * J.y_stride;
+    float* lhb = J.lh ? J.lh + (int64_t)s * J.yh_stride : nullptr;
+    float* rhb = J.rh ? J.rh + (int64_t)s * J.yh_stride : nullptr;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (mf + r < M) {
-        lb[mf + r] = (mr[r] + acc[r]) * 0.5f;
-        rb[mf + r] = (mr[r] - acc[r]) * 0.5f;
+        const float lv = (mr[r] + acc[r]) * 0.5f, rv = (mr[r] - acc[r]) * 0.5f;
+        lb[mf + r] = lv;
+        rb[mf + r] = rv;
+        if (lhb) lhb[mf + r] = lv;
+        if (rhb) rhb[mf + r] = rv;
       }
     }
   }
@@ -222,10 +236,14 @@ __device__ __forceinline__ void fir_tile_any(const StageJob& J, int s, int64_t t
       acc = fmaf(lds[k], pre_op(J.pre, xb[j0 - k], J.pre == PRE_MIX ? cb[j0 - k] : 0.f, J.gain), acc);
     if (J.zi != nullptr && j0 < J.T - 1) acc += (float)J.zi[(int64_t)s * J.zi_stride + j0];
     J.y[(int64_t)s * J.y_stride + m] = acc;
+    if (J.yh) J.yh[(int64_t)s * J.yh_stride + m] = acc;
     if (J.mono != nullptr) {
       const float a = J.mono[(int64_t)s * J.y_stride + m];
-      J.left[(int64_t)s * J.y_stride + m] = (a + acc) * 0.5f;
-      J.right[(int64_t)s * J.y_stride + m] = (a - acc) * 0.5f;
+      const float lv = (a + acc) * 0.5f, rv = (a - acc) * 0.5f;
+      J.left[(int64_t)s * J.y_stride + m] = lv;
+      J.right[(int64_t)s * J.y_stride + m] = rv;
+      if (J.lh) J.lh[(int64_t)s * J.yh_stride + m] = lv;
+      if (J.rh) J.rh[(int64_t)s * J.yh_stride + m] = rv;
     }
   }
 }
@@ -251,6 +269,7 @@ __device__ __forceinline__ void resample_tile(const StageJob& J, int s, int64_t 
     for (int k = k0; k <= khi; k += U, --xi) acc = fmaf(lds[k], xb[xi], acc);
     if (J.zi != nullptr && j0 < J.T - 1) acc += (float)J.zi[(int64_t)s * J.zi_stride + j0];
     J.y[(int64_t)s * J.y_stride + m] = acc * (float)U;
+    if (J.yh) J.yh[(int64_t)s * J.yh_stride + m] = acc * (float)U;
   }
 }
 
@@ -453,12 +472,12 @@ struct sdr_rx {
   int64_t ths = 0;
   double* pllc = nullptr;              // PLL per-sample constants: 2 x S rows of cst
   int64_t cst = 0;
-  void* iq_dev = nullptr;              // host-path upload buffer
-  size_t iq_cap = 0;
   void* pin_in = nullptr;              // pinned host staging (sdr_rx_run)
   size_t pin_in_cap = 0;
   float* pin_out = nullptr;
   size_t pin_out_cap = 0;
+  float* mirror[SDR_RX_NOUTPUTS] = {};  // sdr_rx_run: pinned host rows (out_n apart) the producing
+                                        // stage stores each requested output into, or null
   int parity = 0;
   int64_t blocks = 0;
   bool timing = false;                 // events between the stages of each block
@@ -607,7 +626,6 @@ void sdr_rx_destroy(sdr_rx* r) {
     (void)hipStreamSynchronize(r->c->stream);
   }
   if (r->mem) (void)hipFree(r->mem);
-  if (r->iq_dev) (void)hipFree(r->iq_dev);
   if (r->pin_in) (void)hipHostFree(r->pin_in);
   if (r->pin_out) (void)hipHostFree(r->pin_out);
   for (hipEvent_t e : r->ev)
@@ -680,6 +698,13 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   auto mark = [&](int k) { return r->timing ? hipEventRecord(r->ev[k], st) : hipSuccess; };
   HIP_TRY(mark(0));
   auto zin = [&](int z) { return zi + r->zoff[z]; };
+  auto out_of = [&](const float* y) {
+    for (int o = 0; o < SDR_RX_NOUTPUTS; ++o)
+      if (r->out[o] == y && need_out(r, o)) return o;
+    return -1;
+  };
+  auto mirror_of = [&](const float* y) { const int o = out_of(y); return o < 0 ? nullptr : r->mirror[o]; };
+  auto host_n = [&](const float* y) { const int o = out_of(y); return o < 0 ? (int64_t)0 : r->out_n[o]; };
   auto zout = [&](int z) { return zf + r->zoff[z]; };
   // device taps (cached per context; the pointers stay valid for this call)
   const TapSet* ts[SDR_RX_NFILTERS] = {};
@@ -718,6 +743,8 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     j.y = y; j.y_stride = ys; j.n = n; j.x_stride = xs;
     j.gain = 2.0f;                      // the reference's mixer gain (fmMonoBlock.py:156, fmRDSblock.py:173)
     j.pre = pre; j.D = D; j.U = 1; j.kind = JK_FIR; j.T = (int)r->taps[f].size();
+    j.yh = mirror_of(y);
+    j.yh_stride = host_n(y);
     return j;
   };
   const bool au = r->flags & (SDR_RX_AUDIO | SDR_RX_STEREO), stx = r->flags & SDR_RX_STEREO,
@@ -761,6 +788,9 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     j.mono = o[SDR_RX_O_AUDIO];                                                 // :166-170 (intended)
     j.left = o[SDR_RX_O_LEFT];
     j.right = o[SDR_RX_O_RIGHT];
+    j.lh = r->mirror[SDR_RX_O_LEFT];
+    j.rh = r->mirror[SDR_RX_O_RIGHT];
+    j.yh_stride = r->out_n[SDR_RX_O_STEREO];                                    // == out_n of L and R
     C.push_back(j);
   }
   if (rd) {                                                                     // fmRDSblock.py:173-182
@@ -798,20 +828,9 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
 }
 
 namespace {
-// grow a device buffer / a pinned host buffer (synchronising first: work in flight may use it)
-int grow_dev(sdr_rx* r, void** p, size_t* cap, size_t bytes) {
-  if (*cap >= bytes) return SDR_OK;
-  if (*p) {
-    HIP_TRY(hipStreamSynchronize(r->c->stream));
-    HIP_TRY(hipFree(*p));
-    *p = nullptr;
-    *cap = 0;
-  }
-  hipError_t e = hipMalloc(p, bytes);
-  if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx: hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
-  *cap = bytes;
-  return SDR_OK;
-}
+// grow a pinned host buffer (synchronising first: work in flight may use it).  Coherent
+// (uncached by the GPU): the device reads the IQ the host wrote for this block, and the
+// host reads what the stage kernels stored, with no copy engine in between.
 int grow_pinned(sdr_rx* r, void** p, size_t* cap, size_t bytes) {
   if (*cap >= bytes) return SDR_OK;
   if (*p) {
@@ -820,10 +839,15 @@ int grow_pinned(sdr_rx* r, void** p, size_t* cap, size_t bytes) {
     *p = nullptr;
     *cap = 0;
   }
-  hipError_t e = hipHostMalloc(p, bytes, hipHostMallocDefault);
+  hipError_t e = hipHostMalloc(p, bytes, hipHostMallocCoherent);
   if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx: hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
   *cap = bytes;
   return SDR_OK;
+}
+// outputs a stage kernel stores (and can store a host copy of); the demod (FE kernel) and
+// the NCOs (PLL) come back by copy
+bool stage_output(int o) {
+  return o != SDR_RX_O_DEMOD && o != SDR_RX_O_STEREO_NCO && o != SDR_RX_O_RDS_NCO_I && o != SDR_RX_O_RDS_NCO_Q;
 }
 }  // namespace
 
@@ -831,8 +855,13 @@ int sdr_rx_process(sdr_rx* r, const void* iq_host, int64_t iq_stride) {
   return sdr_rx_run(r, iq_host, iq_stride, 0, nullptr, nullptr, nullptr);
 }
 
-// One block from host memory: the IQ goes through pinned staging to the device, the chain
-// runs, every requested output comes back through pinned staging, and the call waits once.
+// One block from host memory.  The per-block cost at the reference's block sizes is the
+// number of engine hand-offs, not bytes (tools/xfer_probe.hip: an SDMA upload, two kernels,
+// an SDMA download and a wait take 35 us; the same kernels reading and writing pinned host
+// memory directly, 25 us), so: the IQ is copied into pinned host memory and the FE kernel
+// reads it from there over PCIe; each requested output is stored into pinned host memory by
+// the stage kernel that produces it (the demod and NCO rows, which no stage kernel stores,
+// come back by copy); the call waits once.
 int sdr_rx_run(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, const int* which, float* const* out,
                const int64_t* out_stride) {
   if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
@@ -852,30 +881,37 @@ int sdr_rx_run(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, cons
   const int64_t es = r->u8 ? 2 : 8;                      // bytes per complex sample
   const int64_t xs = r->S > 1 ? iq_stride : r->B;
   const size_t bytes = (size_t)(xs * (r->S - 1) + r->B) * es;
+  // pinned output regions, one per distinct requested output (rows out_n apart)
+  size_t region[SDR_RX_NOUTPUTS];
+  bool want[SDR_RX_NOUTPUTS] = {};
   size_t obytes = 0;
-  for (int i = 0; i < nout; ++i) obytes += sizeof(float) * (size_t)(r->out_n[which[i]] * r->S);
-  TRY(grow_dev(r, &r->iq_dev, &r->iq_cap, bytes));
-  TRY(grow_pinned(r, &r->pin_in, &r->pin_in_cap, bytes));
-  TRY(grow_pinned(r, reinterpret_cast<void**>(&r->pin_out), &r->pin_out_cap, std::max<size_t>(obytes, 16)));
-  // (one DMA: a chunked copy overlapping the host memcpy turns into per-chunk blit kernels)
-  std::memcpy(r->pin_in, iq_host, bytes);
-  HIP_TRY(hipMemcpyAsync(r->iq_dev, r->pin_in, bytes, hipMemcpyHostToDevice, st));
-  TRY(sdr_rx_process_dev(r, r->iq_dev, xs));
-  size_t off = 0;
   for (int i = 0; i < nout; ++i) {
     const int o = which[i];
+    if (want[o]) continue;
+    want[o] = true;
+    region[o] = obytes / sizeof(float);
+    obytes += sizeof(float) * (size_t)(r->out_n[o] * r->S);
+  }
+  TRY(grow_pinned(r, &r->pin_in, &r->pin_in_cap, bytes));
+  TRY(grow_pinned(r, reinterpret_cast<void**>(&r->pin_out), &r->pin_out_cap, std::max<size_t>(obytes, 16)));
+  std::memcpy(r->pin_in, iq_host, bytes);
+  for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) r->mirror[o] = want[o] && stage_output(o) ? r->pin_out + region[o] : nullptr;
+  const int rc = sdr_rx_process_dev(r, r->pin_in, xs);
+  for (float*& m : r->mirror) m = nullptr;
+  TRY(rc);
+  for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) {
+    if (!want[o] || stage_output(o)) continue;
     const int64_t n = r->out_n[o];
-    HIP_TRY(hipMemcpy2DAsync(r->pin_out + off, sizeof(float) * (size_t)n, r->out[o], sizeof(float) * (size_t)r->out_stride[o],
-                             sizeof(float) * (size_t)n, (size_t)r->S, hipMemcpyDeviceToHost, st));
-    off += (size_t)(n * r->S);
+    HIP_TRY(hipMemcpy2DAsync(r->pin_out + region[o], sizeof(float) * (size_t)n, r->out[o],
+                             sizeof(float) * (size_t)r->out_stride[o], sizeof(float) * (size_t)n, (size_t)r->S,
+                             hipMemcpyDeviceToHost, st));
   }
   HIP_TRY(hipStreamSynchronize(st));
-  off = 0;
   for (int i = 0; i < nout; ++i) {
     const int64_t n = r->out_n[which[i]];
     const int64_t os = (r->S > 1 && out_stride) ? out_stride[i] : n;
-    for (int s = 0; s < r->S; ++s) std::memcpy(out[i] + s * os, r->pin_out + off + s * n, sizeof(float) * (size_t)n);
-    off += (size_t)(n * r->S);
+    const float* src = r->pin_out + region[which[i]];
+    for (int s = 0; s < r->S; ++s) std::memcpy(out[i] + s * os, src + s * n, sizeof(float) * (size_t)n);
   }
   return SDR_OK;
 }
