@@ -22,7 +22,10 @@ Other workloads (`--workload`, one JSON line each; BASELINE.json configs):
       stream (>= 256 blocks per stream by default); per-stage GPU times from HIP events.
   c3 / c4  configs[2] / [3]: the per-block drop-in path at fmMonoBlock.py's 51 200-sample
       blocks, host buffers in and out (PCIe-inclusive by nature), one stream: mono (c3) or
-      mono + stereo (c4).
+      mono + stereo (c4).  Blocks are submitted as a live receiver feeds them (sdr_rx_submit:
+      block k runs while block k-1's outputs are delivered; the reference's rf / audio
+      thread overlap); the synchronous one-block call (sdr_rx_run) is timed beside it
+      ("sync", "block_latency_ms").  --no-pipeline: sdr_rx_run only.
   CPU baselines for these: the reference's own C++ receiver (src/filter.cpp, helper.cpp,
   rf_module.cpp compiled from its sources, oracle/ref_driver.cpp ref_rx_streams).
 
@@ -71,6 +74,8 @@ def parse():
     ap.add_argument("--path", choices=["fused", "split"], default="fused",
                     help="fused: one fe_mono_kernel (demod stays on chip); split: FE kernel + FIR kernel")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="c3/c4/c5: one block at a time (c3/c4: sdr_rx_run; c5: one stream of launches)")
     ap.add_argument("--split-stream", action="store_true",
                     help="mono: ONE stream of --blocks blocks split over the ranks, each range with a read-only "
                          "halo (SURVEY §8e; strong scaling) instead of one stream per rank")
@@ -458,8 +463,14 @@ def run_rx(args, ws, rank, local):
     rds = c5
     rf_taps = 151 if c5 else args.taps
     rf_b, au_b = rtsdr.design.mono_coeffs(rf_taps, args.audio_taps)
-    rx = rtsdr.Receiver(S, B, stereo=stereo, rds=rds, iq_dtype=np.uint8 if u8 else np.float32,
-                        rf_coeff=rf_b, audio_coeff=au_b, ctx=ctx)
+    pipe = not args.no_pipeline
+    # the second stream only pays where there is a back half (PLLs, stereo / RDS stages) to
+    # overlap; c3's two launches gain nothing from it but the cross-stream event hops
+    two_streams = pipe and (stereo or rds)
+    mk = lambda two: rtsdr.Receiver(S, B, stereo=stereo, rds=rds, iq_dtype=np.uint8 if u8 else np.float32,
+                                    rf_coeff=rf_b, audio_coeff=au_b, pipeline=two, ctx=ctx)
+    rx = mk(two_streams)
+    rx_sync = mk(False) if (pipe and not c5) else rx     # the one-block-at-a-time call
     nres = 16                                           # distinct blocks per stream, cycled
     dt = np.uint8 if u8 else np.float32
     # one synthetic stream per stream index (seed = rank * S + s), nres consecutive blocks
@@ -474,11 +485,17 @@ def run_rx(args, ws, rank, local):
         def step(k):
             rx.process_dev(d_iq.ptr + (k % nres) * blk_bytes, B)
     else:
-        def step(k):
-            o = rx.process(host[k % nres], fetch=fetch)
-            return o
+        def sync_step(k):
+            return rx_sync.process(host[k % nres], fetch=fetch)
+
+        def step(k):                         # block k launched, block k-1 delivered
+            if not pipe:
+                return sync_step(k)
+            return rx.submit(host[k % nres], fetch=fetch)
     for k in range(args.warmup):
         step(k)
+    if not c5:
+        rx.flush()
     ctx.synchronize()
     t_set = time.perf_counter()
     settle = 0
@@ -488,12 +505,23 @@ def run_rx(args, ws, rank, local):
             settle += 1
         ctx.synchronize()
     # per-stage GPU times (events between the receiver's launches), a separate pass
-    rx.set_timing(True)
+    (rx if c5 else rx_sync).set_timing(True)
     stages = []
     for k in range(8):
-        step(k)
-        stages.append(rx.stage_ms())
-    rx.set_timing(False)
+        rx.process_dev(d_iq.ptr + (k % nres) * blk_bytes, B) if c5 else rx_sync.process(host[k % nres], fetch=fetch)
+        stages.append((rx if c5 else rx_sync).stage_ms())
+    (rx if c5 else rx_sync).set_timing(False)
+    sync = None
+    if not c5 and pipe:                      # the synchronous drop-in call, for its latency
+        sl = []
+        for k in range(args.steps):
+            t = time.perf_counter()
+            sync_step(k)
+            sl.append(time.perf_counter() - t)
+        sl = np.array(sl) * 1e3
+        sync = {"ms_per_block": round(float(sl.mean()), 4), "p50": round(float(np.median(sl)), 4),
+                "p99": round(float(np.percentile(sl, 99)), 4),
+                "MS/s": round(S * B / (float(sl.mean()) * 1e-3) / 1e6, 1)}
     stage_ms = {key: round(float(np.mean([st[key] for st in stages])), 5) for key in stages[0]}
     barrier(ws)
     ctx.synchronize()
@@ -511,6 +539,7 @@ def run_rx(args, ws, rank, local):
             t = time.perf_counter()
             step(k)
             lat.append(time.perf_counter() - t)
+        rx.flush()
     ctx.synchronize()
     barrier(ws)
     elapsed = max_over_ranks(ws, time.perf_counter() - t0)
@@ -537,7 +566,11 @@ def run_rx(args, ws, rank, local):
                                     "c5": "configs[4]: independent streams, mono + stereo + RDS to the RRC output"}
                        [args.workload],
                        "block_complex": B, "streams_per_gpu": S, "rf_taps": rf_taps, "iq": "u8" if u8 else "f32",
-                       "parallelism": f"independent streams x{S * ws}"},
+                       "parallelism": f"independent streams x{S * ws}",
+                       "pipeline": " + ".join(
+                           (["sdr_rx_submit: block k launched while block k-1 is delivered"] if not c5 else [])
+                           + (["front half (FE, stage A) of block k beside the back half of k-1 (two streams)"]
+                              if two_streams else [])) or None},
             "roofline": {"bound": "hbm", "achieved": round(fe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(fe_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel": f"FE stage (fe_slot/ring kernel, {rf_taps} taps, + its zf and phase kernels)",
@@ -551,8 +584,12 @@ def run_rx(args, ws, rank, local):
             result["gpu_ms_per_block"] = round(gpu_ms, 5)
         else:
             la = np.array(lat) * 1e3
-            result["block_latency_ms"] = {"mean": round(float(la.mean()), 4), "p50": round(float(np.median(la)), 4),
-                                          "p99": round(float(np.percentile(la, 99)), 4)}
+            result["block_latency_ms"] = ({"mean": round(float(la.mean()), 4), "p50": round(float(np.median(la)), 4),
+                                           "p99": round(float(np.percentile(la, 99)), 4)} if sync is None else
+                                          {"mean": sync["ms_per_block"], "p50": sync["p50"], "p99": sync["p99"],
+                                           "note": "sdr_rx_run (one block in flight)"})
+            if sync is not None:
+                result["sync"] = sync
             result["realtime_factor"] = round((total / elapsed) / 2.4e6, 1)     # x the 2.4 MS/s input rate
     if ws == 1 and not args.no_cpu and rank == 0:
         result["cpu_baseline"] = ref_rx_baseline(args, host[:, 0].reshape(-1), B, u8, stereo, rds, rf_taps)
@@ -561,6 +598,7 @@ def run_rx(args, ws, rank, local):
     if rank == 0:
         print(json.dumps(result), flush=True)
     rx.close()
+    rx_sync.close()
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -234,6 +234,25 @@ int sdr_rx_process(sdr_rx* rx, const void* iq, int64_t iq_stride);       /* sync
  * pinned staging with one wait: the per-block drop-in call of fmMonoBlock.py's loop */
 int sdr_rx_run(sdr_rx* rx, const void* iq, int64_t iq_stride, int nout, const int* which,
                float* const* out, const int64_t* out_stride);
+/* The same without waiting for the block: the IQ is copied into one of two pinned slots and
+ * the chain is launched; then the PREVIOUSLY submitted block is waited for and its outputs
+ * written into the buffers given with it, and the call returns (so the host prepares block
+ * k+1 while block k runs: the reference's rf / audio thread overlap, src/fm_radio.cpp:783-792).
+ * The `out` buffers must stay valid until the next sdr_rx_submit / sdr_rx_flush / sdr_rx_run
+ * returns.  sdr_rx_flush delivers the last submitted block.  nout <= SDR_RX_MAXOUT. */
+enum { SDR_RX_MAXOUT = 32 };
+int sdr_rx_submit(sdr_rx* rx, const void* iq, int64_t iq_stride, int nout, const int* which,
+                  float* const* out, const int64_t* out_stride);
+int sdr_rx_flush(sdr_rx* rx);
+/* Pipelined receiver (set before the first block): block k's front half (FE and the
+ * filters of the demod) runs on a second stream while block k-1's back half (PLLs, stereo
+ * and RDS stages) runs on the context stream; the output rows alternate between two sets
+ * (sdr_rx_output gives the latest block's; block k's stay valid until block k+2 is
+ * processed).  sdr_rx_process_dev then does NOT order the front half after earlier work on
+ * the context stream: its IQ must be ready when it is called (device-resident data, or an
+ * upload that has been waited for).  The back half and everything after it on the context
+ * stream see block k complete, as without pipelining. */
+int sdr_rx_set_pipeline(sdr_rx* rx, int on);
 int sdr_rx_output(sdr_rx* rx, int which, float** dev, int64_t* stride, int64_t* n);
 int sdr_rx_fetch(sdr_rx* rx, int which, float* host, int64_t host_stride); /* sync, all streams */
 /* per-stage timing of the last block (HIP events between the receiver's launches, on the

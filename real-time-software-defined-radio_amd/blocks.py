@@ -41,7 +41,8 @@ class Receiver:
 
     def __init__(self, nstreams: int, block_complex: int, *, mono: bool = True, stereo: bool = False,
                  rds: bool = False, iq_dtype=np.uint8, rf_coeff=None, audio_coeff=None, stereo_taps: int = 151,
-                 rds_taps: int = 151, rf_decim: int = 10, audio_decim: int = 5, ctx=None):
+                 rds_taps: int = 151, rf_decim: int = 10, audio_decim: int = 5, pipeline: bool = False,
+                 ctx=None):
         self.ctx = ctx if ctx is not None else _lib.get_context()
         self.lib = self.ctx.lib
         self.S, self.B = int(nstreams), int(block_complex)
@@ -50,10 +51,13 @@ class Receiver:
         self.flags = flags
         self._lengths = {}
         self._plans = {}
+        self._pending = None                  # submit(): the block in flight's output arrays
         h = ctypes.c_void_p()
         check(self.lib.sdr_rx_create(self.ctx.handle, self.S, self.B, SDR_IQ_U8 if self.u8 else SDR_IQ_F32,
                                      flags, ctypes.byref(h)), "sdr_rx_create")
         self.handle = h
+        if pipeline:                          # front half of block k+1 beside the back half of k
+            check(self.lib.sdr_rx_set_pipeline(self.handle, 1), "sdr_rx_set_pipeline")
         if rf_coeff is None or audio_coeff is None:
             rc, ac = design.mono_coeffs()
             rf_coeff = rc if rf_coeff is None else rf_coeff
@@ -90,10 +94,7 @@ class Receiver:
             return bool(self.flags & SDR_RX_STEREO)
         return bool(self.flags & SDR_RX_RDS)
 
-    def process(self, iq, fetch=None):
-        """One block of every stream; returns {name: (nstreams, n) float32} for `fetch`
-        (default: the configuration's final outputs).  One C call: IQ up, the chain, the
-        outputs down, one wait (sdr_rx_run)."""
+    def _call(self, fn, iq, fetch):
         es = np.uint8 if self.u8 else np.float32
         iq = np.ascontiguousarray(iq, dtype=es)
         if iq.size != self.S * 2 * self.B:
@@ -108,9 +109,30 @@ class Receiver:
         names, which, lengths = plan
         outs = {n: np.empty((self.S, m), dtype=np.float32) for n, m in zip(names, lengths)}
         ptrs = (ctypes.c_void_p * len(names))(*[outs[n].ctypes.data for n in names])
-        check(self.lib.sdr_rx_run(self.handle, iq.ctypes.data, self.B, len(names), which, ptrs, None),
-              "sdr_rx_run")
+        check(getattr(self.lib, fn)(self.handle, iq.ctypes.data, self.B, len(names), which, ptrs, None), fn)
         return outs
+
+    def process(self, iq, fetch=None):
+        """One block of every stream; returns {name: (nstreams, n) float32} for `fetch`
+        (default: the configuration's final outputs).  One C call: IQ up, the chain, the
+        outputs down, one wait (sdr_rx_run)."""
+        if self._pending is not None:         # a submitted block is delivered (and dropped) first
+            self.flush()
+        return self._call("sdr_rx_run", iq, fetch)
+
+    def submit(self, iq, fetch=None):
+        """process() without waiting (sdr_rx_submit): launches this block and returns the
+        PREVIOUS submitted block's outputs (None for the first), so the host prepares the
+        next block while this one runs.  flush() returns the last block's."""
+        outs = self._call("sdr_rx_submit", iq, fetch)
+        prev, self._pending = self._pending, outs
+        return prev
+
+    def flush(self):
+        """Wait for the last submitted block; its outputs (or None)."""
+        check(self.lib.sdr_rx_flush(self.handle), "sdr_rx_flush")
+        prev, self._pending = self._pending, None
+        return prev
 
     def _length(self, name):
         if name not in self._lengths:
@@ -145,6 +167,7 @@ class Receiver:
 
     def reset(self):
         check(self.lib.sdr_rx_reset(self.handle), "sdr_rx_reset")
+        self._pending = None
 
     def set_timing(self, on: bool = True):
         """Record HIP events between the receiver's launches (stage_ms)."""

@@ -458,7 +458,8 @@ struct sdr_rx {
   PllCfg pll[2] = {};
   bool ready = false;
   int64_t M = 0, A = 0, R = 0;
-  float* out[SDR_RX_NOUTPUTS] = {};
+  float* out[SDR_RX_NOUTPUTS] = {};    // the rows of the latest block (one of outs[])
+  float* outs[2][SDR_RX_NOUTPUTS] = {}; // row sets; the second only when pipelined
   int64_t out_n[SDR_RX_NOUTPUTS] = {}, out_stride[SDR_RX_NOUTPUTS] = {};
   void* mem = nullptr;                 // one allocation for outputs, states and phases
   double* bank[2] = {};
@@ -480,6 +481,22 @@ struct sdr_rx {
                                         // stage stores each requested output into, or null
   int parity = 0;
   int64_t blocks = 0;
+  // sdr_rx_set_pipeline: block k's front half (FE, stage A) runs on `front` while block
+  // k-1's back half (B, PLLs, C, D, E) runs on the context stream; row set k % 2
+  int pipe = 0;
+  hipStream_t front = nullptr;
+  hipEvent_t ev_front[2] = {}, ev_back[2] = {}, ev_done[2] = {};
+  // sdr_rx_submit: pinned slots (input and outputs per block parity) and the block in flight
+  size_t in_slot = 0, out_slot = 0;
+  int64_t subs = 0;
+  struct Pending {
+    bool on = false;
+    int slot = 0, nout = 0;
+    int which[SDR_RX_MAXOUT] = {};
+    float* out[SDR_RX_MAXOUT] = {};
+    int64_t os[SDR_RX_MAXOUT] = {};
+    size_t region[SDR_RX_NOUTPUTS] = {};
+  } pend;
   bool timing = false;                 // events between the stages of each block
   hipEvent_t ev[SDR_RX_NSTAGES + 1] = {};
 };
@@ -557,9 +574,13 @@ int rx_finalize(sdr_rx* r) {
     }
     r->out_n[o] = n;
     r->out_stride[o] = st;
-    r->out[o] = reinterpret_cast<float*>((intptr_t)floats);   // offset for now
-    floats += st * S + 64;
   }
+  for (int q = 0; q < (r->pipe ? 2 : 1); ++q)
+    for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) {
+      if (!need_out(r, o)) continue;
+      r->outs[q][o] = reinterpret_cast<float*>((intptr_t)floats);   // offset for now
+      floats += r->out_stride[o] * S + 64;
+    }
   int64_t zl = 0;
   for (int z = 0; z < Z_N; ++z) {
     const int f = filter_of_zs(z);
@@ -578,8 +599,10 @@ int rx_finalize(sdr_rx* r) {
   hipError_t e = hipMalloc(&r->mem, bytes);
   if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx: hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
   char* base = static_cast<char*>(r->mem);
-  for (int o = 0; o < SDR_RX_NOUTPUTS; ++o)
-    if (need_out(r, o)) r->out[o] = reinterpret_cast<float*>(base) + (intptr_t)r->out[o];
+  for (int q = 0; q < (r->pipe ? 2 : 1); ++q)
+    for (int o = 0; o < SDR_RX_NOUTPUTS; ++o)
+      if (need_out(r, o)) r->outs[q][o] = reinterpret_cast<float*>(base) + (intptr_t)r->outs[q][o];
+  std::memcpy(r->out, r->outs[0], sizeof r->out);
   double* d = reinterpret_cast<double*>(base + round_up(floats * 4, 64));
   r->bank[0] = d;
   r->bank[1] = d + zl;
@@ -623,6 +646,7 @@ void sdr_rx_destroy(sdr_rx* r) {
   if (r == nullptr) return;
   if (r->c) {
     (void)hipSetDevice(r->c->device);
+    if (r->front) (void)hipStreamSynchronize(r->front);
     (void)hipStreamSynchronize(r->c->stream);
   }
   if (r->mem) (void)hipFree(r->mem);
@@ -630,6 +654,10 @@ void sdr_rx_destroy(sdr_rx* r) {
   if (r->pin_out) (void)hipHostFree(r->pin_out);
   for (hipEvent_t e : r->ev)
     if (e) (void)hipEventDestroy(e);
+  for (int q = 0; q < 2; ++q)
+    for (hipEvent_t e : {r->ev_front[q], r->ev_back[q], r->ev_done[q]})
+      if (e) (void)hipEventDestroy(e);
+  if (r->front) (void)hipStreamDestroy(r->front);
   delete r;
 }
 
@@ -668,6 +696,8 @@ int sdr_rx_reset(sdr_rx* r) {
   if (!r->ready) return SDR_OK;   // nothing allocated yet: the first block starts from zero
   TRY(set_dev(r->c));
   hipStream_t st = r->c->stream;
+  if (r->front) HIP_TRY(hipStreamSynchronize(r->front));
+  r->pend.on = false;                            // a submitted block's outputs are dropped
   // state banks, phases and wrap counters (contiguous)
   HIP_TRY(hipMemsetAsync(r->bank[0], 0, sizeof(double) * (size_t)(2 * r->bank_len + 2 * round_up(r->S, 2)), st));
   std::vector<double> ps(6 * (size_t)r->S);
@@ -680,6 +710,22 @@ int sdr_rx_reset(sdr_rx* r) {
   HIP_TRY(hipStreamSynchronize(st));
   r->parity = 0;
   r->blocks = 0;
+  std::memcpy(r->out, r->outs[0], sizeof r->out);
+  return SDR_OK;
+}
+
+int sdr_rx_set_pipeline(sdr_rx* r, int on) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (r->ready) return fail(SDR_EINVAL, "sdr_rx_set_pipeline: the receiver has processed a block");
+  if (on && !r->front) {
+    TRY(set_dev(r->c));
+    HIP_TRY(hipStreamCreateWithFlags(&r->front, hipStreamNonBlocking));
+    for (int q = 0; q < 2; ++q) {
+      HIP_TRY(hipEventCreateWithFlags(&r->ev_front[q], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&r->ev_back[q], hipEventDisableTiming));
+    }
+  }
+  r->pipe = on != 0;
   return SDR_OK;
 }
 
@@ -690,17 +736,32 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   if (!r->ready) TRY(rx_finalize(r));
   sdr_ctx* c = r->c;
   TRY(set_dev(c));
-  hipStream_t st = c->stream;
+  hipStream_t st = c->stream;             // the back half (everything when not pipelined)
   const int S = r->S;
   const int64_t M = r->M;
   double* zi = r->bank[r->parity];
   double* zf = r->bank[r->parity ^ 1];
-  auto mark = [&](int k) { return r->timing ? hipEventRecord(r->ev[k], st) : hipSuccess; };
-  HIP_TRY(mark(0));
+  const int q = r->pipe ? (int)(r->blocks & 1) : 0;
+  // FE: RF FIR + decimate + demod (fe.hip).  The tiled kernels take the reference's RF
+  // configurations; their carried state (I/Q zf, demod phase) is finished by workgroups of
+  // the stage-A launch.  Other configurations run sdr_rf_frontend_dev's generic path (on the
+  // context stream, so a pipelined receiver's front half runs there for such blocks).
+  const int Trf = (int)r->taps[SDR_RX_F_RF].size();
+  const int64_t xs = S > 1 ? iq_stride : r->B;
+  const int G = r->u8 ? 8 : 2;
+  const bool fast = (Trf == 101 || Trf == 151) && r->rf_decim == 10 && (S <= 1 || r->u8 || xs % G == 0) &&
+                    ((uintptr_t)iq % (r->u8 ? 4 : 16)) == 0;
+  hipStream_t fs = (r->pipe && fast) ? r->front : st;
+  if (r->pipe) {
+    if (r->blocks >= 1) HIP_TRY(hipStreamWaitEvent(fs, r->ev_front[q ^ 1], 0));   // states of block k-1
+    if (r->blocks >= 2) HIP_TRY(hipStreamWaitEvent(fs, r->ev_back[q], 0));        // set q read by k-2
+  }
+  auto mark = [&](int k, hipStream_t s) { return r->timing ? hipEventRecord(r->ev[k], s) : hipSuccess; };
+  HIP_TRY(mark(0, fs));
   auto zin = [&](int z) { return zi + r->zoff[z]; };
   auto out_of = [&](const float* y) {
     for (int o = 0; o < SDR_RX_NOUTPUTS; ++o)
-      if (r->out[o] == y && need_out(r, o)) return o;
+      if (r->outs[q][o] == y && need_out(r, o)) return o;
     return -1;
   };
   auto mirror_of = [&](const float* y) { const int o = out_of(y); return o < 0 ? nullptr : r->mirror[o]; };
@@ -710,23 +771,15 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   const TapSet* ts[SDR_RX_NFILTERS] = {};
   for (int f = 0; f < SDR_RX_NFILTERS; ++f)
     if (filter_used(r, f)) TRY(get_taps(c, r->taps[f].data(), (int)r->taps[f].size(), &ts[f]));
-  float** o = r->out;
+  float** o = r->outs[q];
   const int64_t ms = r->out_stride[SDR_RX_O_DEMOD];
-  // FE: RF FIR + decimate + demod (fe.hip).  The tiled kernels take the reference's RF
-  // configurations; their carried state (I/Q zf, demod phase) is finished by workgroups of
-  // the stage-A launch.  Other configurations run sdr_rf_frontend_dev's generic path.
-  const int Trf = (int)r->taps[SDR_RX_F_RF].size();
-  const int64_t xs = S > 1 ? iq_stride : r->B;
-  const int G = r->u8 ? 8 : 2;
-  const bool fast = (Trf == 101 || Trf == 151) && r->rf_decim == 10 && (S <= 1 || r->u8 || xs % G == 0) &&
-                    ((uintptr_t)iq % (r->u8 ? 4 : 16)) == 0;
   FeState fst{};
   if (fast) {
     const int64_t fstride = S > 1 ? xs : ceil_div(r->B, G) * G;
     FeLaunch a{iq, r->B, fstride, 0, S, ts[SDR_RX_F_RF]->dev_f32, &ts[SDR_RX_F_RF]->h, Trf, r->rf_decim, r->u8,
                zin(Z_FE_I), zin(Z_FE_Q), r->zlen[Z_FE_I], r->phase, o[SDR_RX_O_DEMOD], ms, nullptr, nullptr,
                r->last_phi, r->wraps};
-    HIP_TRY(sdr_launch_fe(a, st));
+    HIP_TRY(sdr_launch_fe(a, fs));
     fst = FeState{iq, r->B, xs, ts[SDR_RX_F_RF]->dev_f64, zin(Z_FE_I), zin(Z_FE_Q), zout(Z_FE_I), zout(Z_FE_Q),
                   r->zlen[Z_FE_I], r->last_phi, r->wraps, r->phase, Trf, r->u8, 1};
   } else {
@@ -734,7 +787,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
                             Trf, r->rf_decim, zin(Z_FE_I), zin(Z_FE_Q), r->zlen[Z_FE_I], zout(Z_FE_I), zout(Z_FE_Q),
                             r->phase, o[SDR_RX_O_DEMOD], ms, nullptr, nullptr));
   }
-  HIP_TRY(mark(1 + SDR_RX_ST_FE));
+  HIP_TRY(mark(1 + SDR_RX_ST_FE, fs));
   auto fir = [&](int f, int z, const float* x, int64_t n, int64_t xs, float* y, int64_t ys, int D, int pre = PRE_NONE,
                  const float* cmix = nullptr) {
     StageJob j{};
@@ -759,12 +812,16 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     A.push_back(fir(SDR_RX_F_STEREO_BPF, Z_BAND, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_BPF_EXTRACTION], ms, 1));
   }
   if (rd) A.push_back(fir(SDR_RX_F_RDS_EXTRACT, Z_EXTRACT, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_RDS_EXTRACT], ms, 1));
-  HIP_TRY(launch_stage(A, S, st, &fst));
-  HIP_TRY(mark(1 + SDR_RX_ST_A));
+  HIP_TRY(launch_stage(A, S, fs, &fst));
+  HIP_TRY(mark(1 + SDR_RX_ST_A, fs));
+  if (r->pipe) {
+    HIP_TRY(hipEventRecord(r->ev_front[q], fs));
+    HIP_TRY(hipStreamWaitEvent(st, r->ev_front[q], 0));
+  }
   // stage B: RDS squaring non-linearity + BPF (model/fmRDSblock.py:161-164)
   if (rd) HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_SQUARE, Z_SQUARE, o[SDR_RX_O_RDS_EXTRACT], M, ms,
                                     o[SDR_RX_O_RDS_PRE_PLL], ms, 1, PRE_SQUARE)}, S, st));
-  HIP_TRY(mark(1 + SDR_RX_ST_B));
+  HIP_TRY(mark(1 + SDR_RX_ST_B, st));
   // PLLs (model/fmMonoBlock.py:119, model/fmRDSblock.py:167): one lane per recurrence
   if (stx || rd) {
     PllJobs P{};
@@ -779,7 +836,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
                               r->pllc + (int64_t)S * r->cst, r->cst};
     HIP_TRY(sdr_launch_pll_jobs(P, st));
   }
-  HIP_TRY(mark(1 + SDR_RX_ST_PLL));
+  HIP_TRY(mark(1 + SDR_RX_ST_PLL, st));
   // stage C: mixers + LPFs; the stereo LPF's store also forms L and R
   std::vector<StageJob> C;
   if (stx) {
@@ -800,7 +857,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
                     o[SDR_RX_O_RDS_NCO_Q]));
   }
   HIP_TRY(launch_stage(C, S, st));
-  HIP_TRY(mark(1 + SDR_RX_ST_C));
+  HIP_TRY(mark(1 + SDR_RX_ST_C, st));
   if (rd) {
     // stage D: rational resamplers (fmRDSblock.py:184-199)
     const int64_t rs = r->out_stride[SDR_RX_O_RDS_RES_I];
@@ -813,15 +870,17 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       Dj.push_back(j);
     }
     HIP_TRY(launch_stage(Dj, S, st));
-    HIP_TRY(mark(1 + SDR_RX_ST_D));
+    HIP_TRY(mark(1 + SDR_RX_ST_D, st));
     // stage E: RRC (fmRDSblock.py:202-204)
     HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_RRC, Z_RRC_I, o[SDR_RX_O_RDS_RES_I], r->R, rs, o[SDR_RX_O_RDS_RRC_I], rs, 1),
                           fir(SDR_RX_F_RDS_RRC, Z_RRC_Q, o[SDR_RX_O_RDS_RES_Q], r->R, rs, o[SDR_RX_O_RDS_RRC_Q], rs, 1)},
                          S, st));
   } else {
-    HIP_TRY(mark(1 + SDR_RX_ST_D));
+    HIP_TRY(mark(1 + SDR_RX_ST_D, st));
   }
-  HIP_TRY(mark(1 + SDR_RX_ST_E));
+  HIP_TRY(mark(1 + SDR_RX_ST_E, st));
+  if (r->pipe) HIP_TRY(hipEventRecord(r->ev_back[q], st));
+  std::memcpy(r->out, r->outs[q], sizeof r->out);
   r->parity ^= 1;
   ++r->blocks;
   return SDR_OK;
@@ -849,32 +908,51 @@ int grow_pinned(sdr_rx* r, void** p, size_t* cap, size_t bytes) {
 bool stage_output(int o) {
   return o != SDR_RX_O_DEMOD && o != SDR_RX_O_STEREO_NCO && o != SDR_RX_O_RDS_NCO_I && o != SDR_RX_O_RDS_NCO_Q;
 }
+
+// Deliver the block in flight: wait for it, copy its rows out of pinned memory.
+int deliver(sdr_rx* r) {
+  sdr_rx::Pending& P = r->pend;
+  if (!P.on) return SDR_OK;
+  P.on = false;
+  HIP_TRY(hipEventSynchronize(r->ev_done[P.slot]));
+  const float* base = r->pin_out + (size_t)P.slot * r->out_slot / sizeof(float);
+  for (int i = 0; i < P.nout; ++i) {
+    const int64_t n = r->out_n[P.which[i]];
+    const float* src = base + P.region[P.which[i]];
+    for (int s = 0; s < r->S; ++s) std::memcpy(P.out[i] + s * P.os[i], src + s * n, sizeof(float) * (size_t)n);
+  }
+  return SDR_OK;
+}
+
 }  // namespace
 
 int sdr_rx_process(sdr_rx* r, const void* iq_host, int64_t iq_stride) {
   return sdr_rx_run(r, iq_host, iq_stride, 0, nullptr, nullptr, nullptr);
 }
 
-// One block from host memory.  The per-block cost at the reference's block sizes is the
-// number of engine hand-offs, not bytes (tools/xfer_probe.hip: an SDMA upload, two kernels,
-// an SDMA download and a wait take 35 us; the same kernels reading and writing pinned host
-// memory directly, 25 us), so: the IQ is copied into pinned host memory and the FE kernel
-// reads it from there over PCIe; each requested output is stored into pinned host memory by
-// the stage kernel that produces it (the demod and NCO rows, which no stage kernel stores,
-// come back by copy); the call waits once.
-int sdr_rx_run(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, const int* which, float* const* out,
-               const int64_t* out_stride) {
+// One block from host memory, without waiting for it.  The per-block cost at the
+// reference's block sizes is the number of engine hand-offs, not bytes
+// (tools/xfer_probe.hip: an SDMA upload, two kernels, an SDMA download and a wait take
+// 35 us; the same kernels reading and writing pinned host memory directly, 25 us), so: the
+// IQ is copied into a pinned slot and the FE kernel reads it from there over PCIe; each
+// requested output is stored into the slot's pinned output region by the stage kernel that
+// produces it (the demod and NCO rows, which no stage kernel stores, come back by copy).
+// Two slots by block parity: while block k runs, the host delivers block k-1's outputs
+// (into the buffers given with k-1) and returns; sdr_rx_flush delivers the last one.
+int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, const int* which, float* const* out,
+                  const int64_t* out_stride) {
   if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
-  if (iq_host == nullptr) return fail(SDR_EINVAL, "sdr_rx_run: iq is NULL");
-  if (r->S > 1 && iq_stride < r->B) return fail(SDR_EINVAL, "sdr_rx_run: iq_stride %lld < block", (long long)iq_stride);
-  if (nout < 0 || (nout > 0 && (which == nullptr || out == nullptr))) return fail(SDR_EINVAL, "sdr_rx_run: outputs");
+  if (iq_host == nullptr) return fail(SDR_EINVAL, "sdr_rx_submit: iq is NULL");
+  if (r->S > 1 && iq_stride < r->B) return fail(SDR_EINVAL, "sdr_rx_submit: iq_stride %lld < block", (long long)iq_stride);
+  if (nout < 0 || nout > SDR_RX_MAXOUT || (nout > 0 && (which == nullptr || out == nullptr)))
+    return fail(SDR_EINVAL, "sdr_rx_submit: %d outputs (at most %d)", nout, SDR_RX_MAXOUT);
   if (!r->ready) TRY(rx_finalize(r));
   for (int i = 0; i < nout; ++i) {
     if (which[i] < 0 || which[i] >= SDR_RX_NOUTPUTS || !need_out(r, which[i]))
-      return fail(SDR_EINVAL, "sdr_rx_run: output %d is not produced by flags 0x%x", which[i], r->flags);
-    if (out[i] == nullptr) return fail(SDR_EINVAL, "sdr_rx_run: output buffer %d is NULL", i);
+      return fail(SDR_EINVAL, "sdr_rx_submit: output %d is not produced by flags 0x%x", which[i], r->flags);
+    if (out[i] == nullptr) return fail(SDR_EINVAL, "sdr_rx_submit: output buffer %d is NULL", i);
     if (r->S > 1 && out_stride && out_stride[i] < r->out_n[which[i]])
-      return fail(SDR_EINVAL, "sdr_rx_run: out_stride[%d] too small", i);
+      return fail(SDR_EINVAL, "sdr_rx_submit: out_stride[%d] too small", i);
   }
   TRY(set_dev(r->c));
   hipStream_t st = r->c->stream;
@@ -882,38 +960,68 @@ int sdr_rx_run(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, cons
   const int64_t xs = r->S > 1 ? iq_stride : r->B;
   const size_t bytes = (size_t)(xs * (r->S - 1) + r->B) * es;
   // pinned output regions, one per distinct requested output (rows out_n apart)
-  size_t region[SDR_RX_NOUTPUTS];
+  sdr_rx::Pending P;
   bool want[SDR_RX_NOUTPUTS] = {};
   size_t obytes = 0;
   for (int i = 0; i < nout; ++i) {
     const int o = which[i];
+    P.which[i] = o;
+    P.out[i] = out[i];
+    P.os[i] = (r->S > 1 && out_stride) ? out_stride[i] : r->out_n[o];
     if (want[o]) continue;
     want[o] = true;
-    region[o] = obytes / sizeof(float);
+    P.region[o] = obytes / sizeof(float);
     obytes += sizeof(float) * (size_t)(r->out_n[o] * r->S);
   }
-  TRY(grow_pinned(r, &r->pin_in, &r->pin_in_cap, bytes));
-  TRY(grow_pinned(r, reinterpret_cast<void**>(&r->pin_out), &r->pin_out_cap, std::max<size_t>(obytes, 16)));
-  std::memcpy(r->pin_in, iq_host, bytes);
-  for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) r->mirror[o] = want[o] && stage_output(o) ? r->pin_out + region[o] : nullptr;
-  const int rc = sdr_rx_process_dev(r, r->pin_in, xs);
+  const size_t in_slot = (bytes + 255) / 256 * 256, out_slot = (std::max<size_t>(obytes, 16) + 255) / 256 * 256;
+  if (in_slot > r->in_slot || out_slot > r->out_slot) {   // grow (the block in flight is delivered first)
+    TRY(deliver(r));
+    TRY(grow_pinned(r, &r->pin_in, &r->pin_in_cap, 2 * in_slot));
+    TRY(grow_pinned(r, reinterpret_cast<void**>(&r->pin_out), &r->pin_out_cap, 2 * out_slot));
+    r->in_slot = std::max(r->in_slot, in_slot);
+    r->out_slot = std::max(r->out_slot, out_slot);
+    for (int q = 0; q < 2; ++q)
+      if (!r->ev_done[q]) HIP_TRY(hipEventCreateWithFlags(&r->ev_done[q], hipEventDisableTiming));
+  }
+  const int slot = (int)(r->subs & 1);
+  // slot `slot` was last used by block k-2, delivered (waited for) by the previous call
+  char* pin = static_cast<char*>(r->pin_in) + (size_t)slot * r->in_slot;
+  float* pout = r->pin_out + (size_t)slot * r->out_slot / sizeof(float);
+  std::memcpy(pin, iq_host, bytes);
+  for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) r->mirror[o] = want[o] && stage_output(o) ? pout + P.region[o] : nullptr;
+  const int rc = sdr_rx_process_dev(r, pin, xs);
   for (float*& m : r->mirror) m = nullptr;
   TRY(rc);
   for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) {
     if (!want[o] || stage_output(o)) continue;
     const int64_t n = r->out_n[o];
-    HIP_TRY(hipMemcpy2DAsync(r->pin_out + region[o], sizeof(float) * (size_t)n, r->out[o],
+    HIP_TRY(hipMemcpy2DAsync(pout + P.region[o], sizeof(float) * (size_t)n, r->out[o],
                              sizeof(float) * (size_t)r->out_stride[o], sizeof(float) * (size_t)n, (size_t)r->S,
                              hipMemcpyDeviceToHost, st));
   }
-  HIP_TRY(hipStreamSynchronize(st));
-  for (int i = 0; i < nout; ++i) {
-    const int64_t n = r->out_n[which[i]];
-    const int64_t os = (r->S > 1 && out_stride) ? out_stride[i] : n;
-    const float* src = r->pin_out + region[which[i]];
-    for (int s = 0; s < r->S; ++s) std::memcpy(out[i] + s * os, src + s * n, sizeof(float) * (size_t)n);
-  }
+  HIP_TRY(hipEventRecord(r->ev_done[slot], st));
+  ++r->subs;
+  TRY(deliver(r));                                       // block k-1
+  P.on = true;
+  P.slot = slot;
+  P.nout = nout;
+  r->pend = P;
   return SDR_OK;
+}
+
+int sdr_rx_flush(sdr_rx* r) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (!r->pend.on) return SDR_OK;
+  TRY(set_dev(r->c));
+  return deliver(r);
+}
+
+// One block from host memory, waited for: the per-block drop-in call of fmMonoBlock.py's loop.
+int sdr_rx_run(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, const int* which, float* const* out,
+               const int64_t* out_stride) {
+  if (r != nullptr) TRY(sdr_rx_flush(r));                // an earlier submit's block first
+  TRY(sdr_rx_submit(r, iq_host, iq_stride, nout, which, out, out_stride));
+  return sdr_rx_flush(r);
 }
 
 int sdr_rx_output(sdr_rx* r, int which, float** dev, int64_t* stride, int64_t* n) {

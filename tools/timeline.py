@@ -6,7 +6,7 @@ import sys
 
 d, pre = sys.argv[1], sys.argv[2]
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 40
-ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0][-48:])
+ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")[:60])
       for r in csv.DictReader(open(f"{d}/{pre}_kernel_trace.csv"))]
 try:
     ev += [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Direction"][12:])
