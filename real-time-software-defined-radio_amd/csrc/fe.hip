@@ -1294,6 +1294,8 @@ hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int
   const int64_t total = (int64_t)tps * a.nstreams;
   if (total > 0x7fffffff) return hipErrorInvalidValue;
   if (a.u8) {
+    const hipError_t em = sdr_launch_fe_mono_mfma(a, ataps, TA, DA, audio, audio_stride, st);
+    if (em != hipErrorInvalidValue) return em;
     SlotArgs sa{};
     sa.tps = tps; sa.total = total;
     sa.audio = audio; sa.audio_stride = audio_stride; sa.ataps = ataps;

@@ -1,0 +1,331 @@
+// u8 RF front end + mono audio on the matrix cores (gfx950 v_mfma_i32_16x16x64_i8).
+//
+// Replaces, for u8 IQ (src/iofunc.cpp:61-69, model/fmRDSblock.py:58-59) over whole streams:
+//   model/fmMonoBlock.py:86-95   lfilter(rf_coeff, 1.0, iq[0::2] / iq[1::2]) + [::10]
+//   model/fmMonoBlock.py:98      fmDemodArctan (model/fmSupportLib.py:15-44), state 0
+//   model/fmMonoBlock.py:101-109 lfilter(audio_coeff, ...) + [::5]
+//
+// Why integer MFMA: a u8 sample minus 128 is an exact int8, so the 101-tap RF FIR is an
+// integer product once the taps are fixed-point.  Taps are quantised to 22-bit integers
+// h_q = rint(h 2^S) (S from the largest tap) and split into three signed base-256 digits
+// h_q = d0 + 256 d1 + 65536 d2; each digit's FIR is accumulated EXACTLY in int32 by the
+// matrix cores, and y = (65536 acc2 + 256 acc1 + acc0) 2^-S / 128 is formed in f32 (two
+// roundings; the quantisation is 2^-22 of the largest tap -- the f32 FMA chain it replaces
+// rounds 101 times; the scale itself is never applied, atan2 is scale-free).  The FIR then
+// costs the matrix pipe, not the VALU: on the vector path (fe_slot_kernel) 303
+// v_pk_fma_f32 per 192 outputs were 56 % of the issue slots.
+//
+// GEMM form of one tile (256 decimated outputs m0 + 16 p + r, p, r in [0, 16)):
+//   y[16p + r] = sum_j' H[r][j'] X[j'][p],  H[r][j'] = h[10 r + 104 - j'] (0 outside [0, T)),
+//   X[j'][p] = x[10 m0 - 104 + 160 p + j'],  j' in [0, 256)
+// so M = 16 (r), N = 16 (p), K = 256 = 4 steps of 64; per channel and digit 4 MFMAs, per
+// tile 2 channels x 3 digits x 4 = 24 (K-order inside a step is the same map for A and B,
+// so it cancels).  The C fragment gives lane l = (p = l & 15, g = l >> 4) the outputs
+// 16 p + 4 g + i, i in [0, 4): four consecutive outputs per lane, I and Q in the same lane.
+//
+// Tile image: samples [10 m0 - 104, 10 m0 + 2552) (2656 = 332 chunks of 8), de-interleaved
+// into two int8 planes (x - 128 = u8 ^ 0x80) in LDS; the next tile's chunks are loaded into
+// registers while this tile computes.  Demod -> an LDS window of the audio block (5 tiles =
+// 1280 samples = 256 audio outputs, 4 per lane) after a 150-sample history; the audio FIR
+// (151 taps, f32) runs on the VALU at the block's end.  Each wave owns whole audio blocks
+// (a run starting mid-stream first runs the previous tile as a warm-up: history + carry).
+#include <cmath>
+
+#include "sdr_launch.h"
+
+namespace {
+
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+constexpr float kPiF = 3.14159265358979323846f;
+constexpr float k2PiF = 6.28318530717958647692f;
+
+struct MfmaFe {
+  const unsigned char* iq;  // interleaved u8 IQ, 16-B aligned, stream bases 16-B aligned
+  int64_t n, stride;        // complex samples per stream / between stream bases
+  int64_t M, A;             // demod / audio samples per stream
+  int bps;                  // audio blocks per stream
+  int64_t total;            // audio blocks over all streams
+  const float* taps;        // 101 RF taps (device)
+  float qscale;             // 2^S
+  const float* ataps;       // 151 audio taps (device)
+  float* audio;
+  int64_t audio_stride;
+};
+
+constexpr int D = 10, T = 101, TO = 256, OFF = 104;
+constexpr int IMG = D * TO + 96;          // image samples
+constexpr int NCH = IMG / 8;              // 16-B raw chunks (8 complex u8 samples)
+constexpr int NLD = (NCH + 63) / 64;      // chunks per lane
+constexpr int TA = 151, DA = 5, AB = DA * TO, HA = 152, NW = DA * 3 + TA;   // 166
+static_assert(IMG % 8 == 0 && NLD == 6, "image layout");
+static_assert(D * 15 + T - 1 + (OFF - 100 - 0) < 256 && OFF - (T - 1) >= 0, "K = 256 covers the band");
+
+// One wave per workgroup and a wave's LDS instructions execute in order, so ordering LDS
+// traffic between lanes needs no s_barrier (whose fence would also drain the image
+// prefetch's vmcnt): only the compiler must not move LDS accesses across this point.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+__device__ __forceinline__ unsigned bperm(int src_lane, unsigned v) {
+  return (unsigned)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+// one signed base-256 digit of a fixed-point tap
+__device__ __forceinline__ int digit(int q, int k) {
+  int d = 0;
+  for (int j = 0; j <= k; ++j) {
+    d = ((q & 0xff) ^ 0x80) - 0x80;
+    q = (q - d) >> 8;
+  }
+  return d;
+}
+
+__global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
+  __shared__ __attribute__((aligned(16))) signed char img[2][IMG + 16];   // I, Q planes
+  __shared__ __attribute__((aligned(16))) float dh[HA + AB + 8];
+  __shared__ __attribute__((aligned(16))) f4v ptab[NW + 2];
+
+  const int lane = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * p.total / gridDim.x;
+  const int64_t b1 = ((int64_t)blockIdx.x + 1) * p.total / gridDim.x;
+  if (b0 >= b1) return;
+  const int pl = lane & 15, gl = lane >> 4;
+
+  // A fragments: lane (r = l & 15, g = l >> 4), byte j of K-step ks <-> j' = 64 ks + 16 g + j
+  i4v afr[4][3];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    int w[3][4] = {};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = D * pl + OFF - (64 * ks + 16 * gl + j);
+      const float h = (k >= 0 && k < T) ? p.taps[k] : 0.f;
+      const int q = (int)rintf(h * p.qscale);
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg) w[dg][j >> 2] |= (digit(q, dg) & 0xff) << (8 * (j & 3));
+    }
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg) afr[ks][dg] = i4v{w[dg][0], w[dg][1], w[dg][2], w[dg][3]};
+  }
+  // audio tap quads: ptab[w] = {g[150-w], g[155-w], g[160-w], g[165-w]}
+  for (int w = lane; w < NW + 2; w += 64) {
+    float t4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = TA - 1 + DA * r - w;
+      t4[r] = (w < NW && k >= 0 && k < TA) ? p.ataps[k] : 0.f;
+    }
+    ptab[w] = f4v{t4[0], t4[1], t4[2], t4[3]};
+  }
+
+  // ---- image loads: chunk c = lane + 64 q of tile t's image (raw interleaved u8) ----
+  unsigned stg[NLD][4];
+  auto load_image = [&](int s, int64_t t) {
+    const int64_t n_lo = (int64_t)TO * D * t - OFF;
+    const unsigned char* base = p.iq + 2 * ((int64_t)s * p.stride + n_lo);
+    const bool interior = n_lo >= 0 && n_lo + IMG <= p.n;
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int c = lane + 64 * q;
+      if (c < NCH) {
+        if (interior) {
+          const i4v v = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(base) + c);
+          stg[q][0] = v.x; stg[q][1] = v.y; stg[q][2] = v.z; stg[q][3] = v.w;
+        } else {
+          unsigned w4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t n0 = n_lo + 8 * c + 2 * e;         // samples n0, n0 + 1
+            const unsigned lo = (n0 >= 0 && n0 < p.n) ? *reinterpret_cast<const unsigned short*>(base + 2 * (8 * c + 2 * e)) : 0x8080u;
+            const unsigned hi = (n0 + 1 >= 0 && n0 + 1 < p.n) ? *reinterpret_cast<const unsigned short*>(base + 2 * (8 * c + 2 * e + 1)) : 0x8080u;
+            w4[e] = lo | (hi << 16);
+          }
+          stg[q][0] = w4[0]; stg[q][1] = w4[1]; stg[q][2] = w4[2]; stg[q][3] = w4[3];
+        }
+      }
+    }
+  };
+  // de-interleave (I0 Q0 I1 Q1 ...) into the int8 planes: x - 128 = u8 ^ 0x80
+  auto store_image = [&]() {
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) {
+      const int c = lane + 64 * q;
+      if (c < NCH) {
+        const unsigned i_lo = __builtin_amdgcn_perm(stg[q][1], stg[q][0], 0x06040200u) ^ 0x80808080u;
+        const unsigned i_hi = __builtin_amdgcn_perm(stg[q][3], stg[q][2], 0x06040200u) ^ 0x80808080u;
+        const unsigned q_lo = __builtin_amdgcn_perm(stg[q][1], stg[q][0], 0x07050301u) ^ 0x80808080u;
+        const unsigned q_hi = __builtin_amdgcn_perm(stg[q][3], stg[q][2], 0x07050301u) ^ 0x80808080u;
+        *reinterpret_cast<uint2*>(&img[0][8 * c]) = make_uint2(i_lo, i_hi);
+        *reinterpret_cast<uint2*>(&img[1][8 * c]) = make_uint2(q_lo, q_hi);
+      }
+    }
+  };
+
+  // ---- run: audio blocks [b0, b1), warm-up tile first when starting mid-stream ----
+  int s = (int)(b0 / p.bps);
+  int64_t t = (b0 - (int64_t)s * p.bps) * DA;
+  const int64_t tps = (int64_t)p.bps * DA;
+  const bool warm = t > 0;
+  if (warm) --t;
+  const int64_t U = (b1 - b0) * DA + (warm ? 1 : 0);
+  for (int e = lane; e < HA; e += 64) dh[e] = 0.f;          // zero history at a stream start
+  load_image(s, t);
+  store_image();
+  int s_nx = s;
+  int64_t t_nx = t + 1;
+  if (t_nx == tps) { t_nx = 0; ++s_nx; }
+  if (U > 1) load_image(s_nx, t_nx);
+  float carry = 0.f;
+  float d4[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t u = 0; u < U; ++u) {
+    lds_order();                                              // image of tile t written
+    // B fragments of both channels, all four K-steps
+    i4v bf[2][4];
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        bf[ch][ks] = *reinterpret_cast<const i4v*>(&img[ch][160 * pl + 64 * ks + 16 * gl]);
+    i4v acc[2][3];
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg) acc[ch][dg] = i4v{0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int dg = 0; dg < 3; ++dg)
+          acc[ch][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch][ks], acc[ch][dg], 0, 0, 0);
+    // the next image replaces this one once the B reads have returned
+    const bool more = u + 1 < U;
+    lds_order();
+    if (more) {
+      store_image();
+      int s2 = s_nx;
+      int64_t t2 = t_nx + 1;
+      if (t2 == tps) { t2 = 0; ++s2; }
+      if (u + 2 < U) load_image(s2, t2);
+    }
+    // combine the digits, phases, predecessor, wrap
+    float phi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float yi = fmaf((float)acc[0][2][i], 65536.f, (float)acc[0][1][i] * 256.f) + (float)acc[0][0][i];
+      const float yq = fmaf((float)acc[1][2][i], 65536.f, (float)acc[1][1][i] * 256.f) + (float)acc[1][0][i];
+      phi[i] = fast_atan2f(yq, yi);      // atan2 is scale-free: the 2^-S / 128 is never applied
+    }
+    const int src = gl > 0 ? lane - 16 : (pl > 0 ? lane + 47 : 63);
+    const float left = __uint_as_float(bperm(src, __float_as_uint(phi[3])));
+    float prev = (lane == 0) ? carry : left;
+    const int64_t mo = (int64_t)TO * t + 16 * pl + 4 * gl;     // first output of this lane
+    float d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float dd = phi[i] - prev;
+      if (dd > kPiF) dd -= k2PiF;
+      else if (dd < -kPiF) dd += k2PiF;
+      d[i] = (mo + i == 0) ? phi[i] : dd;                     // m = 0: prev_phase 0
+      prev = phi[i];
+    }
+    carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[3]), 63));
+    const int o = 16 * pl + 4 * gl;                           // output within the tile
+    const int tb = (int)(t % DA);
+    if (warm && u == 0) {                                     // history of the first block
+      if (o >= TO - HA) *reinterpret_cast<f4v*>(&dh[HA - TO + o]) = f4v{d[0], d[1], d[2], d[3]};
+    } else {
+      *reinterpret_cast<f4v*>(&dh[HA + TO * tb + o]) = f4v{d[0], d[1], d[2], d[3]};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d4[i] = d[i];
+    }
+    if (!(warm && u == 0) && tb == DA - 1) {
+      // audio block jb: a[j] = sum_k g[k] d[5j - k], lane -> j = 256 jb + 4 l + r
+      lds_order();
+      const float* aw = dh + (HA - (TA - 1)) + DA * 4 * lane;
+      f2v a01 = f2v{0.f, 0.f}, a23 = f2v{0.f, 0.f}, b01 = f2v{0.f, 0.f}, b23 = f2v{0.f, 0.f};
+#pragma unroll 4
+      for (int w = 0; w < NW; w += 2) {
+        const f2v x2 = *reinterpret_cast<const f2v*>(aw + w);
+        const f4v t0 = ptab[w], t1 = ptab[w + 1];
+        pk_fma_bcast_x<false>(a01, f2v{t0.x, t0.y}, x2);
+        pk_fma_bcast_x<false>(a23, f2v{t0.z, t0.w}, x2);
+        pk_fma_bcast_x<true>(b01, f2v{t1.x, t1.y}, x2);
+        pk_fma_bcast_x<true>(b23, f2v{t1.z, t1.w}, x2);
+      }
+      const f2v r01 = a01 + b01, r23 = a23 + b23;
+      const int64_t jb = t / DA;
+      const int64_t j = TO * jb + 4 * lane;
+      float* ao = p.audio + (int64_t)s * p.audio_stride + j;
+      if (j + 4 <= p.A && ((uintptr_t)ao & 15) == 0) {
+        *reinterpret_cast<f4v*>(ao) = f4v{r01.x, r01.y, r23.x, r23.y};
+      } else {
+        const float rv[4] = {r01.x, r01.y, r23.x, r23.y};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (j + r < p.A) ao[r] = rv[r];
+      }
+      lds_order();
+      // this block's last 150 demod samples become the next block's history
+      if (o >= TO - HA) *reinterpret_cast<f4v*>(&dh[HA - TO + o]) = f4v{d4[0], d4[1], d4[2], d4[3]};
+    }
+    // advance
+    if (more) {
+      s = s_nx;
+      t = t_nx;
+      if (t == 0) {                                           // new stream: zero history
+        lds_order();
+        for (int e = lane; e < HA; e += 64) dh[e] = 0.f;
+      }
+      t_nx = t + 1;
+      s_nx = s;
+      if (t_nx == tps) { t_nx = 0; ++s_nx; }
+    }
+  }
+}
+
+}  // namespace
+
+// Fused u8 FE + mono on the matrix cores.  Supported: 101 RF taps at decim 10, 151 audio
+// taps at decim 5, u8 IQ with 16-B aligned stream bases; otherwise hipErrorInvalidValue
+// (the caller runs fe_slot_kernel).
+hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps, int TA_, int DA_, float* audio,
+                                   int64_t audio_stride, hipStream_t st) {
+  if (!a.u8 || a.D != D || a.T != T || TA_ != TA || DA_ != DA || a.hist != 0 || a.zi_i || a.prev_phase || a.demod ||
+      a.i_ds || a.last_phi || a.wraps)
+    return hipErrorInvalidValue;
+  if (((uintptr_t)a.iq & 15) != 0 || (a.nstreams > 1 && (a.stride % 8) != 0)) return hipErrorInvalidValue;
+  if (a.n <= 0 || a.nstreams <= 0) return hipSuccess;
+  float hmax = 0.f;
+  for (int k = 0; k < T; ++k) hmax = std::max(hmax, std::fabs(a.taps->h[k]));
+  if (!(hmax > 0.f) || !std::isfinite(hmax)) return hipErrorInvalidValue;
+  // |h_q| <= 2^22: the top digit stays within [-65, 65]
+  const int S = 22 - (int)std::ceil(std::log2((double)hmax));
+  MfmaFe p{};
+  p.iq = static_cast<const unsigned char*>(a.iq);
+  p.n = a.n;
+  p.stride = a.nstreams > 1 ? a.stride : 0;
+  p.M = (a.n + D - 1) / D;
+  p.A = (p.M + DA - 1) / DA;
+  p.bps = (int)((p.M + AB - 1) / AB);
+  p.total = (int64_t)p.bps * a.nstreams;
+  if (p.total > 0x7fffffff) return hipErrorInvalidValue;
+  p.taps = a.taps_dev;
+  p.qscale = std::ldexp(1.0f, S);
+  p.ataps = ataps;
+  p.audio = audio;
+  p.audio_stride = audio_stride;
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, per = 0;
+    hipDeviceProp_t prop;
+    int cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_mono_kernel, 64, 0) != hipSuccess || per <= 0) per = 1;
+    slots = cus * std::min(per, 12);
+  }
+  const int64_t grid = std::min<int64_t>(slots, p.total);
+  hipLaunchKernelGGL(fe_mfma_mono_kernel, dim3((unsigned)grid), dim3(64), 0, st, p);
+  return hipGetLastError();
+}

@@ -30,6 +30,10 @@ struct PllCfg { double freq, fs, scale, adj, kp, ki; };
 hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st);
 hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
                               int64_t audio_stride, hipStream_t st);
+// u8 FE + mono with the RF FIR on the int8 matrix cores (fe_mfma.hip); hipErrorInvalidValue
+// when the configuration is not the one it covers
+hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
+                                   int64_t audio_stride, hipStream_t st);
 hipError_t sdr_launch_iq_zf(const void* iq, int u8, int64_t n, int64_t stride, int nstreams,
                             const double* b_dev, int T, const double* zi_i, const double* zi_q,
                             int64_t zi_stride, double* zf_i, double* zf_q, hipStream_t st);

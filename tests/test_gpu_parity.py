@@ -365,6 +365,23 @@ def test_fm_mono_streams_u8_ragged(sdr, gpu_ctx, oracle, n):
         assert rms(got[s], ref) < AUDIO_RMS and maxabs(got[s], ref) < AUDIO_MAX, (s, rms(got[s], ref))
 
 
+@pytest.mark.parametrize("n", [8, 25_600, 64000 * 3 + 16, 1_024_000])
+def test_fm_mono_streams_u8_mfma(sdr, gpu_ctx, oracle, n):
+    """u8 IQ with 16-B aligned stream bases: the fused front end on the int8 matrix cores
+    (fe_mfma.hip: fixed-point taps in three base-256 digits, exact int32 accumulation) over
+    4 streams (more audio blocks than one per wave: runs start mid-stream) == the f64 oracle
+    at the same audio tolerance as the f32 kernels."""
+    rf_b, au_b = sdr.design.mono_coeffs(101, 151)
+    S = 4
+    iq = np.stack([sdr.synth.fm_iq(n, seed=90 + s, dtype=np.uint8) for s in range(S)])
+    got = sdr.fm_mono_streams(iq, rf_b, au_b)
+    for s in range(S):
+        ref, _ = oracle.mono_basic_coeffs((iq[s].astype(np.float64) - 128.0) / 128.0, rf_b, au_b)
+        assert got[s].shape == ref.shape
+        assert rms(got[s], ref) < AUDIO_RMS and maxabs(got[s], ref) < AUDIO_MAX, (s, rms(got[s], ref),
+                                                                                 maxabs(got[s], ref))
+
+
 # ---------------------------------------------------------------------------- split stream
 @pytest.mark.parametrize("taps", [101, 151])
 def test_split_stream_ranges_equal_single_pass(sdr, gpu_ctx, taps):
