@@ -283,7 +283,7 @@ def main():
         _lib.check(lib.sdr_fir_dev(h, d_dm.ptr, None, 1.0, 0, M, M, 0, 1, aup, TA, 5, None, 0, None, d_au.ptr, A),
                    "mono")
 
-    # fused: fe_ring_kernel for f32 IQ, fe_slot_kernel (u8 converted on the way in) for u8
+    # fused: fe_ring_kernel for f32 IQ, fe_mfma_mono_kernel (RF FIR on the int8 matrix cores) for u8
     stages = [fused] if args.path == "fused" else [fe, mono]
     tm = _lib.Timer(ctx)
     # fused: one kernel per step -> one event pair around the whole timed region (per-step
@@ -332,7 +332,9 @@ def main():
     if args.path == "fused" and lib.sdr_fe_mono_fused(T, 10, TA, 5):
         # compulsory HBM bytes of the fused kernel: IQ in + audio out
         k_bytes = n * bpc + A * 4
-        kname = (f"fe_slot_kernel<{args.taps},fused,u8>" if args.iq == "u8" else f"fe_ring_kernel<{args.taps},fused>") + \
+        # u8: the int8-MFMA kernel takes 16-B aligned stream bases (every stride here is)
+        kname = ("fe_mfma_mono_kernel (RF FIR on v_mfma_i32_16x16x64_i8)" if args.iq == "u8"
+                 else f"fe_ring_kernel<{args.taps},fused>") + \
             f" (sdr_fe_mono_dev: FE {args.taps} taps + audio {args.audio_taps} taps)"
         kernels = {"fe_mono": round(k_avg, 5)}
     elif args.path == "fused":

@@ -118,46 +118,59 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
     ptab[w] = f4v{t4[0], t4[1], t4[2], t4[3]};
   }
 
-  // ---- image loads: chunk c = lane + 64 q of tile t's image (raw interleaved u8) ----
-  unsigned stg[NLD][4];
+  // ---- tile images: chunk c = lane + 64 q (16 raw bytes = 8 complex u8 samples) ----
+  // Interior images: hand-issued 16-B loads into stg, waited for (one s_waitcnt) when the
+  // image is written, at the end of the tile before (compiler-placed waits serialised the
+  // loads one at a time).  Only the asm loads write stg: a second, compiler-visible writer
+  // made the compiler merge the two through register copies taken before the data landed.
+  // Boundary images (stream head / tail: zeros, 0x80, outside [0, n)) are built at write
+  // time from guarded 2-B loads.
+  f4v stg[NLD];
+  const unsigned voff = 16u * lane;
+  auto n_lo_of = [&](int64_t t) { return (int64_t)TO * D * t - OFF; };
+  auto interior = [&](int64_t t) { return n_lo_of(t) >= 0 && n_lo_of(t) + IMG <= p.n; };
+  auto base_of = [&](int s, int64_t t) { return p.iq + 2 * ((int64_t)s * p.stride + n_lo_of(t)); };
   auto load_image = [&](int s, int64_t t) {
-    const int64_t n_lo = (int64_t)TO * D * t - OFF;
-    const unsigned char* base = p.iq + 2 * ((int64_t)s * p.stride + n_lo);
-    const bool interior = n_lo >= 0 && n_lo + IMG <= p.n;
+    const unsigned char* base = base_of(s, t);
+    static_for<0, NLD>([&](auto Q) {
+      constexpr int q = Q;
+      if (q < NLD - 1 || lane < NCH - 64 * (NLD - 1)) gload16_nt_v<0>(stg[q], voff, base + 1024 * q);
+    });
+  };
+  // de-interleave (I0 Q0 I1 Q1 ...) into the int8 planes: x - 128 = u8 ^ 0x80
+  auto put_chunk = [&](int c, unsigned w0, unsigned w1, unsigned w2, unsigned w3) {
+    const unsigned i_lo = __builtin_amdgcn_perm(w1, w0, 0x06040200u) ^ 0x80808080u;
+    const unsigned i_hi = __builtin_amdgcn_perm(w3, w2, 0x06040200u) ^ 0x80808080u;
+    const unsigned q_lo = __builtin_amdgcn_perm(w1, w0, 0x07050301u) ^ 0x80808080u;
+    const unsigned q_hi = __builtin_amdgcn_perm(w3, w2, 0x07050301u) ^ 0x80808080u;
+    *reinterpret_cast<uint2*>(&img[0][8 * c]) = make_uint2(i_lo, i_hi);
+    *reinterpret_cast<uint2*>(&img[1][8 * c]) = make_uint2(q_lo, q_hi);
+  };
+  auto store_image = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
       const int c = lane + 64 * q;
       if (c < NCH) {
-        if (interior) {
-          const i4v v = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(base) + c);
-          stg[q][0] = v.x; stg[q][1] = v.y; stg[q][2] = v.z; stg[q][3] = v.w;
-        } else {
-          unsigned w4[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int64_t n0 = n_lo + 8 * c + 2 * e;         // samples n0, n0 + 1
-            const unsigned lo = (n0 >= 0 && n0 < p.n) ? *reinterpret_cast<const unsigned short*>(base + 2 * (8 * c + 2 * e)) : 0x8080u;
-            const unsigned hi = (n0 + 1 >= 0 && n0 + 1 < p.n) ? *reinterpret_cast<const unsigned short*>(base + 2 * (8 * c + 2 * e + 1)) : 0x8080u;
-            w4[e] = lo | (hi << 16);
-          }
-          stg[q][0] = w4[0]; stg[q][1] = w4[1]; stg[q][2] = w4[2]; stg[q][3] = w4[3];
-        }
+        asm volatile("" : "+v"(stg[q]));
+        put_chunk(c, __float_as_uint(stg[q].x), __float_as_uint(stg[q].y), __float_as_uint(stg[q].z),
+                  __float_as_uint(stg[q].w));
       }
     }
   };
-  // de-interleave (I0 Q0 I1 Q1 ...) into the int8 planes: x - 128 = u8 ^ 0x80
-  auto store_image = [&]() {
+  auto build_guarded = [&](int s, int64_t t) {
+    const int64_t n_lo = n_lo_of(t);
+    const unsigned char* base = base_of(s, t);
+    for (int c = lane; c < NCH; c += 64) {
+      unsigned w4[4];
 #pragma unroll
-    for (int q = 0; q < NLD; ++q) {
-      const int c = lane + 64 * q;
-      if (c < NCH) {
-        const unsigned i_lo = __builtin_amdgcn_perm(stg[q][1], stg[q][0], 0x06040200u) ^ 0x80808080u;
-        const unsigned i_hi = __builtin_amdgcn_perm(stg[q][3], stg[q][2], 0x06040200u) ^ 0x80808080u;
-        const unsigned q_lo = __builtin_amdgcn_perm(stg[q][1], stg[q][0], 0x07050301u) ^ 0x80808080u;
-        const unsigned q_hi = __builtin_amdgcn_perm(stg[q][3], stg[q][2], 0x07050301u) ^ 0x80808080u;
-        *reinterpret_cast<uint2*>(&img[0][8 * c]) = make_uint2(i_lo, i_hi);
-        *reinterpret_cast<uint2*>(&img[1][8 * c]) = make_uint2(q_lo, q_hi);
+      for (int e = 0; e < 4; ++e) {
+        const int64_t n0 = n_lo + 8 * c + 2 * e;             // samples n0, n0 + 1
+        const unsigned lo = (n0 >= 0 && n0 < p.n) ? *reinterpret_cast<const unsigned short*>(base + 2 * (8 * c + 2 * e)) : 0x8080u;
+        const unsigned hi = (n0 + 1 >= 0 && n0 + 1 < p.n) ? *reinterpret_cast<const unsigned short*>(base + 2 * (8 * c + 2 * e + 1)) : 0x8080u;
+        w4[e] = lo | (hi << 16);
       }
+      put_chunk(c, w4[0], w4[1], w4[2], w4[3]);
     }
   };
 
@@ -169,16 +182,25 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
   if (warm) --t;
   const int64_t U = (b1 - b0) * DA + (warm ? 1 : 0);
   for (int e = lane; e < HA; e += 64) dh[e] = 0.f;          // zero history at a stream start
-  load_image(s, t);
-  store_image();
+  if (interior(t)) {
+    load_image(s, t);
+    store_image();
+  } else {
+    build_guarded(s, t);
+  }
   int s_nx = s;
   int64_t t_nx = t + 1;
   if (t_nx == tps) { t_nx = 0; ++s_nx; }
-  if (U > 1) load_image(s_nx, t_nx);
   float carry = 0.f;
   float d4[4] = {0.f, 0.f, 0.f, 0.f};
 
   for (int64_t u = 0; u < U; ++u) {
+    // the next tile's loads fly during this tile's MFMAs, epilogue and audio; they are
+    // waited for and written to LDS at the end of the iteration (an in-flight register
+    // never crosses the loop's back edge, where the compiler may copy it)
+    const bool more = u + 1 < U;
+    const bool staged = more && interior(t_nx);
+    if (staged) load_image(s_nx, t_nx);
     lds_order();                                              // image of tile t written
     // B fragments of both channels, all four K-steps
     i4v bf[2][4];
@@ -199,16 +221,6 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
 #pragma unroll
         for (int dg = 0; dg < 3; ++dg)
           acc[ch][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch][ks], acc[ch][dg], 0, 0, 0);
-    // the next image replaces this one once the B reads have returned
-    const bool more = u + 1 < U;
-    lds_order();
-    if (more) {
-      store_image();
-      int s2 = s_nx;
-      int64_t t2 = t_nx + 1;
-      if (t2 == tps) { t2 = 0; ++s2; }
-      if (u + 2 < U) load_image(s2, t2);
-    }
     // combine the digits, phases, predecessor, wrap
     float phi[4];
 #pragma unroll
@@ -270,8 +282,11 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
       // this block's last 150 demod samples become the next block's history
       if (o >= TO - HA) *reinterpret_cast<f4v*>(&dh[HA - TO + o]) = f4v{d4[0], d4[1], d4[2], d4[3]};
     }
-    // advance
+    // advance: the next image replaces this one (its B reads returned long ago)
     if (more) {
+      lds_order();
+      if (staged) store_image();
+      else build_guarded(s_nx, t_nx);
       s = s_nx;
       t = t_nx;
       if (t == 0) {                                           // new stream: zero history
