@@ -213,6 +213,19 @@ def cpu_threads():
     return env if env > 0 else cpu_cores()[0]
 
 
+def copy_bandwidth(lib, handle, nbytes: int = 2 << 30, reps: int = 10):
+    """the achieved fraction beside a measured copy kernel on the same box --
+    libsdr's 16-B-per-lane streaming copy (sdr_copy_bandwidth), best of `reps`, GB/s counting
+    read + write.  (torch's own copy kernel cannot be used here: torch bundles its own HIP
+    runtime, which does not initialise in a process that already runs libsdr's.)"""
+    g = ctypes.c_double()
+    rc = lib.sdr_copy_bandwidth(handle, nbytes, reps, ctypes.byref(g))
+    if rc != 0:
+        print(f"bench: copy bandwidth not measured: {lib.sdr_last_error().decode()}", file=sys.stderr)
+        return None
+    return round(g.value, 1)
+
+
 def load_traffic(path, taps, blocks, kpath):
     """HBM bytes per launch of the dominant kernel, from tools/pmc_traffic.py's PMC summary."""
     try:
@@ -385,6 +398,10 @@ def main():
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "settle": {"untimed_steps": settle_steps, "min_ms": args.settle_ms},
         }
+    if rank == 0:
+        cbw = copy_bandwidth(lib, h)
+        result["roofline"]["copy_kernel_gbs"] = cbw
+        result["roofline"]["frac_of_copy"] = round(achieved / cbw, 4) if cbw else None
     if ws == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, rf_b, au_b)
     elif rank == 0:

@@ -74,6 +74,10 @@ int sdr_event_create(sdr_ctx* ctx, void** ev);
 int sdr_event_record(sdr_ctx* ctx, void* ev);
 int sdr_event_elapsed_ms(void* ev0, void* ev1, float* ms);
 int sdr_event_destroy(void* ev);
+/* The box's copy-kernel bandwidth (the roofline fraction beside a measured copy):
+ * a 16-B-per-lane streaming copy of `bytes` on the context stream, best of `reps` after two
+ * warm-ups; *gbs counts read + write.  Synchronous; allocates 2 x bytes for the call. */
+int sdr_copy_bandwidth(sdr_ctx* ctx, int64_t bytes, int reps, double* gbs);
 
 /* ================================================================================
  * Host-buffer drop-in entry points (synchronous)

@@ -103,6 +103,16 @@ int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T) 
 }  // namespace sdrint
 
 namespace {
+// streaming copy (16 B per lane, grid-stride): the box's copy-kernel bandwidth, measured beside
+// the path's kernels
+typedef float cp4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void copy_probe_kernel(const cp4* __restrict__ a, cp4* __restrict__ b, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i);
+}
+}  // namespace
+
+namespace {
 
 int h2d(sdr_ctx* c, void* dst, const void* src, size_t bytes) {
   if (bytes) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
@@ -231,6 +241,47 @@ int sdr_event_elapsed_ms(void* ev0, void* ev1, float* ms) {
 }
 int sdr_event_destroy(void* ev) {
   if (ev) HIP_TRY(hipEventDestroy((hipEvent_t)ev));
+  return SDR_OK;
+}
+
+int sdr_copy_bandwidth(sdr_ctx* c, int64_t bytes, int reps, double* gbs) {
+  CHECK_CTX(c);
+  if (gbs == nullptr || bytes < 16 || reps < 1) return fail(SDR_EINVAL, "sdr_copy_bandwidth: bytes %lld, reps %d",
+                                                            (long long)bytes, reps);
+  TRY(set_dev(c));
+  const int64_t n4 = bytes / 16;
+  void *a = nullptr, *b = nullptr;
+  hipError_t e = hipMalloc(&a, (size_t)n4 * 16);
+  if (e == hipSuccess) e = hipMalloc(&b, (size_t)n4 * 16);
+  if (e != hipSuccess) {
+    if (a) (void)hipFree(a);
+    return fail(SDR_ENOMEM, "sdr_copy_bandwidth: hipMalloc: %s", hipGetErrorString(e));
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) cus = prop.multiProcessorCount;
+  const unsigned grid = (unsigned)std::min<int64_t>((int64_t)cus * 8, (n4 + 255) / 256);
+  float best = 0.f;
+  e = hipMemsetAsync(a, 0, (size_t)n4 * 16, c->stream);
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  for (int r = 0; r < reps + 2 && e == hipSuccess; ++r) {
+    e = hipEventRecord(e0, c->stream);
+    hipLaunchKernelGGL(copy_probe_kernel, dim3(grid), dim3(256), 0, c->stream, (const cp4*)a, (cp4*)b, n4);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (r >= 2 && (best == 0.f || ms < best)) best = ms;    // two warm-up copies
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(a);
+  (void)hipFree(b);
+  if (e != hipSuccess) return fail(SDR_EHIP, "sdr_copy_bandwidth: %s", hipGetErrorString(e));
+  *gbs = 2.0 * (double)(n4 * 16) / ((double)best * 1e-3) / 1e9;
   return SDR_OK;
 }
 

@@ -382,6 +382,20 @@ def test_fm_mono_streams_u8_mfma(sdr, gpu_ctx, oracle, n):
                                                                                  maxabs(got[s], ref))
 
 
+@pytest.mark.parametrize("gain", [37.0, 1e-3])
+def test_fm_mono_streams_u8_mfma_tap_scale(sdr, gpu_ctx, oracle, gain):
+    """The int8-MFMA front end quantises the taps against their largest magnitude (2^S), so a
+    filter of any gain -- here the reference's 101-tap LPF scaled by 37 and by 1e-3 --
+    demodulates as the f64 oracle does (atan2 never sees the scale)."""
+    rf_b, au_b = sdr.design.mono_coeffs(101, 151)
+    rf_b = rf_b * gain
+    iq = np.stack([sdr.synth.fm_iq(64_000, seed=95 + s, dtype=np.uint8) for s in range(2)])
+    got = sdr.fm_mono_streams(iq, rf_b, au_b)
+    for s in range(2):
+        ref, _ = oracle.mono_basic_coeffs((iq[s].astype(np.float64) - 128.0) / 128.0, rf_b, au_b)
+        assert rms(got[s], ref) < AUDIO_RMS and maxabs(got[s], ref) < AUDIO_MAX, (s, rms(got[s], ref))
+
+
 # ---------------------------------------------------------------------------- split stream
 @pytest.mark.parametrize("taps", [101, 151])
 def test_split_stream_ranges_equal_single_pass(sdr, gpu_ctx, taps):

@@ -1,10 +1,13 @@
 // A/B probe for the PLL fast step (not product code): times the product pll_lanes kernel
-// (pll.o, sdr_launch_pll_jobs) against candidate step forms on the same inputs, and reports
-// ns per sample step and the deviation of each candidate's phases from the product's.
+// (sdr_launch_pll_jobs: prep + loop + NCO) and bare loop kernels of candidate step forms on
+// the product's per-sample constants, and reports ns per sample step and each candidate's
+// deviation from the product's phases (the variants start from the stream-start state and
+// take every group's first sample by the fast form too, so small deviations are expected).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/pll_probe.hip -o tools/pll_probe \
 //     -Lreal-time-software-defined-radio_amd -lsdr -Wl,-rpath,$ORIGIN/../real-time-software-defined-radio_amd
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -15,149 +18,181 @@
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 namespace {
-constexpr double kP1 = 6.2831854820251465, kP2 = -1.748455600074497e-07, kP3 = -1.0687562935444062e-23;
 constexpr double kInv2Pi = 0.15915494309189535, kPi = 3.14159265358979323846, k2Pi = 6.283185307179586;
 
-__device__ inline double reduce_2pi(double a) {
-  const double n = rint(a * kInv2Pi);
-  double r = fma(-n, kP1, a);
-  r = fma(-n, kP2, r);
-  return fma(-n, kP3, r);
-}
-
-// V=1: reduced angle A carried step to step (A' = wrap1(A + w) + t), e by compare-select;
-//      A re-anchored from the exact arg every PG steps.  Chain: sub, select, select, fma, fma, add.
-// V=2: as V=1 with e by rint (one constant) instead of compare-select.
+// Fast-step forms over the prep kernel's constants c_k (turns), one lane per stream:
+// V=0: the product's step: t = c_k - phase/2pi; f = fract(t); phase' = fma(kC, f, phase + V)
+//      (3 dependent f64 ops, 6 in all);
+// V=3: the error t tracked directly: t' = (c_{k+1} - c_k) + t - V/2pi - (kC/2pi) f
+//      (2 dependent ops: fract, fma; 9 in all).
+// V=4: the integrator's constant drift -kB per step absorbed into the constants: W = V + i kB,
+//      Q = phase + kB i(i-1)/2 (i = step within the group), c'_i = c_i + kB i(i-1)/(4 pi):
+//      t = c'_i - Q/2pi; f = fract(t); Q' = fma(kC, f, Q + W); W' = fma(kA, f, W)
+//      (3 dependent, 5 in all; the phase is Q - kB i(i-1)/2, rebuilt off the loop).
 template <int V>
-__global__ __launch_bounds__(64) void pll_v(const float* in, int64_t n, int64_t in_stride, int nstreams, PllCfg cfg,
-                                            double* state, double* theta, int64_t th_stride) {
-#pragma clang fp contract(off)
+__global__ __launch_bounds__(64) void pll_v(const double* cbuf, int64_t cst, int64_t n, int nstreams, PllCfg cfg,
+                                            const double* state, double* theta, int64_t th_stride) {
   const int s = blockIdx.x * 64 + threadIdx.x;
   if (s >= nstreams) return;
-  constexpr int PG = 32;
-  const float* x = in + (int64_t)s * in_stride;
+  const double* c = cbuf + (int64_t)s * cst;
   double* th = theta + (int64_t)s * th_stride;
-  double* st = state + (int64_t)s * 6;
-  double integ = st[0], phase = st[1], fI = st[2], fQ = st[3];
-  const double off = st[5];
-  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
-  double arg = 0.0;
-  {  // literal first step
-    const double xv = (double)x[0];
-    const double e = atan2(xv * (-fQ), xv * fI);
-    integ = integ + cfg.ki * e;
-    phase = phase + cfg.kp * e + integ;
-    arg = w * ((off + 0.0) + 1.0) + phase;
-    th[0] = arg;
-  }
-  double base = off + 1.0;
-  const double wr = reduce_2pi(w);
-  for (int64_t k0 = 1; k0 < n; k0 += PG) {
-    double A = reduce_2pi(arg);           // re-anchor on the exact formula
-    const int cnt = (int)min<int64_t>(PG, n - k0);
-#pragma unroll 4
-    for (int i = 0; i < cnt; ++i) {
-      const float xf = x[k0 + i];
-      const double sel = xf > 0.f ? 0.0 : kPi;
-      double Aw = A + wr;
-      Aw = Aw > kPi ? Aw - k2Pi : Aw;      // off the chain
-      const double u = sel - A;
-      double e;
-      if (V == 1) {
-        e = u > kPi ? u - k2Pi : (u <= -kPi ? u + k2Pi : u);
+  double integ = state[6 * s], phase = state[6 * s + 1];
+  const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
+  const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
+  const double kCt = kC * kInv2Pi;
+  double Vv = integ - kD;
+  constexpr int PG = 32;
+  double t = 0.0;
+  for (int64_t k0 = 0; k0 + PG <= n; k0 += PG) {
+    double cur[PG + 1];
+#pragma unroll
+    for (int i = 0; i <= PG; ++i) cur[i] = (k0 + i < n) ? c[k0 + i] : 0.0;
+    double ph[PG];
+    if (V == 3) t = fma(-kInv2Pi, phase, cur[0]);
+#pragma unroll
+    for (int i = 0; i < PG; ++i) {
+      if (V == 0) {
+        const double tt = fma(-kInv2Pi, phase, cur[i]);
+        const double f = __builtin_amdgcn_fract(tt);
+        const double S = phase + Vv;
+        Vv = fma(kA, f, Vv - kB);
+        phase = fma(kC, f, S);
       } else {
-        e = fma(-rint(u * kInv2Pi), k2Pi, u);
-        e = e <= -kPi ? e + k2Pi : e;
+        if (V == 3) {
+          const double f = __builtin_amdgcn_fract(t);
+          const double S = phase + Vv;
+          const double R = t + fma(-kInv2Pi, Vv, cur[i + 1] - cur[i]);
+          Vv = fma(kA, f, Vv - kB);
+          phase = fma(kC, f, S);
+          t = fma(-kCt, f, R);
+        } else {                     // V == 4: phase holds Q, Vv holds W (reset per group)
+          const double tt = fma(-kInv2Pi, phase, cur[i]);
+          const double f = __builtin_amdgcn_fract(tt);
+          const double S = phase + Vv;
+          Vv = fma(kA, f, Vv);
+          phase = fma(kC, f, S);
+        }
       }
-      integ = fma(cfg.ki, e, integ);
-      const double t = fma(cfg.kp, e, integ);
-      A = Aw + t;
-      phase = phase + t;                    // off the chain: the exact accumulator for th
-      base = base + 1.0;
-      arg = w * base + phase;
-      th[k0 + i] = arg;
+      ph[i] = phase;
+    }
+#pragma unroll
+    for (int i = 0; i < PG; i += 2) *reinterpret_cast<double2*>(th + k0 + i) = make_double2(ph[i], ph[i + 1]);
+    if (V == 4) {                    // back to (phase, V) at the group end
+      phase -= kB * (PG * (PG - 1) / 2);
+      Vv -= kB * PG;
     }
   }
-  st[0] = integ;
-  st[1] = phase;
+}
+// c'_k = c_k + kB i(i-1)/(4 pi), i = k % 32 (V=4's constants)
+__global__ void cprime(const double* c, double* c2, int64_t n, int64_t cst, int S, double kB) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int s = blockIdx.y;
+  if (k < n) {
+    const double i = (double)(k % 32);
+    c2[s * cst + k] = c[s * cst + k] + kB * (i * (i - 1.0) * 0.5) * kInv2Pi;
+  }
+}
+// the phase rebuilt from Q (V=4's stores: th[k] holds Q after step i = k % 32, i.e. Q_{i+1}),
+// as the NCO kernel would
+__global__ void qfix(double* th, int64_t n, int64_t ths, double kB) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n) {
+    const double i = (double)(k % 32) + 1.0;
+    th[blockIdx.y * ths + k] -= kB * (i * (i - 1.0) * 0.5);
+  }
 }
 }  // namespace
 
 int main() {
-  const int S = 8;
-  const int64_t n = 15360;
-  std::vector<float> h(S * n);
-  for (int s = 0; s < S; ++s)
-    for (int64_t k = 0; k < n; ++k)
-      h[s * n + k] = (float)(0.1 * cos(2 * M_PI * 114e3 / 240e3 * k + 0.3 * s) + 0.01 * sin(0.001 * k * (s + 1)));
-  float* din;
-  double *dst, *dth, *dth2;
-  float *nco_i, *nco_q;
-  double* cb;
-  CK(hipMalloc(&din, sizeof(float) * S * n));
-  CK(hipMalloc(&dst, sizeof(double) * 6 * S));
-  CK(hipMalloc(&dth, sizeof(double) * S * (n + 2)));
-  CK(hipMalloc(&dth2, sizeof(double) * S * (n + 2)));
-  CK(hipMalloc(&nco_i, sizeof(float) * S * (n + 1)));
-  CK(hipMalloc(&nco_q, sizeof(float) * S * (n + 1)));
-  const int64_t cst = n + n / 32 + 2;
-  CK(hipMalloc(&cb, sizeof(double) * S * cst));
-  CK(hipMemcpy(din, h.data(), sizeof(float) * S * n, hipMemcpyHostToDevice));
-  const double bw = 0.001;
-  PllCfg cfg{114e3, 240e3, 0.5, M_PI / 3.3 - M_PI / 1.5, bw * 2.666, bw * bw * 3.555};
-  std::vector<double> st0(6 * S);
-  for (int s = 0; s < S; ++s) { double v[6] = {0, 0, 1, 0, 1, 0}; for (int j = 0; j < 6; ++j) st0[6 * s + j] = v[j]; }
-  hipEvent_t e0, e1;
-  CK(hipEventCreate(&e0));
-  CK(hipEventCreate(&e1));
-  auto reset = [&] { CK(hipMemcpy(dst, st0.data(), sizeof(double) * 6 * S, hipMemcpyHostToDevice)); };
-  const int reps = 20;
-  // product
-  PllJobs P{};
-  P.njobs = 1; P.nstreams = S; P.n = n;
-  P.j[0] = PllJob{din, n, dst, dth, n + 2, nco_i, nco_q, n + 1, cfg, cb, cst};
-  float ms = 0;
-  for (int r = 0; r < 3; ++r) { reset(); CK(sdr_launch_pll_jobs(P, 0)); }
-  CK(hipDeviceSynchronize());
-  float best = 1e9;
-  for (int r = 0; r < reps; ++r) {
-    reset();
-    CK(hipEventRecord(e0, 0));
-    CK(sdr_launch_pll_jobs(P, 0));
-    CK(hipEventRecord(e1, 0));
-    CK(hipEventSynchronize(e1));
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    best = std::min(best, ms);
-  }
-  printf("product  : %8.1f us  %6.1f ns/step (incl. nco kernel)\n", best * 1e3, best * 1e6 / n);
-  // the product's theta rows now hold the phase estimates: rebuild th_k = w (k + 1) + phase_k
-  std::vector<double> t_ref(S * (n + 2)), t_v(S * (n + 2));
-  CK(hipMemcpy(t_ref.data(), dth, sizeof(double) * S * (n + 2), hipMemcpyDeviceToHost));
-  for (int s = 0; s < S; ++s)
-    for (int64_t k = 0; k < n; ++k)
-      t_ref[s * (n + 2) + k] = 2.0 * M_PI * (cfg.freq / cfg.fs) * ((0.0 + (double)k) + 1.0) + t_ref[s * (n + 2) + k];
-  auto run_v = [&](auto kern, const char* name) {
-    float b = 1e9;
-    for (int r = 0; r < reps + 3; ++r) {
+  for (const int S : {1, 8}) {
+    const int64_t n = 15360;
+    std::vector<float> h(S * n);
+    for (int s = 0; s < S; ++s)
+      for (int64_t k = 0; k < n; ++k)
+        h[s * n + k] = (float)(0.1 * cos(2 * M_PI * 114e3 / 240e3 * k + 0.3 * s) + 0.01 * sin(0.001 * k * (s + 1)));
+    float* din;
+    double *dst, *dth, *dth2;
+    float *nco_i, *nco_q;
+    double* cb;
+    CK(hipMalloc(&din, sizeof(float) * S * n));
+    CK(hipMalloc(&dst, sizeof(double) * 6 * S));
+    CK(hipMalloc(&dth, sizeof(double) * S * (n + 2)));
+    CK(hipMalloc(&dth2, sizeof(double) * S * (n + 2)));
+    CK(hipMalloc(&nco_i, sizeof(float) * S * (n + 1)));
+    CK(hipMalloc(&nco_q, sizeof(float) * S * (n + 1)));
+    const int64_t cst = n + n / 32 + 2;
+    CK(hipMalloc(&cb, sizeof(double) * S * cst));
+    CK(hipMemcpy(din, h.data(), sizeof(float) * S * n, hipMemcpyHostToDevice));
+    const double bw = 0.001;
+    PllCfg cfg{114e3, 240e3, 0.5, M_PI / 3.3 - M_PI / 1.5, bw * 2.666, bw * bw * 3.555};
+    std::vector<double> st0(6 * S);
+    for (int s = 0; s < S; ++s) { double v[6] = {0, 0, 1, 0, 1, 0}; for (int j = 0; j < 6; ++j) st0[6 * s + j] = v[j]; }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto reset = [&] { CK(hipMemcpy(dst, st0.data(), sizeof(double) * 6 * S, hipMemcpyHostToDevice)); };
+    const int reps = 20;
+    PllJobs P{};
+    P.njobs = 1; P.nstreams = S; P.n = n;
+    P.j[0] = PllJob{din, n, dst, dth, n + 2, nco_i, nco_q, n + 1, cfg, cb, cst};
+    float ms = 0, best = 1e9f;
+    for (int r = 0; r < 3; ++r) { reset(); CK(sdr_launch_pll_jobs(P, 0)); }
+    CK(hipDeviceSynchronize());
+    for (int r = 0; r < reps; ++r) {
       reset();
       CK(hipEventRecord(e0, 0));
-      hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, 0, din, n, n, S, cfg, dst, dth2, n + 2);
+      CK(sdr_launch_pll_jobs(P, 0));
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       CK(hipEventElapsedTime(&ms, e0, e1));
-      if (r >= 3) b = std::min(b, ms);
+      best = std::min(best, ms);
     }
-    CK(hipMemcpy(t_v.data(), dth2, sizeof(double) * S * (n + 2), hipMemcpyDeviceToHost));
-    double dmax = 0, cmax = 0;
-    for (int s = 0; s < S; ++s)
-      for (int64_t k = 0; k < n; ++k) {
-        const double a = t_ref[s * (n + 2) + k], c = t_v[s * (n + 2) + k];
-        dmax = std::max(dmax, fabs(a - c));
-        cmax = std::max(cmax, fabs(cos(a * 0.5 + cfg.adj) - cos(c * 0.5 + cfg.adj)));
+    printf("S=%d product  : %8.1f us  %6.1f ns/step (prep + loop + nco kernels)\n", S, best * 1e3, best * 1e6 / n);
+    std::vector<double> t_ref(S * (n + 2)), t_v(S * (n + 2));
+    CK(hipMemcpy(t_ref.data(), dth, sizeof(double) * S * (n + 2), hipMemcpyDeviceToHost));
+    auto run_v = [&](auto kern, const char* name) {
+      float b = 1e9f;
+      for (int r = 0; r < reps + 3; ++r) {
+        reset();
+        CK(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, 0, cb, cst, n, S, cfg, dst, dth2, n + 2);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 3) b = std::min(b, ms);
       }
-    printf("%-9s: %8.1f us  %6.1f ns/step  max|dtheta| %.2e  max|dnco| %.2e\n", name, b * 1e3, b * 1e6 / n, dmax, cmax);
-  };
-  run_v(pll_v<1>, "v1 select");
-  run_v(pll_v<2>, "v2 rint");
+      CK(hipMemcpy(t_v.data(), dth2, sizeof(double) * S * (n + 2), hipMemcpyDeviceToHost));
+      double dmax = 0;
+      for (int s = 0; s < S; ++s)
+        for (int64_t k = 32; k < n; ++k) dmax = std::max(dmax, fabs(t_ref[s * (n + 2) + k] - t_v[s * (n + 2) + k]));
+      printf("S=%d %-9s: %8.1f us  %6.1f ns/step  max|dphase| vs product %.2e\n", S, name, b * 1e3, b * 1e6 / n, dmax);
+    };
+    run_v(pll_v<0>, "v0 3-dep");
+    run_v(pll_v<3>, "v3 2-dep");
+    {
+      double* c2;
+      CK(hipMalloc(&c2, sizeof(double) * S * cst));
+      const double kB = kPi * cfg.ki;
+      hipLaunchKernelGGL(cprime, dim3((unsigned)((n + 255) / 256), S), dim3(256), 0, 0, cb, c2, n, cst, S, kB);
+      CK(hipDeviceSynchronize());
+      std::swap(cb, c2);
+      auto fix = [&] {
+        hipLaunchKernelGGL(qfix, dim3((unsigned)((n + 255) / 256), S), dim3(256), 0, 0, dth2, n, n + 2, kB);
+        CK(hipDeviceSynchronize());
+      };
+      run_v(pll_v<4>, "v4 5-op");
+      fix();
+      std::vector<double> t4(S * (n + 2));
+      CK(hipMemcpy(t4.data(), dth2, sizeof(double) * S * (n + 2), hipMemcpyDeviceToHost));
+      double dmax = 0;
+      for (int s = 0; s < S; ++s)
+        for (int64_t k = 32; k < n; ++k) dmax = std::max(dmax, fabs(t_ref[s * (n + 2) + k] - t4[s * (n + 2) + k]));
+      printf("S=%d v4 phase rebuilt: max|dphase| vs product %.2e\n", S, dmax);
+      std::swap(cb, c2);
+      CK(hipFree(c2));
+    }
+    CK(hipFree(din)); CK(hipFree(dst)); CK(hipFree(dth)); CK(hipFree(dth2));
+    CK(hipFree(nco_i)); CK(hipFree(nco_q)); CK(hipFree(cb));
+  }
   return 0;
 }
