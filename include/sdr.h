@@ -249,8 +249,10 @@ int sdr_rx_submit(sdr_rx* rx, const void* iq, int64_t iq_stride, int nout, const
                   float* const* out, const int64_t* out_stride);
 int sdr_rx_flush(sdr_rx* rx);
 /* Pipelined receiver (set before the first block): block k's front half (FE and the
- * filters of the demod) runs on a second stream while block k-1's back half (PLLs, stereo
- * and RDS stages) runs on the context stream; the output rows alternate between two sets
+ * filters of the demod) runs on a second stream, its PLLs on a third once block k-1's PLLs
+ * are done, and its stereo / RDS stages on the context stream -- so block k's PLLs start
+ * while block k-1's stages C-E and block k+1's front half run; the output rows alternate
+ * between two sets
  * (sdr_rx_output gives the latest block's; block k's stay valid until block k+2 is
  * processed).  sdr_rx_process_dev then does NOT order the front half after earlier work on
  * the context stream: its IQ must be ready when it is called (device-resident data, or an

@@ -484,8 +484,9 @@ struct sdr_rx {
   // sdr_rx_set_pipeline: block k's front half (FE, stage A) runs on `front` while block
   // k-1's back half (B, PLLs, C, D, E) runs on the context stream; row set k % 2
   int pipe = 0;
-  hipStream_t front = nullptr;
-  hipEvent_t ev_front[2] = {}, ev_back[2] = {}, ev_done[2] = {};
+  hipStream_t front = nullptr;          // FE, stages A and B
+  hipStream_t mid = nullptr;            // the PLLs (prep, lanes, NCO)
+  hipEvent_t ev_front[2] = {}, ev_mid[2] = {}, ev_back[2] = {}, ev_done[2] = {};
   // sdr_rx_submit: pinned slots (input and outputs per block parity) and the block in flight
   size_t in_slot = 0, out_slot = 0;
   int64_t subs = 0;
@@ -647,6 +648,7 @@ void sdr_rx_destroy(sdr_rx* r) {
   if (r->c) {
     (void)hipSetDevice(r->c->device);
     if (r->front) (void)hipStreamSynchronize(r->front);
+    if (r->mid) (void)hipStreamSynchronize(r->mid);
     (void)hipStreamSynchronize(r->c->stream);
   }
   if (r->mem) (void)hipFree(r->mem);
@@ -655,9 +657,10 @@ void sdr_rx_destroy(sdr_rx* r) {
   for (hipEvent_t e : r->ev)
     if (e) (void)hipEventDestroy(e);
   for (int q = 0; q < 2; ++q)
-    for (hipEvent_t e : {r->ev_front[q], r->ev_back[q], r->ev_done[q]})
+    for (hipEvent_t e : {r->ev_front[q], r->ev_mid[q], r->ev_back[q], r->ev_done[q]})
       if (e) (void)hipEventDestroy(e);
   if (r->front) (void)hipStreamDestroy(r->front);
+  if (r->mid) (void)hipStreamDestroy(r->mid);
   delete r;
 }
 
@@ -697,6 +700,7 @@ int sdr_rx_reset(sdr_rx* r) {
   TRY(set_dev(r->c));
   hipStream_t st = r->c->stream;
   if (r->front) HIP_TRY(hipStreamSynchronize(r->front));
+  if (r->mid) HIP_TRY(hipStreamSynchronize(r->mid));
   r->pend.on = false;                            // a submitted block's outputs are dropped
   // state banks, phases and wrap counters (contiguous)
   HIP_TRY(hipMemsetAsync(r->bank[0], 0, sizeof(double) * (size_t)(2 * r->bank_len + 2 * round_up(r->S, 2)), st));
@@ -720,8 +724,10 @@ int sdr_rx_set_pipeline(sdr_rx* r, int on) {
   if (on && !r->front) {
     TRY(set_dev(r->c));
     HIP_TRY(hipStreamCreateWithFlags(&r->front, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&r->mid, hipStreamNonBlocking));
     for (int q = 0; q < 2; ++q) {
       HIP_TRY(hipEventCreateWithFlags(&r->ev_front[q], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&r->ev_mid[q], hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&r->ev_back[q], hipEventDisableTiming));
     }
   }
@@ -814,16 +820,26 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   if (rd) A.push_back(fir(SDR_RX_F_RDS_EXTRACT, Z_EXTRACT, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_RDS_EXTRACT], ms, 1));
   HIP_TRY(launch_stage(A, S, fs, &fst));
   HIP_TRY(mark(1 + SDR_RX_ST_A, fs));
-  if (r->pipe) {
-    HIP_TRY(hipEventRecord(r->ev_front[q], fs));
-    HIP_TRY(hipStreamWaitEvent(st, r->ev_front[q], 0));
-  }
   // stage B: RDS squaring non-linearity + BPF (model/fmRDSblock.py:161-164)
   if (rd) HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_SQUARE, Z_SQUARE, o[SDR_RX_O_RDS_EXTRACT], M, ms,
-                                    o[SDR_RX_O_RDS_PRE_PLL], ms, 1, PRE_SQUARE)}, S, st));
-  HIP_TRY(mark(1 + SDR_RX_ST_B, st));
+                                    o[SDR_RX_O_RDS_PRE_PLL], ms, 1, PRE_SQUARE)}, S, fs));
+  HIP_TRY(mark(1 + SDR_RX_ST_B, fs));
+  // Pipelined: the PLLs of block k run on their own stream once block k's front half and
+  // block k-1's PLLs are done, beside block k-1's stages C-E (which wait for them) and block
+  // k+1's front half; row set q is free once block k-2's back half has read it.
+  const bool plls = stx || rd;
+  hipStream_t ps = r->pipe ? r->mid : st;
+  if (r->pipe) {
+    HIP_TRY(hipEventRecord(r->ev_front[q], fs));
+    if (plls) {
+      HIP_TRY(hipStreamWaitEvent(ps, r->ev_front[q], 0));
+      if (r->blocks >= 2) HIP_TRY(hipStreamWaitEvent(ps, r->ev_back[q], 0));
+    } else {
+      HIP_TRY(hipStreamWaitEvent(st, r->ev_front[q], 0));
+    }
+  }
   // PLLs (model/fmMonoBlock.py:119, model/fmRDSblock.py:167): one lane per recurrence
-  if (stx || rd) {
+  if (plls) {
     PllJobs P{};
     P.nstreams = S;
     P.n = M;
@@ -834,9 +850,13 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       P.j[P.njobs++] = PllJob{o[SDR_RX_O_RDS_PRE_PLL], ms, r->pll_state[1], r->theta + (int64_t)S * r->ths, r->ths,
                               o[SDR_RX_O_RDS_NCO_I], o[SDR_RX_O_RDS_NCO_Q], ms, r->pll[1],
                               r->pllc + (int64_t)S * r->cst, r->cst};
-    HIP_TRY(sdr_launch_pll_jobs(P, st));
+    HIP_TRY(sdr_launch_pll_jobs(P, ps));
   }
-  HIP_TRY(mark(1 + SDR_RX_ST_PLL, st));
+  HIP_TRY(mark(1 + SDR_RX_ST_PLL, ps));
+  if (r->pipe && plls) {
+    HIP_TRY(hipEventRecord(r->ev_mid[q], ps));
+    HIP_TRY(hipStreamWaitEvent(st, r->ev_mid[q], 0));
+  }
   // stage C: mixers + LPFs; the stereo LPF's store also forms L and R
   std::vector<StageJob> C;
   if (stx) {
