@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
   const int q = g / P.nstreams;
   const int s = g - q * P.nstreams;
   const PllJob& J = P.j[q];
-  const double off = J.state[(int64_t)s * 6 + 5];
+  const double off = J.off_given ? J.off : J.state[(int64_t)s * 6 + 5];
   const double w = 2.0 * kPi * (J.cfg.freq / J.cfg.fs);
   double* c = J.cbuf + (int64_t)s * J.c_stride;
   bool odd = false;
@@ -231,23 +231,54 @@ __global__ void nco_jobs_kernel(PllJobs P) {
 
 }  // namespace
 
-hipError_t sdr_launch_pll_jobs(const PllJobs& P, hipStream_t st) {
+namespace {
+// the job table's strides and whether every row allows 16-B loads / stores
+hipError_t pll_check(const PllJobs& P, bool* vec) {
   if (P.njobs < 1 || P.njobs > SDR_PLL_MAXJ || P.nstreams <= 0 || P.n < 0) return hipErrorInvalidValue;
-  // 16-B loads / stores need every lane's constants row and phase row 16-B aligned
-  bool vec = true;
+  *vec = true;
   for (int q = 0; q < P.njobs; ++q) {
     const PllJob& J = P.j[q];
     if (J.th_stride < P.n + 1 || J.c_stride < P.n + P.n / PG) return hipErrorInvalidValue;
-    vec = vec && ((uintptr_t)J.cbuf % 16) == 0 && (J.c_stride % 2) == 0 && ((uintptr_t)J.theta % 16) == 0 &&
-          (J.th_stride % 2) == 0;
+    *vec = *vec && ((uintptr_t)J.cbuf % 16) == 0 && (J.c_stride % 2) == 0 && ((uintptr_t)J.theta % 16) == 0 &&
+           (J.th_stride % 2) == 0;
   }
-  const int lanes = P.njobs * P.nstreams;
+  return hipSuccess;
+}
+}  // namespace
+
+hipError_t sdr_launch_pll_prep(const PllJobs& P, hipStream_t st) {
+  bool vec;
+  const hipError_t e = pll_check(P, &vec);
+  if (e != hipSuccess) return e;
   if (P.n > 0)
-    hipLaunchKernelGGL(pll_prep_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)lanes), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(pll_prep_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
+                       dim3(256), 0, st, P);
+  return hipGetLastError();
+}
+
+hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
+  bool vec;
+  const hipError_t e = pll_check(P, &vec);
+  if (e != hipSuccess) return e;
   const dim3 grid((unsigned)(P.njobs * ((P.nstreams + 63) / 64)));
   if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, P);
   else hipLaunchKernelGGL(pll_lanes_kernel<false>, grid, dim3(64), 0, st, P);
-  if (P.n > 0)
-    hipLaunchKernelGGL(nco_jobs_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)lanes), dim3(256), 0, st, P);
   return hipGetLastError();
+}
+
+hipError_t sdr_launch_pll_nco(const PllJobs& P, hipStream_t st) {
+  bool vec;
+  const hipError_t e = pll_check(P, &vec);
+  if (e != hipSuccess) return e;
+  if (P.n > 0)
+    hipLaunchKernelGGL(nco_jobs_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
+                       dim3(256), 0, st, P);
+  return hipGetLastError();
+}
+
+hipError_t sdr_launch_pll_jobs(const PllJobs& P, hipStream_t st) {
+  hipError_t e = sdr_launch_pll_prep(P, st);
+  if (e == hipSuccess) e = sdr_launch_pll_loop(P, st);
+  if (e == hipSuccess) e = sdr_launch_pll_nco(P, st);
+  return e;
 }

@@ -469,9 +469,9 @@ struct sdr_rx {
   int* wraps = nullptr;                // FE kernel scratch: per-block wrap count, last phase
   float* last_phi = nullptr;
   double* pll_state[2] = {};           // 6 per stream (stereo, RDS)
-  double* theta = nullptr;             // PLL phases: 2 x S rows of ths
+  double* theta = nullptr;             // PLL phases: 2 x S rows of ths per row set
   int64_t ths = 0;
-  double* pllc = nullptr;              // PLL per-sample constants: 2 x S rows of cst
+  double* pllc = nullptr;              // PLL per-sample constants: 2 x S rows of cst per row set
   int64_t cst = 0;
   void* pin_in = nullptr;              // pinned host staging (sdr_rx_run)
   size_t pin_in_cap = 0;
@@ -594,7 +594,8 @@ int rx_finalize(sdr_rx* r) {
   r->ths = round_up(M, 2) + 2;
   r->cst = round_up(M + M / 32, 2) + 2;
   const int64_t S2 = round_up(S, 2);                 // keeps the phase rows 16-B aligned
-  const int64_t doubles = 2 * zl + 3 * S2 + 2 * 6 * S2 + 2 * S * r->ths + 2 * S * r->cst;
+  const int nsets = r->pipe ? 2 : 1;
+  const int64_t doubles = 2 * zl + 3 * S2 + 2 * 6 * S2 + nsets * (2 * S * r->ths + 2 * S * r->cst);
   const size_t bytes = (size_t)floats * 4 + 64 + (size_t)doubles * 8;
   TRY(set_dev(r->c));
   hipError_t e = hipMalloc(&r->mem, bytes);
@@ -613,7 +614,7 @@ int rx_finalize(sdr_rx* r) {
   r->pll_state[0] = r->phase + 3 * S2;
   r->pll_state[1] = r->pll_state[0] + 6 * S2;
   r->theta = r->pll_state[1] + 6 * S2;
-  r->pllc = r->theta + 2 * S * r->ths;
+  r->pllc = r->theta + nsets * 2 * S * r->ths;
   r->ready = true;
   return sdr_rx_reset(r);
 }
@@ -824,11 +825,33 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   if (rd) HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_SQUARE, Z_SQUARE, o[SDR_RX_O_RDS_EXTRACT], M, ms,
                                     o[SDR_RX_O_RDS_PRE_PLL], ms, 1, PRE_SQUARE)}, S, fs));
   HIP_TRY(mark(1 + SDR_RX_ST_B, fs));
-  // Pipelined: the PLLs of block k run on their own stream once block k's front half and
-  // block k-1's PLLs are done, beside block k-1's stages C-E (which wait for them) and block
-  // k+1's front half; row set q is free once block k-2's back half has read it.
+  // PLLs (model/fmMonoBlock.py:119, model/fmRDSblock.py:167): one lane per recurrence.
+  // Pipelined, the three launches go to three streams: the per-sample constants with the
+  // front half (trigOffset = M x blocks since reset, known here), the recurrence alone on
+  // its own stream -- block k's starts as soon as block k-1's is done, beside block k-1's
+  // NCO and stages C-E and block k+1's front half -- and the NCO with the back half.  Phase
+  // and constant rows alternate with the row set; set q is free once block k-2's back half
+  // (which waited for its recurrence) is done.
   const bool plls = stx || rd;
   hipStream_t ps = r->pipe ? r->mid : st;
+  PllJobs P{};
+  if (plls) {
+    P.nstreams = S;
+    P.n = M;
+    double* th = r->theta + (int64_t)q * 2 * S * r->ths;
+    double* pc = r->pllc + (int64_t)q * 2 * S * r->cst;
+    const double off = (double)M * (double)r->blocks;
+    if (stx) {
+      P.j[P.njobs++] = PllJob{o[SDR_RX_O_BPF_RECOVERY], ms, r->pll_state[0], th, r->ths,
+                              o[SDR_RX_O_STEREO_NCO], nullptr, ms, r->pll[0], pc, r->cst, off, 1};
+    }
+    if (rd) {
+      P.j[P.njobs++] = PllJob{o[SDR_RX_O_RDS_PRE_PLL], ms, r->pll_state[1], th + (int64_t)S * r->ths, r->ths,
+                              o[SDR_RX_O_RDS_NCO_I], o[SDR_RX_O_RDS_NCO_Q], ms, r->pll[1],
+                              pc + (int64_t)S * r->cst, r->cst, off, 1};
+    }
+    HIP_TRY(sdr_launch_pll_prep(P, fs));
+  }
   if (r->pipe) {
     HIP_TRY(hipEventRecord(r->ev_front[q], fs));
     if (plls) {
@@ -838,25 +861,13 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       HIP_TRY(hipStreamWaitEvent(st, r->ev_front[q], 0));
     }
   }
-  // PLLs (model/fmMonoBlock.py:119, model/fmRDSblock.py:167): one lane per recurrence
-  if (plls) {
-    PllJobs P{};
-    P.nstreams = S;
-    P.n = M;
-    if (stx)
-      P.j[P.njobs++] = PllJob{o[SDR_RX_O_BPF_RECOVERY], ms, r->pll_state[0], r->theta, r->ths,
-                              o[SDR_RX_O_STEREO_NCO], nullptr, ms, r->pll[0], r->pllc, r->cst};
-    if (rd)
-      P.j[P.njobs++] = PllJob{o[SDR_RX_O_RDS_PRE_PLL], ms, r->pll_state[1], r->theta + (int64_t)S * r->ths, r->ths,
-                              o[SDR_RX_O_RDS_NCO_I], o[SDR_RX_O_RDS_NCO_Q], ms, r->pll[1],
-                              r->pllc + (int64_t)S * r->cst, r->cst};
-    HIP_TRY(sdr_launch_pll_jobs(P, ps));
-  }
+  if (plls) HIP_TRY(sdr_launch_pll_loop(P, ps));
   HIP_TRY(mark(1 + SDR_RX_ST_PLL, ps));
   if (r->pipe && plls) {
     HIP_TRY(hipEventRecord(r->ev_mid[q], ps));
     HIP_TRY(hipStreamWaitEvent(st, r->ev_mid[q], 0));
   }
+  if (plls) HIP_TRY(sdr_launch_pll_nco(P, st));
   // stage C: mixers + LPFs; the stereo LPF's store also forms L and R
   std::vector<StageJob> C;
   if (stx) {

@@ -62,6 +62,12 @@ hipError_t sdr_launch_dft(const double* x, int64_t n, double* X, hipStream_t st)
 struct PllJob {
   const float* in; int64_t in_stride; double* state; double* theta; int64_t th_stride;
   float* nco_i; float* nco_q; int64_t out_stride; PllCfg cfg; double* cbuf; int64_t c_stride;
+  double off; int off_given;   // the prep kernel's trigOffset, when not read from state[5]
 };
 struct PllJobs { PllJob j[SDR_PLL_MAXJ]; int njobs; int nstreams; int64_t n; };
+// prep (per-sample constants) -> loop (one lane per recurrence) -> NCO; the three launches
+// separately (the receiver puts them on different streams) or together
+hipError_t sdr_launch_pll_prep(const PllJobs& jobs, hipStream_t st);
+hipError_t sdr_launch_pll_loop(const PllJobs& jobs, hipStream_t st);
+hipError_t sdr_launch_pll_nco(const PllJobs& jobs, hipStream_t st);
 hipError_t sdr_launch_pll_jobs(const PllJobs& jobs, hipStream_t st);
