@@ -52,16 +52,23 @@ __device__ inline double reduce_2pi(double a) {
 // Steps per group: the next group's inputs are loaded (registers) while this one runs,
 // and the group's phases leave as 16-B stores.
 constexpr int PG = 32;
+// Recurrences per wave (P.lpw, chosen by the launcher): a wave's f64 step slows with its
+// active lanes (one stream 30 ns, 8 streams 34 ns, 64 streams 54 ns per step), so the
+// recurrences are spread over up to 32 waves that run side by side on different SIMDs --
+// 1 stream per wave up to 16 per job, 4 per wave at 64 (measured C5 blocks: 8 streams
+// 543 -> 521 us, 64 streams 833 -> 576 us; 128 one-lane waves were slower again, 692 us).
+constexpr int kMaxPllWaves = 32;
 
 template <bool VEC>
 __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
 #pragma clang fp contract(off)  // Python evaluates a*b + c with two roundings
   // one job per wave (a lane-varying job index into the kernarg table would copy the whole
   // table to scratch); lane = stream
-  const int wpj = (P.nstreams + 63) / 64;
+  const int lpw = P.lpw;
+  const int wpj = (P.nstreams + lpw - 1) / lpw;
   const int q = blockIdx.x / wpj;
-  const int s = (blockIdx.x - q * wpj) * 64 + threadIdx.x;
-  if (s >= P.nstreams) return;  // votes below run over the active lanes only
+  const int s = (blockIdx.x - q * wpj) * lpw + threadIdx.x;
+  if ((int)threadIdx.x >= lpw || s >= P.nstreams) return;  // votes below run over the active lanes only
   const PllJob& J = P.j[q];
   struct {
     const float* in; double* th; const double* c; float* nco_i; float* nco_q;
@@ -260,9 +267,12 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
   bool vec;
   const hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
-  const dim3 grid((unsigned)(P.njobs * ((P.nstreams + 63) / 64)));
-  if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, P);
-  else hipLaunchKernelGGL(pll_lanes_kernel<false>, grid, dim3(64), 0, st, P);
+  PllJobs L = P;
+  L.lpw = 1;
+  while (L.lpw < 64 && L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw) > kMaxPllWaves) L.lpw *= 2;
+  const dim3 grid((unsigned)(L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw)));
+  if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, L);
+  else hipLaunchKernelGGL(pll_lanes_kernel<false>, grid, dim3(64), 0, st, L);
   return hipGetLastError();
 }
 
