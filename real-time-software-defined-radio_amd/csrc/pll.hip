@@ -188,6 +188,169 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
   }
 }
 
+// One recurrence per workgroup (P.lpw == 1): wave 0's lane 0 runs it, wave 1 feeds it.  A
+// lone recurrence issues its 6 f64 ops in ~26 cycles per step (11 ns, tools/f64_probe.hip);
+// fed by its own per-step 16-B loads it ran at ~30 ns -- vmcnt counts at most 63
+// operations, so with a load and a store every two steps no more than ~2 groups of
+// constants could be in flight against a ~1 us load latency -- and with its constants and
+// phases staged through LDS by the same wave, at 67 cycles per step (a single wave's wide LDS
+// stores run at half rate).  Here wave 1 brings the constants into an LDS ring by 64-lane
+// LDS-DMA (128 steps = 1 KiB per instruction, NPF chunks ahead; it alone issues loads, so its
+// vmcnt waits are exact), the waves meet at one raw s_barrier per chunk (no fence: the DMA
+// stays in flight), and lane 0 reads each group's 32 constants in one LDS burst and stores
+// its phases straight to HBM (stores only: it never waits on vmcnt).  Constants of 0 / NaN
+// inputs are NaN (pll_prep_kernel): a fast group that meets one ends in a NaN phase and is
+// redone in the general form from its checkpoint.
+constexpr int CH = 128;     // steps per chunk (64 lanes x 16 B)
+constexpr int NPF = 4;      // chunks of constants in flight
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+// a group's 32 constants, read from LDS by hand in one burst and waited for once (left to
+// itself the compiler read them 4 at a time, each batch waiting out the LDS latency)
+template <int J = 0>
+__device__ __forceinline__ void lds_group_rd(f4v (&c)[PG / 2], const double* src) {
+  if constexpr (J < PG / 2) {
+    c[J] = lds_read_b128<16 * J>(src);
+    lds_group_rd<J + 1>(c, src);
+  }
+}
+template <int J = 0>
+__device__ __forceinline__ void lds_group_wait(f4v (&c)[PG / 2]) {
+  if constexpr (J < PG / 2) {
+    lds_wait<0>(c[J]);
+    lds_group_wait<J + 1>(c);
+  }
+}
+__device__ __forceinline__ double dbl(const f4v& v, int h) {
+  const d2v d = __builtin_bit_cast(d2v, v);
+  return h ? d.y : d.x;
+}
+
+__global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
+#pragma clang fp contract(off)  // Python evaluates a*b + c with two roundings
+  __shared__ __attribute__((aligned(16))) double cring[NPF][CH];
+  const int q = blockIdx.x / P.nstreams;   // one stream per workgroup
+  const int s = blockIdx.x - q * P.nstreams;
+  const bool loader = threadIdx.x >= 64;
+  const int lane = threadIdx.x & 63;
+  const PllJob& J = P.j[q];
+  const int64_t n = P.n;
+  const int64_t nch = n / CH;
+  const double* cr = J.cbuf + (int64_t)s * J.c_stride;
+  if (loader) {
+    // ---- wave 1: constants -> LDS ring, one barrier per chunk ----
+    const unsigned voff = 16u * lane;
+    int64_t next = 0;                                    // next chunk to fetch
+    for (; next < nch && next < NPF; ++next) glds16x<1>(voff, cr + next * CH, lds_addr_of(&cring[next % NPF][0]));
+    for (int64_t ch = 0; ch < nch; ++ch) {
+      wait_vm_chain<NPF>((int)(next - ch - 1));          // chunk ch has landed
+      __builtin_amdgcn_s_barrier();                      // ready; and lane 0 is done with ch-1
+      if (ch >= 1 && next < nch) {                       // ch-1's slot -> chunk ch-1+NPF
+        glds16x<1>(voff, cr + next * CH, lds_addr_of(&cring[next % NPF][0]));
+        ++next;
+      }
+    }
+    return;
+  }
+  // ---- wave 0: the recurrence on lane 0 (the other lanes only take the barriers) ----
+  const bool rec = lane == 0;
+  const float* in = J.in + (int64_t)s * J.in_stride;
+  double* th = J.theta + (int64_t)s * J.th_stride;
+  float* nco_i = J.nco_i + (int64_t)s * J.out_stride;
+  float* nco_q = J.nco_q ? J.nco_q + (int64_t)s * J.out_stride : nullptr;
+  const PllCfg cfg = J.cfg;
+  double* st = J.state + (int64_t)s * 6;
+  double integ = st[0], phase = st[1], fI = st[2], fQ = st[3];
+  const double off = st[5];
+  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  if (rec) {
+    nco_i[0] = (float)st[4];
+    if (nco_q) nco_q[0] = (float)((off > 0.0) ? sin((w * off + phase) * cfg.scale + cfg.adj) : 0.0);
+  }
+  double arg = 0.0;
+  auto general = [&](float xf, int64_t k, bool literal) {   // as pll_lanes_kernel
+    const double xv = (double)xf;
+    double e;
+    if (literal || !(xv > 0.0 || xv < 0.0)) {
+      if (!literal) { fI = cos(arg); fQ = sin(arg); }
+      e = atan2(xv * (-fQ), xv * fI);
+    } else {
+      e = reduce_2pi(xv > 0.0 ? -arg : kPi - arg);
+      if (e <= -kPi) e += 2.0 * kPi;
+    }
+    integ = integ + cfg.ki * e;
+    phase = phase + cfg.kp * e + integ;
+    arg = w * ((off + (double)k) + 1.0) + phase;
+  };
+  const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
+  const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
+  double V = 0.0;
+  auto fast = [&](double c) {
+    const double t = fma(-kInv2Pi, phase, c);
+    const double f = __builtin_amdgcn_fract(t);
+    const double S = phase + V;
+    V = fma(kA, f, V - kB);
+    phase = fma(kC, f, S);
+  };
+  for (int64_t ch = 0; ch < nch; ++ch) {
+    __builtin_amdgcn_s_barrier();                        // chunk ch is in LDS
+    asm volatile("" ::: "memory");
+    if (rec) {
+      const double* cc = &cring[ch % NPF][0];
+#pragma unroll 1
+      for (int g = 0; g < CH / PG; ++g) {
+        const int64_t k0 = ch * CH + g * PG;
+        bool redo = k0 == 0;                             // the call's literal first sample
+        if (!redo) {
+          const double ph0 = phase, in0 = integ, ar0 = arg;
+          f4v cv[PG / 2];
+          lds_group_rd(cv, cc + g * PG);
+          lds_group_wait(cv);
+          double pv[PG];
+          V = integ - kD;
+#pragma unroll
+          for (int i = 0; i < PG; ++i) {
+            fast(dbl(cv[i / 2], i & 1));
+            pv[i] = phase;
+          }
+          if (phase != phase) {                          // a 0 / NaN input in the group
+            phase = ph0; integ = in0; arg = ar0;
+            redo = true;
+          } else {
+            integ = V + kD;
+            arg = w * ((off + (double)(k0 + PG - 1)) + 1.0) + phase;
+            double* tp = th + k0;
+#pragma unroll
+            for (int i = 0; i < PG; i += 2) *reinterpret_cast<double2*>(tp + i) = make_double2(pv[i], pv[i + 1]);
+          }
+        }
+        if (redo) {
+          for (int i = 0; i < PG; ++i) {
+            general(in[k0 + i], k0 + i, k0 + i == 0);
+            th[k0 + i] = phase;
+          }
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+  }
+  if (rec) {
+    for (int64_t k = nch * CH; k < n; ++k) {      // tail (< CH samples)
+      general(in[k], k, k == 0);
+      th[k] = phase;
+    }
+    th[n] = off;                                  // the NCO kernel's trigOffset
+    if (n > 0) {
+      st[0] = integ;
+      st[1] = phase;
+      st[2] = cos(arg);
+      st[3] = sin(arg);
+      st[4] = cos(arg * cfg.scale + cfg.adj);
+      st[5] = off + (double)n;
+    }
+  }
+}
+
 // Per-sample constants of the loop (parallel): c_k = (sel_k - w (off + k)) / 2pi + 1/2 and one flag per
 // PG-sample group holding a 0 or NaN input; c row layout: c[0..n) | flags[0..n/PG).
 __global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
@@ -205,7 +368,9 @@ __global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
     const float x = J.in[(int64_t)s * J.in_stride + k];
     odd = !(x > 0.f || x < 0.f);
     const double cc = (x > 0.f ? 0.0 : kPi) - w * (off + (double)k);   // the previous step's w (off + k)
-    c[k] = fma(cc, kInv2Pi, 0.5);
+    // a 0 / NaN input gets a NaN constant: a fast group over it ends in a NaN phase, which
+    // pll_chunk_kernel takes as its signal to redo the group in the general form
+    c[k] = odd ? __builtin_nan("") : fma(cc, kInv2Pi, 0.5);
   }
   // groups of PG = 32 lanes: the low and high half of each wave
   const uint64_t m = __ballot(odd);
@@ -271,7 +436,8 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
   L.lpw = 1;
   while (L.lpw < 64 && L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw) > kMaxPllWaves) L.lpw *= 2;
   const dim3 grid((unsigned)(L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw)));
-  if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, L);
+  if (vec && L.lpw == 1) hipLaunchKernelGGL(pll_chunk_kernel, grid, dim3(128), 0, st, L);
+  else if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, L);
   else hipLaunchKernelGGL(pll_lanes_kernel<false>, grid, dim3(64), 0, st, L);
   return hipGetLastError();
 }
