@@ -52,12 +52,12 @@ __device__ inline double reduce_2pi(double a) {
 // Steps per group: the next group's inputs are loaded (registers) while this one runs,
 // and the group's phases leave as 16-B stores.
 constexpr int PG = 32;
-// Recurrences per wave (P.lpw, chosen by the launcher): a wave's f64 step slows with its
-// active lanes (one stream 30 ns, 8 streams 34 ns, 64 streams 54 ns per step), so the
-// recurrences are spread over up to 32 waves that run side by side on different SIMDs --
-// 1 stream per wave up to 16 per job, 4 per wave at 64 (measured C5 blocks: 8 streams
-// 543 -> 521 us, 64 streams 833 -> 576 us; 128 one-lane waves were slower again, 692 us).
-constexpr int kMaxPllWaves = 32;
+// Recurrences per wave (P.lpw, chosen by the launcher): one per workgroup (pll_chunk_kernel,
+// a recurrence wave + a loader wave) up to 128 recurrences -- 64 streams x 2 PLLs; C5 blocks:
+// 8 streams 379 us, 64 streams 454 us -- and beyond that several per wave
+// (pll_lanes_kernel: a wave's f64 step slows with its active lanes, 30 ns for one stream,
+// 54 ns for 64).
+constexpr int kMaxPllWaves = 128;
 
 template <bool VEC>
 __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
@@ -297,15 +297,15 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
     asm volatile("" ::: "memory");
     if (rec) {
       const double* cc = &cring[ch % NPF][0];
-#pragma unroll 1
-      for (int g = 0; g < CH / PG; ++g) {
+      // two register buffers: group g+1's constants are read while group g runs
+      f4v ca[PG / 2], cb[PG / 2];
+      auto group = [&](f4v (&cv)[PG / 2], f4v (&nx)[PG / 2], int g) {
+        lds_group_wait(cv);                              // read a group ago
+        if (g + 1 < CH / PG) lds_group_rd(nx, cc + (g + 1) * PG);
         const int64_t k0 = ch * CH + g * PG;
         bool redo = k0 == 0;                             // the call's literal first sample
         if (!redo) {
           const double ph0 = phase, in0 = integ, ar0 = arg;
-          f4v cv[PG / 2];
-          lds_group_rd(cv, cc + g * PG);
-          lds_group_wait(cv);
           double pv[PG];
           V = integ - kD;
 #pragma unroll
@@ -330,7 +330,13 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
             th[k0 + i] = phase;
           }
         }
-      }
+      };
+      static_assert(CH / PG == 4, "two buffers, four groups per chunk");
+      lds_group_rd(ca, cc);
+      group(ca, cb, 0);
+      group(cb, ca, 1);
+      group(ca, cb, 2);
+      group(cb, ca, 3);
     }
     asm volatile("" ::: "memory");
   }
