@@ -214,12 +214,15 @@ __device__ __forceinline__ void lds_group_rd(f4v (&c)[PG / 2], const double* src
     lds_group_rd<J + 1>(c, src);
   }
 }
-template <int J = 0>
+// ONE wait naming all 16 registers: per-register waits let the compiler sink them into the
+// steps, and the next group's reads (ordered after the waits) then went out at the end of
+// the group instead of its start
 __device__ __forceinline__ void lds_group_wait(f4v (&c)[PG / 2]) {
-  if constexpr (J < PG / 2) {
-    lds_wait<0>(c[J]);
-    lds_group_wait<J + 1>(c);
-  }
+  static_assert(PG / 2 == 16, "16 registers");
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]),
+                 "+v"(c[8]), "+v"(c[9]), "+v"(c[10]), "+v"(c[11]), "+v"(c[12]), "+v"(c[13]), "+v"(c[14]),
+                 "+v"(c[15]));
 }
 __device__ __forceinline__ double dbl(const f4v& v, int h) {
   const d2v d = __builtin_bit_cast(d2v, v);
@@ -302,6 +305,9 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
       auto group = [&](f4v (&cv)[PG / 2], f4v (&nx)[PG / 2], int g) {
         lds_group_wait(cv);                              // read a group ago
         if (g + 1 < CH / PG) lds_group_rd(nx, cc + (g + 1) * PG);
+        // the steps depend on phase: pinning it here keeps the next group's reads (volatile,
+        // so after the wait) ahead of this group's steps instead of sunk behind them
+        asm volatile("" : "+v"(phase), "+v"(integ));
         const int64_t k0 = ch * CH + g * PG;
         bool redo = k0 == 0;                             // the call's literal first sample
         if (!redo) {
