@@ -285,15 +285,25 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
     phase = phase + cfg.kp * e + integ;
     arg = w * ((off + (double)k) + 1.0) + phase;
   };
+  // Q-form (5 f64 ops per step, P.qform): the integrator's constant drift -pi Ki per step is
+  // absorbed into the constants.  Within a group (step i = k mod 32), W_i = V_i + i kB and
+  // Q_i = phase_i + kB i(i-1)/2 obey W' = W + kA f, Q' = Q + W + kC f, and with the prep
+  // kernel's c'_i = c_i + kB i(i-1)/(4 pi), t = c'_i - Q_i/2pi is the same t.  Q is what
+  // the theta row holds (for every step of the call, general ones included); the NCO kernel
+  // takes kB (i+1) i / 2 back off.
   const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
   const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
-  double V = 0.0;
-  auto fast = [&](double c) {
+  double W = 0.0;
+  auto fastq = [&](double c) {
     const double t = fma(-kInv2Pi, phase, c);
     const double f = __builtin_amdgcn_fract(t);
-    const double S = phase + V;
-    V = fma(kA, f, V - kB);
+    const double S = phase + W;
+    W = fma(kA, f, W);
     phase = fma(kC, f, S);
+  };
+  auto qof = [&](double ph, int64_t k) {                 // the stored Q of step k's result
+    const double i = (double)(k % PG);
+    return ph + kB * ((i + 1.0) * i * 0.5);
   };
   for (int64_t ch = 0; ch < nch; ++ch) {
     __builtin_amdgcn_s_barrier();                        // chunk ch is in LDS
@@ -313,17 +323,18 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
         if (!redo) {
           const double ph0 = phase, in0 = integ, ar0 = arg;
           double pv[PG];
-          V = integ - kD;
+          W = integ - kD;                                // V_0 = W_0
 #pragma unroll
           for (int i = 0; i < PG; ++i) {
-            fast(dbl(cv[i / 2], i & 1));
-            pv[i] = phase;
+            fastq(dbl(cv[i / 2], i & 1));
+            pv[i] = phase;                               // Q_{i+1}
           }
           if (phase != phase) {                          // a 0 / NaN input in the group
             phase = ph0; integ = in0; arg = ar0;
             redo = true;
           } else {
-            integ = V + kD;
+            phase -= kB * (double)(PG * (PG - 1) / 2);   // Q_32 -> phase_32
+            integ = (W - kB * (double)PG) + kD;          // W_32 -> V_32 -> integ
             arg = w * ((off + (double)(k0 + PG - 1)) + 1.0) + phase;
             double* tp = th + k0;
 #pragma unroll
@@ -333,7 +344,7 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
         if (redo) {
           for (int i = 0; i < PG; ++i) {
             general(in[k0 + i], k0 + i, k0 + i == 0);
-            th[k0 + i] = phase;
+            th[k0 + i] = qof(phase, k0 + i);
           }
         }
       };
@@ -349,7 +360,7 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
   if (rec) {
     for (int64_t k = nch * CH; k < n; ++k) {      // tail (< CH samples)
       general(in[k], k, k == 0);
-      th[k] = phase;
+      th[k] = qof(phase, k);
     }
     th[n] = off;                                  // the NCO kernel's trigOffset
     if (n > 0) {
@@ -382,7 +393,12 @@ __global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
     const double cc = (x > 0.f ? 0.0 : kPi) - w * (off + (double)k);   // the previous step's w (off + k)
     // a 0 / NaN input gets a NaN constant: a fast group over it ends in a NaN phase, which
     // pll_chunk_kernel takes as its signal to redo the group in the general form
-    c[k] = odd ? __builtin_nan("") : fma(cc, kInv2Pi, 0.5);
+    double cv = fma(cc, kInv2Pi, 0.5);
+    if (P.qform) {                                      // pll_chunk_kernel's Q-form
+      const double i = (double)(k % PG);
+      cv = cv + (kPi * J.cfg.ki) * kInv2Pi * (i * (i - 1.0) * 0.5);
+    }
+    c[k] = odd ? __builtin_nan("") : cv;
   }
   // groups of PG = 32 lanes: the low and high half of each wave
   const uint64_t m = __ballot(odd);
@@ -405,7 +421,12 @@ __global__ void nco_jobs_kernel(PllJobs P) {
   const double* ph = J.theta + (int64_t)s * J.th_stride;
   const double off = ph[P.n];
   const double w = 2.0 * kPi * (J.cfg.freq / J.cfg.fs);
-  const double th = w * ((off + (double)k) + 1.0) + ph[k];
+  double p = ph[k];
+  if (P.qform) {                                        // Q_{i+1} -> phase_{i+1}
+    const double i = (double)(k % PG);
+    p = p - (kPi * J.cfg.ki) * ((i + 1.0) * i * 0.5);
+  }
+  const double th = w * ((off + (double)k) + 1.0) + p;
   const double a = th * J.cfg.scale + J.cfg.adj;
   double sv, cv;
   sincos(a, &sv, &cv);
@@ -417,6 +438,13 @@ __global__ void nco_jobs_kernel(PllJobs P) {
 
 namespace {
 // the job table's strides and whether every row allows 16-B loads / stores
+// recurrences per wave as the loop launcher picks them, and whether pll_chunk_kernel (and so
+// the Q-form, which the prep and NCO kernels must agree on) runs
+int pll_lpw(const PllJobs& P) {
+  int lpw = 1;
+  while (lpw < 64 && P.njobs * ((P.nstreams + lpw - 1) / lpw) > kMaxPllWaves) lpw *= 2;
+  return lpw;
+}
 hipError_t pll_check(const PllJobs& P, bool* vec) {
   if (P.njobs < 1 || P.njobs > SDR_PLL_MAXJ || P.nstreams <= 0 || P.n < 0) return hipErrorInvalidValue;
   *vec = true;
@@ -434,9 +462,11 @@ hipError_t sdr_launch_pll_prep(const PllJobs& P, hipStream_t st) {
   bool vec;
   const hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
+  PllJobs L = P;
+  L.qform = vec && pll_lpw(P) == 1;
   if (P.n > 0)
     hipLaunchKernelGGL(pll_prep_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
-                       dim3(256), 0, st, P);
+                       dim3(256), 0, st, L);
   return hipGetLastError();
 }
 
@@ -445,8 +475,8 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
   const hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
   PllJobs L = P;
-  L.lpw = 1;
-  while (L.lpw < 64 && L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw) > kMaxPllWaves) L.lpw *= 2;
+  L.lpw = pll_lpw(P);
+  L.qform = vec && L.lpw == 1;
   const dim3 grid((unsigned)(L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw)));
   if (vec && L.lpw == 1) hipLaunchKernelGGL(pll_chunk_kernel, grid, dim3(128), 0, st, L);
   else if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, L);
@@ -458,9 +488,11 @@ hipError_t sdr_launch_pll_nco(const PllJobs& P, hipStream_t st) {
   bool vec;
   const hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
+  PllJobs L = P;
+  L.qform = vec && pll_lpw(P) == 1;
   if (P.n > 0)
     hipLaunchKernelGGL(nco_jobs_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
-                       dim3(256), 0, st, P);
+                       dim3(256), 0, st, L);
   return hipGetLastError();
 }
 

@@ -148,6 +148,9 @@ int main() {
       best = std::min(best, ms);
     }
     printf("S=%d product  : %8.1f us  %6.1f ns/step (prep + loop + nco kernels)\n", S, best * 1e3, best * 1e6 / n);
+    // the product's chunk kernel stores the Q-form phase (pll.hip); rebuild the phase
+    hipLaunchKernelGGL(qfix, dim3((unsigned)((n + 255) / 256), S), dim3(256), 0, 0, dth, n, n + 2, kPi * cfg.ki);
+    CK(hipDeviceSynchronize());
     std::vector<double> t_ref(S * (n + 2)), t_v(S * (n + 2));
     CK(hipMemcpy(t_ref.data(), dth, sizeof(double) * S * (n + 2), hipMemcpyDeviceToHost));
     auto run_v = [&](auto kern, const char* name) {
