@@ -13,3 +13,5 @@ done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o c5 -- python3 $GRAFT_REPO_ROOT/bench.py --workload c5 --no-cpu --steps 64 > $O/prof_c5.json 2>&1
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_default -o fused -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --steps 20 > $O/prof_default.json 2>&1
+cd $GRAFT_REPO_ROOT
+timeout -k 10 200 python3 bench.py --workload c5 --streams 64 --steps 64 --no-cpu > $O/bench_c5_s64.json 2> $O/bench_c5_s64.err
