@@ -28,6 +28,8 @@
 //      (fmPll.py:33, Python's rounding), ncoOut[k+1] = cos(th_k*scale + adj),
 //      ncoOutQ[k+1] = sin(th_k*scale + adj) (fmPll.py:36-37).
 // All phase arithmetic is f64 (SURVEY §7 hard part 5: an fp32 NCO drifts).
+#include <stdlib.h>
+
 #include "sdr_launch.h"
 
 namespace {
@@ -74,6 +76,7 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
     const float* in; double* th; const double* c; float* nco_i; float* nco_q;
   } L{J.in + (int64_t)s * J.in_stride, J.theta + (int64_t)s * J.th_stride, J.cbuf + (int64_t)s * J.c_stride,
       J.nco_i + (int64_t)s * J.out_stride, J.nco_q ? J.nco_q + (int64_t)s * J.out_stride : nullptr};
+  if (P.n > 0 && L.c[0] == __builtin_inf()) return;      // solved by pll_spec_kernel
   const PllCfg cfg = J.cfg;
   double* st = J.state + (int64_t)s * 6;
   const int64_t n = P.n;
@@ -240,6 +243,7 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
   const int64_t n = P.n;
   const int64_t nch = n / CH;
   const double* cr = J.cbuf + (int64_t)s * J.c_stride;
+  if (n > 0 && cr[0] == __builtin_inf()) return;        // solved by pll_spec_kernel
   if (loader) {
     // ---- wave 1: constants -> LDS ring, one barrier per chunk ----
     const unsigned voff = 16u * lane;
@@ -374,6 +378,204 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
   }
 }
 
+// ---------------------------------------------------------------------------------
+// pll_spec_kernel: the recurrence of a block solved in parallel, then checked (one
+// workgroup of SPEC_T threads per recurrence; launched before the loop kernel, which skips
+// every recurrence this kernel completed).
+//
+// With the wrap's integer part m_k = floor(t_k) known, the fast step is LINEAR in the
+// state x = (phaseEst, V): f = (c_k - m_k) - phase/2pi, so
+//   x' = A x + u_k,  A = [[1 - kC/2pi, 1], [-kA/2pi, 1]],  u_k = (kC d_k, kA d_k - kB), d_k = c_k - m_k
+// and A is a contraction (|eig| = sqrt(1 - Kp) = 0.987 per step at the reference's bandwidth).
+//   1. Guess: thread j runs the true (nonlinear) step over the SPEC_W samples before its
+//      chunk, from the state after sample 0 with the phase estimate extrapolated by the
+//      integrator (the loop pulls the guess onto the trajectory), then over its chunk,
+//      keeping each step's m_k (LDS, a byte relative to floor(c_k)).
+//   2. Solve: each chunk's response to its d_k from zero state, then the chunk-start states by
+//      a Hillis-Steele scan of y_{j+1} = A^L y_j + z_j across the threads (y_0 exact).
+//   3. Check: every thread reruns the true step from its y_j, stores the phases, and compares
+//      each step's m_k with the one the solve used.  No mismatch anywhere => every chunk ran
+//      from its exact start state (induction over chunks), i.e. the sequential recurrence,
+//      up to rounding (the scan's association; the f32 outputs cannot see it).  Otherwise
+//      the rerun's m_k are the next guess (each round fixes at least the first wrong chunk).
+// A locked loop keeps fract(t) >= 0.2 away from the wrap (tools/pll_spec_probe.py), so the
+// guess holds after a few hundred samples; the sequential kernel remains the path for what
+// does not converge in SPEC_IT rounds (acquisition transients, noise), for 0 / NaN inputs
+// (the general form) and for blocks beyond SPEC_NMAX samples.  Sample 0 of a call is the
+// literal general step (fI, fQ from the caller's state), as in the loop kernels.  A completed
+// recurrence is marked by c[0] = +inf (c[0] is the literal sample's slot: the loop kernels
+// never read it, and the prep kernel rewrites it every call).
+constexpr int SPEC_T = 256;          // threads (chunks) per recurrence
+constexpr int SPEC_W = 128;          // warm-up samples before each chunk
+constexpr int SPEC_IT = 3;           // solve / check rounds before the sequential kernel takes over
+constexpr int SPEC_NMAX = 16384 + 1; // samples per call (the constants of steps 1.. in LDS: 128 KiB)
+
+__global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
+#pragma clang fp contract(off)
+  __shared__ double cl[SPEC_NMAX - 1];         // c_k of steps 1 .. n-1 (plain form)
+  __shared__ int8_t mrel[SPEC_NMAX - 1];       // m_k - floor(c_k) + jb, jb = floor(phaseEst_1 / 2pi)
+  __shared__ d2v yb[SPEC_T];
+  __shared__ double x1s[2];
+  const int q = blockIdx.x / P.nstreams;
+  const int s = blockIdx.x - q * P.nstreams;
+  const int tid = threadIdx.x;
+  const PllJob& J = P.j[q];
+  const int64_t n = P.n;
+  const float* in = J.in + (int64_t)s * J.in_stride;
+  double* th = J.theta + (int64_t)s * J.th_stride;
+  double* cr = J.cbuf + (int64_t)s * J.c_stride;
+  const PllCfg cfg = J.cfg;
+  double* st = J.state + (int64_t)s * 6;
+  const double off = st[5];
+  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
+  const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
+  // the prep kernel's constants are in the Q-form when the chunk kernel is the loop kernel
+  auto cplain = [&](int64_t k) {
+    double c = cr[k];
+    if (P.qform) {
+      const double i = (double)(k % PG);
+      c = c - (kPi * cfg.ki) * kInv2Pi * (i * (i - 1.0) * 0.5);
+    }
+    return c;
+  };
+  auto thval = [&](double ph, int64_t k) {       // what the theta row holds for step k
+    if (!P.qform) return ph;
+    const double i = (double)(k % PG);
+    return ph + kB * ((i + 1.0) * i * 0.5);
+  };
+  // sample 0: the literal general step (thread 0), as the loop kernels' general()
+  if (tid == 0) {
+    const double xv = (double)in[0];
+    const double e = atan2(xv * (-st[3]), xv * st[2]);
+    const double integ = st[0] + cfg.ki * e;
+    const double phase = st[1] + cfg.kp * e + integ;
+    x1s[0] = phase;
+    x1s[1] = integ - kD;
+  }
+  __syncthreads();
+  const double p1 = x1s[0], v1 = x1s[1];
+  const int64_t N = n - 1;                       // steps 1 .. n-1
+  // every step reads its constant several times: stage them (plain form) in LDS
+  for (int64_t k = tid; k < N; k += SPEC_T) cl[k] = cplain(k + 1);
+  __syncthreads();
+  // the integer part relative to floor(c_k) is floor(-phaseEst/2pi + frac(c_k)): near -jb
+  // within a block, so it fits a byte once jb is taken off (a drifting phase estimate moves jb)
+  const double jb = floor(kInv2Pi * p1);
+  auto rel_of = [&](double t, double c) { return floor(t) - floor(c) + jb; };
+  const int L = (int)((N + SPEC_T - 1) / SPEC_T);
+  const int TE = (int)((N + L - 1) / L);         // chunks in use; chunks 0 .. TE-2 are full
+  const int64_t k0 = 1 + (int64_t)tid * L;
+  const int64_t k1 = tid < TE ? min<int64_t>(k0 + L, n) : k0;
+  // 1. guess
+  bool bad = false;
+  {
+    // a locked loop's phase estimate moves by integ per step (mean f = 1/2): the warm-up
+    // starts from that extrapolation, so a short warm-up lands within the wrap margin
+    const int64_t kw = max<int64_t>(1, k0 - SPEC_W);
+    double p = p1 + (double)(kw - 1) * (v1 + kD), V = v1;
+#pragma unroll 8
+    for (int64_t k = kw; k < k0 && tid < TE; ++k) {
+      const double t = fma(-kInv2Pi, p, cl[k - 1]);
+      const double f = __builtin_amdgcn_fract(t);
+      const double S = p + V;
+      V = fma(kA, f, V - kB);
+      p = fma(kC, f, S);
+    }
+    for (int64_t k = k0; k < k1; ++k) {
+      const double c = cl[k - 1];
+      const double t = fma(-kInv2Pi, p, c);
+      const double r = rel_of(t, c);
+      bad |= !(r >= -127.0 && r <= 127.0);       // also a NaN constant (a 0 / NaN input)
+      mrel[k - 1] = (int8_t)(bad ? 0.0 : r);
+      const double f = __builtin_amdgcn_fract(t);
+      const double S = p + V;
+      V = fma(kA, f, V - kB);
+      p = fma(kC, f, S);
+    }
+  }
+  if (__syncthreads_or(bad)) return;             // a 0 / NaN input (the general form's case)
+  // A^L and its squarings (every thread the same operations)
+  const double a00 = 1.0 - kC * kInv2Pi, a10 = -kA * kInv2Pi;
+  double P00 = 1.0, P01 = 0.0, P10 = 0.0, P11 = 1.0;
+  for (int i = 0; i < L; ++i) {                  // P = A P
+    const double n00 = a00 * P00 + P10, n01 = a00 * P01 + P11;
+    const double n10 = a10 * P00 + P10, n11 = a10 * P01 + P11;
+    P00 = n00; P01 = n01; P10 = n10; P11 = n11;
+  }
+  for (int round = 0; round < SPEC_IT; ++round) {
+    // 2. solve: the chunk's response from zero state
+    double zp = 0.0, zv = 0.0;
+#pragma unroll 4
+    for (int64_t k = k0; k < k1; ++k) {
+      const double c = cl[k - 1];
+      const double d = c - (floor(c) + ((double)mrel[k - 1] - jb));
+      const double np = a00 * zp + zv + kC * d;
+      const double nv = a10 * zp + zv + (kA * d - kB);
+      zp = np; zv = nv;
+    }
+    __syncthreads();                             // mrel reads done before the checks below
+    // v_0 = x_1, v_j = z_{j-1}; y_j = sum_{i<=j} (A^L)^(j-i) v_i
+    double vp = 0.0, vv = 0.0;
+    if (tid + 1 < SPEC_T) yb[tid + 1] = d2v{zp, zv};
+    if (tid == 0) yb[0] = d2v{p1, v1};
+    __syncthreads();
+    if (tid < TE) { vp = yb[tid].x; vv = yb[tid].y; }
+    double Q00 = P00, Q01 = P01, Q10 = P10, Q11 = P11;
+    for (int o = 1; o < SPEC_T; o <<= 1) {
+      __syncthreads();
+      yb[tid] = d2v{vp, vv};
+      __syncthreads();
+      if (tid >= o && tid < TE) {
+        const d2v u = yb[tid - o];
+        vp = vp + (Q00 * u.x + Q01 * u.y);
+        vv = vv + (Q10 * u.x + Q11 * u.y);
+      }
+      const double n00 = Q00 * Q00 + Q01 * Q10, n01 = Q00 * Q01 + Q01 * Q11;
+      const double n10 = Q10 * Q00 + Q11 * Q10, n11 = Q10 * Q01 + Q11 * Q11;
+      Q00 = n00; Q01 = n01; Q10 = n10; Q11 = n11;
+    }
+    // 3. check: the true step from y_j
+    bool miss = false;
+    double p = vp, V = vv;
+    for (int64_t k = k0; k < k1; ++k) {
+      const double c = cl[k - 1];
+      const double t = fma(-kInv2Pi, p, c);
+      const double r = rel_of(t, c);
+      miss |= r != (double)mrel[k - 1];          // (out of a byte's range: a miss, and so on)
+      mrel[k - 1] = (int8_t)(r >= -127.0 && r <= 127.0 ? r : 0.0);
+      const double f = __builtin_amdgcn_fract(t);
+      const double S = p + V;
+      V = fma(kA, f, V - kB);
+      p = fma(kC, f, S);
+      th[k] = thval(p, k);
+    }
+    if (!__syncthreads_or(miss)) {
+      // done: the caller-visible results exactly as the loop kernels leave them
+      if (tid == 0) {
+        th[0] = thval(p1, 0);
+        J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];
+        if (J.nco_q)
+          J.nco_q[(int64_t)s * J.out_stride] =
+              (float)((off > 0.0) ? sin((w * off + st[1]) * cfg.scale + cfg.adj) : 0.0);
+      }
+      __syncthreads();                           // st[1], st[4] read before the last chunk writes st
+      if (tid == TE - 1) {
+        const double arg = w * ((off + (double)(n - 1)) + 1.0) + p;
+        th[n] = off;
+        st[0] = V + kD;
+        st[1] = p;
+        st[2] = cos(arg);
+        st[3] = sin(arg);
+        st[4] = cos(arg * cfg.scale + cfg.adj);
+        st[5] = off + (double)n;
+      }
+      if (tid == 0) cr[0] = __builtin_inf();      // the loop kernel skips this recurrence
+      return;
+    }
+  }
+}
+
 // Per-sample constants of the loop (parallel): c_k = (sel_k - w (off + k)) / 2pi + 1/2 and one flag per
 // PG-sample group holding a 0 or NaN input; c row layout: c[0..n) | flags[0..n/PG).
 __global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
@@ -445,6 +647,11 @@ int pll_lpw(const PllJobs& P) {
   while (lpw < 64 && P.njobs * ((P.nstreams + lpw - 1) / lpw) > kMaxPllWaves) lpw *= 2;
   return lpw;
 }
+// the parallel solve runs ahead of the loop kernel unless SDR_PLL_SPEC=0 (A/B runs)
+bool pll_spec_enabled() {
+  static const bool on = [] { const char* e = getenv("SDR_PLL_SPEC"); return !(e && e[0] == '0'); }();
+  return on;
+}
 hipError_t pll_check(const PllJobs& P, bool* vec) {
   if (P.njobs < 1 || P.njobs > SDR_PLL_MAXJ || P.nstreams <= 0 || P.n < 0) return hipErrorInvalidValue;
   *vec = true;
@@ -478,6 +685,8 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
   L.lpw = pll_lpw(P);
   L.qform = vec && L.lpw == 1;
   const dim3 grid((unsigned)(L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw)));
+  if (pll_spec_enabled() && L.n >= 2 && L.n <= SPEC_NMAX)
+    hipLaunchKernelGGL(pll_spec_kernel, dim3((unsigned)(L.njobs * L.nstreams)), dim3(SPEC_T), 0, st, L);
   if (vec && L.lpw == 1) hipLaunchKernelGGL(pll_chunk_kernel, grid, dim3(128), 0, st, L);
   else if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, L);
   else hipLaunchKernelGGL(pll_lanes_kernel<false>, grid, dim3(64), 0, st, L);
