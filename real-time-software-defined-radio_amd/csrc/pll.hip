@@ -388,8 +388,8 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 //   x' = A x + u_k,  A = [[1 - kC/2pi, 1], [-kA/2pi, 1]],  u_k = (kC d_k, kA d_k - kB), d_k = c_k - m_k
 // and A is a contraction (|eig| = sqrt(1 - Kp) = 0.987 per step at the reference's bandwidth).
 //   1. Guess: thread j runs the true (nonlinear) step over the SPEC_W samples before its
-//      chunk, from the state after sample 0 with the phase estimate extrapolated by the
-//      integrator (the loop pulls the guess onto the trajectory), then over its chunk,
+//      chunk, from the state after sample 0 (the loop pulls the guess onto the
+//      trajectory), then over its chunk,
 //      keeping each step's m_k (LDS, a byte relative to floor(c_k)).
 //   2. Solve: each chunk's response to its d_k from zero state, then the chunk-start states by
 //      a Hillis-Steele scan of y_{j+1} = A^L y_j + z_j across the threads (y_0 exact).
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 // recurrence is marked by c[0] = +inf (c[0] is the literal sample's slot: the loop kernels
 // never read it, and the prep kernel rewrites it every call).
 constexpr int SPEC_T = 256;          // threads (chunks) per recurrence
-constexpr int SPEC_W = 128;          // warm-up samples before each chunk
+constexpr int SPEC_W = 256;          // warm-up samples before each chunk
 constexpr int SPEC_IT = 3;           // solve / check rounds before the sequential kernel takes over
 constexpr int SPEC_NMAX = 16384 + 1; // samples per call (the constants of steps 1.. in LDS: 128 KiB)
 
@@ -470,10 +470,12 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
   // 1. guess
   bool bad = false;
   {
-    // a locked loop's phase estimate moves by integ per step (mean f = 1/2): the warm-up
-    // starts from that extrapolation, so a short warm-up lands within the wrap margin
+    // from the block's first state: a locked estimate moves little within a block (a 3 Hz
+    // pilot offset: 1.2 rad over 15 360 samples), and 256 steps of the loop shrink that
+    // ~30-fold.  (Extrapolating by integ does worse: integ swings with the loop's own
+    // oscillation, and a 64-step mean of it mispredicts a block's drift by up to 4 rad.)
     const int64_t kw = max<int64_t>(1, k0 - SPEC_W);
-    double p = p1 + (double)(kw - 1) * (v1 + kD), V = v1;
+    double p = p1, V = v1;
 #pragma unroll 8
     for (int64_t k = kw; k < k0 && tid < TE; ++k) {
       const double t = fma(-kInv2Pi, p, cl[k - 1]);
