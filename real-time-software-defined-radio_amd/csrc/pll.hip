@@ -405,11 +405,14 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 // literal general step (fI, fQ from the caller's state), as in the loop kernels.  A completed
 // recurrence is marked by c[0] = +inf (c[0] is the literal sample's slot: the loop kernels
 // never read it, and the prep kernel rewrites it every call).
-constexpr int SPEC_T = 256;          // threads (chunks) per recurrence
 constexpr int SPEC_W = 256;          // warm-up samples before each chunk
 constexpr int SPEC_IT = 3;           // solve / check rounds before the sequential kernel takes over
 constexpr int SPEC_NMAX = 16384 + 1; // samples per call (the constants of steps 1.. in LDS: 128 KiB)
 
+// SPEC_T threads (chunks) per recurrence: 256 (one wave per SIMD) up to 10 240 samples, 512
+// beyond (the warm-up is the same length either way; 512 halves the chunks, and a second
+// wave per SIMD then pays: c5 blocks 56 -> ~50 us, c4 blocks slower)
+template <int SPEC_T>
 __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
 #pragma clang fp contract(off)
   __shared__ double cl[SPEC_NMAX - 1];         // c_k of steps 1 .. n-1 (plain form)
@@ -552,7 +555,9 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
       p = fma(kC, f, S);
       th[k] = thval(p, k);
     }
-    if (!__syncthreads_or(miss)) {
+    const int nmiss = __syncthreads_count(miss);
+    if (P.spec_dbg && tid == 0) printf("pll_spec q%d s%d n%ld T%d L%d TE%d round %d: %d chunks missed\n", q, s, (long)n, SPEC_T, L, TE, round, nmiss);
+    if (nmiss == 0) {
       // done: the caller-visible results exactly as the loop kernels leave them
       if (tid == 0) {
         th[0] = thval(p1, 0);
@@ -687,8 +692,13 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
   L.lpw = pll_lpw(P);
   L.qform = vec && L.lpw == 1;
   const dim3 grid((unsigned)(L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw)));
-  if (pll_spec_enabled() && L.n >= 2 && L.n <= SPEC_NMAX)
-    hipLaunchKernelGGL(pll_spec_kernel, dim3((unsigned)(L.njobs * L.nstreams)), dim3(SPEC_T), 0, st, L);
+  if (pll_spec_enabled() && L.n >= 2 && L.n <= SPEC_NMAX) {
+    PllJobs S = L;
+    S.spec_dbg = getenv("SDR_PLL_SPEC_DEBUG") != nullptr;   // per-round prints (A/B runs)
+    const dim3 g((unsigned)(L.njobs * L.nstreams));
+    if (L.n > 10240) hipLaunchKernelGGL(pll_spec_kernel<512>, g, dim3(512), 0, st, S);
+    else hipLaunchKernelGGL(pll_spec_kernel<256>, g, dim3(256), 0, st, S);
+  }
   if (vec && L.lpw == 1) hipLaunchKernelGGL(pll_chunk_kernel, grid, dim3(128), 0, st, L);
   else if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, L);
   else hipLaunchKernelGGL(pll_lanes_kernel<false>, grid, dim3(64), 0, st, L);

@@ -64,7 +64,7 @@ struct PllJob {
   float* nco_i; float* nco_q; int64_t out_stride; PllCfg cfg; double* cbuf; int64_t c_stride;
   double off; int off_given;   // the prep kernel's trigOffset, when not read from state[5]
 };
-struct PllJobs { PllJob j[SDR_PLL_MAXJ]; int njobs; int nstreams; int64_t n; int lpw; int qform; };  // lpw, qform: set by the launchers
+struct PllJobs { PllJob j[SDR_PLL_MAXJ]; int njobs; int nstreams; int64_t n; int lpw; int qform; int spec_dbg; };  // lpw, qform, spec_dbg: set by the launchers
 // prep (per-sample constants) -> loop (one lane per recurrence) -> NCO; the three launches
 // separately (the receiver puts them on different streams) or together
 hipError_t sdr_launch_pll_prep(const PllJobs& jobs, hipStream_t st);
