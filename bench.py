@@ -60,6 +60,12 @@ def parse():
                     help="mono: configs[1]+[2] batched (the headline); c3/c4: per-block drop-in path; "
                          "c5: multi-stream mono+stereo+RDS")
     ap.add_argument("--streams", type=int, default=8, help="c5: independent streams per GPU")
+    ap.add_argument("--span", type=int, default=256,
+                    help="c5: 153 600-sample blocks of every stream processed per receiver call (device-resident "
+                         "spans, time-parallel: FE and filters as one pass, PLLs as long calls); 1 = the per-block "
+                         "receiver, one block of every stream per call")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="mono: skip the c5 (8 and 1 streams) and u8 blocks appended to the headline line")
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default 50; c5: 256 blocks)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--settle-ms", type=float, default=250.0,
@@ -85,7 +91,8 @@ def parse():
                     help="PMC-derived HBM bytes per FE launch (written by tools/pmc_traffic.py)")
     a = ap.parse_args()
     if a.steps is None:
-        a.steps = 256 if a.workload == "c5" else (200 if a.workload in ("c3", "c4") else 50)
+        a.steps = ((256 if a.span == 1 else 10) if a.workload == "c5" else
+                   (200 if a.workload in ("c3", "c4") else 50))
     return a
 
 
@@ -239,6 +246,16 @@ def load_traffic(path, taps, blocks, kpath):
     return None
 
 
+def split_range(n_total: int, ws: int, rank: int, halo: int, step: int = 50):
+    """--split-stream: rank r's range [s0, s1) of ONE stream of n_total complex
+    samples (boundaries on whole audio samples, `step` = rf_decim x audio_decim IQ samples)
+    and the start w0 = s0 - halo of the read-only halo it reads before it.  Returns
+    (w0, s0, s1); its audio outputs are those of IQ positions [s0, s1)."""
+    s0 = (rank * n_total // ws) // step * step
+    s1 = n_total if rank == ws - 1 else ((rank + 1) * n_total // ws) // step * step
+    return max(0, s0 - halo), s0, s1
+
+
 def device_for(local: int) -> int:
     """GPU of this rank: LOCAL_RANK (one process per GPU); ranks beyond the visible devices
     wrap around (a multi-process rehearsal on a one-GPU box)."""
@@ -252,6 +269,8 @@ def main():
     ws, rank, local = dist_setup(args)
     local = device_for(local)
     os.environ["SDR_DEVICE"] = str(local)
+    if args.workload == "c5" and args.span > 1:
+        return run_c5_span(args, ws, rank, local)
     if args.workload != "mono":
         return run_rx(args, ws, rank, local)
     import rtsdr
@@ -266,10 +285,7 @@ def main():
     dt = np.uint8 if args.iq == "u8" else np.float32
     if args.split_stream:
         # rank r: IQ [s0, s1) of the one stream plus the halo before s0 (no exchange)
-        step = 50
-        s0 = (rank * n_total // ws) // step * step
-        s1 = n_total if rank == ws - 1 else ((rank + 1) * n_total // ws) // step * step
-        w0 = max(0, s0 - rtsdr.split_halo(len(rf_b), len(au_b)))
+        w0, s0, s1 = split_range(n_total, ws, rank, rtsdr.split_halo(len(rf_b), len(au_b)))
         iq = rtsdr.synth.fm_iq(n_total, seed=0, dtype=dt)[2 * w0:2 * s1].copy()
         n = s1 - w0
     else:
@@ -407,6 +423,18 @@ def main():
     elif rank == 0:
         result["cpu_baseline"] = None
     tm.close()
+    if not args.no_extras and not args.split_stream and args.iq == "f32" and args.path == "fused":
+        # the other configurations, measured in the same run (same box, same clock): C5 at its
+        # per-GPU shapes (8 streams and 1 stream, >= 256 blocks per stream) and the u8 FE + mono
+        del d_iq, d_dm, d_au
+        extras = {
+            "c5": c5_measure(ctx, 8, 256, 5, 2, rank, ws, cpu=(ws == 1 and not args.no_cpu and rank == 0),
+                             args=args),
+            "c5_1stream": c5_measure(ctx, 1, 256, 10, 2, rank, ws),
+            "u8": u8_measure(ctx, 64, 50, 10, rank),
+        }
+        if rank == 0:
+            result.update(extras)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if ws > 1:
@@ -621,6 +649,161 @@ def run_rx(args, ws, rank, local):
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+C5_B = 153_600                 # complex samples per reference block (src/fm_radio.cpp:23)
+VALU_PEAK_TFLOPS = 157.3       # MI355X FP32 vector peak (MI355X_MICROARCH.md)
+
+
+def chain_flops_per_sample(rf_taps=151, taps=151, audio_decim=5, up=19, down=80):
+    """FP32 flops (2 per multiply-add) of the C5 chain's FIR work per complex input sample
+    (DESIGN.md §4): the RF FIR on I and Q at 1/10 of the input rate, then
+    per demod sample the stage filters -- audio LPF /5, pilot BPF, stereo BPF, RDS extract
+    (stage A), RDS square BPF (B), stereo LPF /5 and RDS I/Q LPFs (C), the x19 /80 resamplers
+    (taps/19 per output, 19/80 outputs per sample; D) and the RRC I/Q at the resampled rate
+    (E).  The demod atan2 and the PLLs (f64) are not counted."""
+    macs_demod = (taps / audio_decim + 3 * taps + taps + taps / audio_decim + 2 * taps
+                  + 2 * (taps / up) * up / down + 2 * taps * up / down)
+    return 2.0 * (2 * rf_taps + macs_demod) / 10.0
+
+
+def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, args=None):
+    """configs[4] per GPU: S independent u8 streams of K reference blocks each, device-resident,
+    mono + stereo + RDS to the RRC output, K blocks of every stream per receiver call (one
+    span: the time-parallel receiver).  The synthetic span is K x 64 ms, over
+    which every tone of the composite completes whole cycles, so repeating it is seamless
+    (the PLLs stay locked across steps); stream s is the span rotated by s/S of its length."""
+    import rtsdr
+    from importlib import import_module
+    _lib = import_module("real-time-software-defined-radio_amd._lib")
+    rf_b, au_b = rtsdr.design.mono_coeffs(151, 151)
+    n = K * C5_B
+    base = rtsdr.synth.fm_iq(n, seed=rank * 1009, dtype=np.uint8)
+    rows = np.stack([np.roll(base, 2 * ((s * n // S) // 50 * 50)) for s in range(S)])
+    del base
+    d_iq = _lib.DeviceBuffer.from_array(ctx, rows)
+    cpu_rows = rows[0, :16 * 2 * C5_B].copy() if cpu else None
+    del rows
+    rx = rtsdr.Receiver(S, n, stereo=True, rds=True, iq_dtype=np.uint8, rf_coeff=rf_b, audio_coeff=au_b,
+                        pipeline=pipeline, ctx=ctx)
+
+    def step():
+        rx.process_dev(d_iq.ptr, n)
+
+    for _ in range(warmup):
+        step()
+    ctx.synchronize()
+    rx.set_timing(True)                       # per-stage GPU times: a separate pass
+    stages = []
+    for _ in range(2):
+        step()
+        stages.append(rx.stage_ms())
+    rx.set_timing(False)
+    stage_ms = {k: round(float(np.mean([st[k] for st in stages])), 4) for k in stages[0]}
+    rx.pll_stats(reset=True)
+    barrier(ws)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.synchronize()
+    barrier(ws)
+    elapsed = max_over_ranks(ws, time.perf_counter() - t0)
+    pll = rx.pll_stats()
+    rx.close()
+    d_iq.free()
+    total = S * n * steps * ws
+    fps = chain_flops_per_sample()
+    per_gpu_tflops = fps * S * n * steps / elapsed / 1e12
+    dom = max(stage_ms, key=stage_ms.get)
+    out = {
+        "value": round(total / elapsed / 1e6, 1), "unit": "MS/s",
+        "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps, "warmup": warmup,
+        "config": {"streams_per_gpu": S, "blocks_per_stream_per_step": K, "block_complex": C5_B,
+                   "complex_per_step": S * n, "iq": "u8", "rf_taps": 151, "pipeline": bool(pipeline),
+                   "chain": "FE + mono + stereo + RDS to the RRC output (fmMonoBlock.py:80-173, fmRDSblock.py:127-204)"},
+        "stage_ms": stage_ms,
+        "dominant_stage": {"stage": dom, "ms": stage_ms[dom],
+                           "bound": ("PLL: pseudo-blocks solved in parallel from warm-up guesses and chained "
+                                     "(f64, csrc/pll.hip long calls)") if dom == "pll" else
+                           ("HBM: u8 IQ in, demod out" if dom == "fe" else "FP32 VALU: FIR multiply-adds")},
+        "roofline": {"bound": "valu", "achieved": round(per_gpu_tflops, 3), "peak": VALU_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(per_gpu_tflops / VALU_PEAK_TFLOPS, 4), "traffic": None,
+                     "flops_per_sample": round(fps, 2),
+                     "note": "FIR flops of the whole chain per input sample x samples / wall time per GPU"},
+        "pll_solver": pll,
+    }
+    if cpu and args is not None:
+        out["cpu_baseline"] = ref_rx_baseline(args, cpu_rows, C5_B, True, True, True, 151)
+    return out
+
+
+def u8_measure(ctx, blocks, steps, warmup, rank):
+    """The u8 fused FE + mono kernel (fe_mfma_mono_kernel: the RF FIR on the int8 matrix
+    cores) over `blocks` x 1 024 000 u8 samples of one device-resident stream: HIP events
+    around the launches on the libsdr stream."""
+    import rtsdr
+    from importlib import import_module
+    _lib = import_module("real-time-software-defined-radio_amd._lib")
+    lib, h = ctx.lib, ctx.handle
+    rf_b, au_b = rtsdr.design.mono_coeffs(101, 151)
+    n = blocks * BLOCK
+    M = (n + 9) // 10
+    A = (M + 4) // 5
+    d_iq = _lib.DeviceBuffer.from_array(ctx, rtsdr.synth.fm_iq(n, seed=rank, dtype=np.uint8))
+    d_au = _lib.DeviceBuffer(ctx, 4 * A)
+    rfp, aup = _lib.f64p(rf_b), _lib.f64p(au_b)
+
+    def launch():
+        _lib.check(lib.sdr_fe_mono_dev(h, d_iq.ptr, _lib.SDR_IQ_U8, n, n, 1, rfp, 101, 10, aup, 151, 5, d_au.ptr, A),
+                   "fe_mono u8")
+
+    for _ in range(warmup):
+        launch()
+    ctx.synchronize()
+    tm = _lib.Timer(ctx)
+    e0, e1 = tm.event(), tm.event()
+    tm.record(e0)
+    for _ in range(steps):
+        launch()
+    tm.record(e1)
+    k_ms = tm.elapsed_ms(e0, e1) / steps
+    tm.close()
+    d_iq.free()
+    d_au.free()
+    k_bytes = n * 2 + A * 4
+    gbs = k_bytes / (k_ms * 1e-3) / 1e9
+    return {"value": round(n / (k_ms * 1e-3) / 1e6, 1), "unit": "MS/s", "avg_launch_ms": round(k_ms, 5),
+            "config": {"blocks": blocks, "block_complex": BLOCK, "iq": "u8", "rf_taps": 101, "audio_taps": 151},
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "fe_mfma_mono_kernel (RF FIR on v_mfma_i32_16x16x64_i8) + audio FIR",
+                         "algorithmic_bytes_per_launch": k_bytes}}
+
+
+def run_c5_span(args, ws, rank, local):
+    """--workload c5 (span > 1): the time-parallel receiver, one JSON line."""
+    from importlib import import_module
+    _lib = import_module("real-time-software-defined-radio_amd._lib")
+    ctx = _lib.Context(local)
+    m = c5_measure(ctx, args.streams, args.span, args.steps, args.warmup, rank, ws,
+                   pipeline=not args.no_pipeline, cpu=(ws == 1 and not args.no_cpu and rank == 0), args=args)
+    if rank == 0:
+        result = {"metric": "IQ MSamples/s through the multi-stream mono+stereo+RDS receiver (c5); "
+                            "FIR TFLOP/s vs FP32 VALU peak",
+                  "value": m["value"], "unit": "MS/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+                  "ms_per_step": m["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                  "dtype": "f32",
+                  "data": "synthetic FM IQ (u8), device-resident, one seamless span per stream repeated",
+                  "config": dict(m["config"], workload="configs[4]: independent streams, mono + stereo + RDS to the "
+                                                       "RRC output, time-parallel spans",
+                                 parallelism=f"independent streams x{args.streams * ws}"),
+                  "roofline": m["roofline"], "stage_ms": m["stage_ms"], "dominant_stage": m["dominant_stage"],
+                  "pll_solver": m["pll_solver"], "cpu_baseline": m.get("cpu_baseline")}
+        print(json.dumps(result), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
 
 
 if __name__ == "__main__":

@@ -134,6 +134,31 @@ int sdr_fm_demod(sdr_ctx* ctx, const float* I, const float* Q, int64_t n, double
 int sdr_pll(sdr_ctx* ctx, const float* in, int64_t n, double freq, double fs, double nco_scale,
             double phase_adj, double norm_bw, double* state6, float* nco_i, float* nco_q);
 
+/* How the context's PLL calls were solved (device counters, accumulated since the context was
+ * created or last reset; sdr_pll*, and the receivers built on the context).  A recurrence is
+ * one (stream, PLL) of a call, or one pseudo-block of a long call (n > SDR_PLL_BLOCK_MAX =
+ * 16 385 samples, which is cut into pseudo-blocks solved in parallel and chained).
+ *   RECURRENCES   recurrences solved
+ *   SPEC_R0..R2   ... by the parallel solve (guess + scan + check) in its 1st / 2nd / 3rd round
+ *   SEQUENTIAL    ... by the sequential kernel (the fallback: acquisition, 0 / NaN input)
+ *   LONG_GUESSED  long calls: pseudo-blocks kept as solved from their warm-up start guess
+ *                 (start within the acceptance bound of the chained state after a 2 pi shift)
+ *   LONG_CHAINED  long calls: pseudo-blocks solved again from the start the chain computed
+ *   LONG_MAXGAP   largest accepted bound on the phase deviation between a pseudo-block's
+ *                 solved start and the chained state (radians, the bits of an f64)
+ *   LONG_STOPS    long calls: pseudo-blocks whose start guess was beyond the linear bound (the
+ *                 chain stopped there that round and re-solved it from the exact start)
+ *   LONG_TAIL     long calls: pseudo-blocks left after the rounds, solved sequentially from the
+ *                 chain's exact position (also counted in SEQUENTIAL)
+ * out: SDR_PLL_NSTATS int64 (LONG_MAXGAP: reinterpret as double).  Synchronises the context
+ * stream; reset != 0 zeroes the counters after reading. */
+enum {
+  SDR_PLL_ST_RECURRENCES, SDR_PLL_ST_SPEC_R0, SDR_PLL_ST_SPEC_R1, SDR_PLL_ST_SPEC_R2, SDR_PLL_ST_SEQUENTIAL,
+  SDR_PLL_ST_LONG_GUESSED, SDR_PLL_ST_LONG_CHAINED, SDR_PLL_ST_LONG_MAXGAP, SDR_PLL_ST_LONG_STOPS,
+  SDR_PLL_ST_LONG_TAIL, SDR_PLL_NSTATS
+};
+int sdr_pll_stats(sdr_ctx* ctx, int64_t* out, int reset);
+
 /* Fused mono block: RF front end + audio lfilter + [::audio_decim], intermediate demod
  * kept in HBM.  Replaces the body of model/fmMonoBlock.py:80-109 (one loop
  * iteration) and src/fm_radio.cpp:66-84 + :258.  demod_out optional. */
@@ -272,6 +297,8 @@ int sdr_rx_stage_ms(sdr_rx* rx, float* ms);
 /* carried states (host copies; any may be NULL): demod prev_phase [nstreams], PLL states
  * [nstreams][6] in fmPll's order (model/fmPll.py:39-44) */
 int sdr_rx_state(sdr_rx* rx, double* phase, double* pll_stereo, double* pll_rds);
+/* sdr_pll_stats of the receiver's context, after waiting for every block in flight */
+int sdr_rx_pll_stats(sdr_rx* rx, int64_t* out, int reset);
 
 /* ---- spectral diagnostics -----------------------------------------
  * Bartlett PSD, model/fmSupportLib.py:66-140 (estimatePSD; the C++ src/fourier.cpp:36-110

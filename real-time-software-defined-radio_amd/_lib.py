@@ -27,6 +27,9 @@ RX_OUTPUTS = ("demod", "audio", "bpf_recovery", "nco", "bpf_extraction", "stereo
               "extract", "pre_pll", "nco_i", "nco_q", "lpf_i", "lpf_q", "resample_i", "resample_q",
               "rrc_i", "rrc_q")
 RX_STAGES = ("fe", "filters_of_demod", "rds_square", "pll", "mix_lpf", "resample", "rrc")
+# PLL solve counters (include/sdr.h SDR_PLL_ST_*)
+PLL_STATS = ("recurrences", "spec_r0", "spec_r1", "spec_r2", "sequential", "long_guessed", "long_chained",
+             "long_maxgap", "long_stops", "long_tail")
 
 
 class SdrUnavailable(RuntimeError):
@@ -80,6 +83,7 @@ SIGNATURES = {
     "sdr_fm_demod_dev": (_i32, [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp, _i64]),
     "sdr_pll_dev": (_i32, [_vp, _vp, _i64, _i64, _i32, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp,
                            _i64]),
+    "sdr_pll_stats": (_i32, [_vp, _vp, _i32]),
     "sdr_stereo_combine_dev": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
     "sdr_psd": (_i32, [_vp, _dp, _i64, _i32, _f64, _dp]),
     "sdr_psd_dev": (_i32, [_vp, _vp, _i32, _i64, _i32, _f64, _vp]),
@@ -99,6 +103,7 @@ SIGNATURES = {
     "sdr_rx_output": (_i32, [_vp, _i32, _c.POINTER(_vp), _c.POINTER(_i64), _c.POINTER(_i64)]),
     "sdr_rx_fetch": (_i32, [_vp, _i32, _fp, _i64]),
     "sdr_rx_state": (_i32, [_vp, _dp, _dp, _dp]),
+    "sdr_rx_pll_stats": (_i32, [_vp, _vp, _i32]),
     "sdr_rx_set_timing": (_i32, [_vp, _i32]),
     "sdr_rx_stage_ms": (_i32, [_vp, _fp]),
     "sdr_rds_link_create": (_i32, [_c.POINTER(_vp)]),
@@ -185,6 +190,11 @@ class Context:
     def synchronize(self):
         check(self.lib.sdr_synchronize(self.handle), "sdr_synchronize")
 
+    def pll_stats(self, reset: bool = False) -> dict:
+        """How this context's PLL calls were solved (sdr_pll_stats): counts by solver, and
+        'long_maxgap' (radians) for long calls."""
+        return decode_pll_stats(lambda a: self.lib.sdr_pll_stats(self.handle, a.ctypes.data, int(bool(reset))))
+
 
 _tls = threading.local()
 
@@ -203,6 +213,14 @@ def get_context() -> Context:
         ctx = Context(default_device())
         _tls.ctx = ctx
     return ctx
+
+
+def decode_pll_stats(call) -> dict:
+    a = np.zeros(len(PLL_STATS), dtype=np.int64)
+    check(call(a), "pll_stats")
+    out = {k: int(v) for k, v in zip(PLL_STATS, a)}
+    out["long_maxgap"] = float(a[PLL_STATS.index("long_maxgap"):][:1].view(np.float64)[0])
+    return out
 
 
 # ---- small helpers ----------------------------------------------------------------

@@ -165,6 +165,12 @@ class Receiver:
         check(self.lib.sdr_rx_state(self.handle, f64p(ph), f64p(ps), f64p(pr)), "sdr_rx_state")
         return ph, ps, pr
 
+    def pll_stats(self, reset: bool = False) -> dict:
+        """How the PLL recurrences were solved (sdr_rx_pll_stats: the context's counters, after
+        every block in flight): counts by solver; see _lib.PLL_STATS."""
+        return _lib.decode_pll_stats(lambda a: self.lib.sdr_rx_pll_stats(self.handle, a.ctypes.data,
+                                                                         int(bool(reset))))
+
     def reset(self):
         check(self.lib.sdr_rx_reset(self.handle), "sdr_rx_reset")
         self._pending = None

@@ -150,7 +150,11 @@ int sdr_create(int device, sdr_ctx** out) {
   c->device = device;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&c->pll_stats, sizeof(unsigned long long) * SDR_PLL_NSTATS);
+  if (e == hipSuccess) e = hipMemset(c->pll_stats, 0, sizeof(unsigned long long) * SDR_PLL_NSTATS);
   if (e != hipSuccess) {
+    if (c->pll_stats) (void)hipFree(c->pll_stats);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return fail(SDR_EHIP, "context creation on device %d: %s", device, hipGetErrorString(e));
   }
@@ -164,6 +168,7 @@ void sdr_destroy(sdr_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (int s = 0; s < S_NSLOT; ++s) if (c->slot[s]) (void)hipFree(c->slot[s]);
   for (TapSet& t : c->taps) { (void)hipFree(t.dev_f32); (void)hipFree(t.dev_f64); }
+  if (c->pll_stats) (void)hipFree(c->pll_stats);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -506,7 +511,22 @@ int sdr_pll_dev(sdr_ctx* c, const float* in, int64_t n, int64_t in_stride, int n
   P.j[0] = PllJob{in, nstreams > 1 ? in_stride : n, state, theta, ths, nco_i, nco_q,
                   nstreams > 1 ? out_stride : n + 1,
                   PllCfg{freq, fs, nco_scale, phase_adj, norm_bw * 2.666, norm_bw * norm_bw * 3.555}, cbuf, cst};
+  P.stats = c->pll_stats;
+  const int64_t wb = sdr_pll_work_bytes(1, nstreams, n);    // long calls: pseudo-block records
+  if (wb > 0) TRY(scratch(c, S_PLLW, (size_t)wb, &P.work));
   HIP_TRY(sdr_launch_pll_jobs(P, c->stream));
+  return SDR_OK;
+}
+
+int sdr_pll_stats(sdr_ctx* c, int64_t* out, int reset) {
+  CHECK_CTX(c);
+  if (out == nullptr) return fail(SDR_EINVAL, "sdr_pll_stats: out is NULL");
+  TRY(set_dev(c));
+  unsigned long long h[SDR_PLL_NSTATS];
+  HIP_TRY(hipMemcpyAsync(h, c->pll_stats, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  if (reset) HIP_TRY(hipMemsetAsync(c->pll_stats, 0, sizeof h, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < SDR_PLL_NSTATS; ++i) out[i] = (int64_t)h[i];
   return SDR_OK;
 }
 

@@ -28,11 +28,30 @@
 //      (fmPll.py:33, Python's rounding), ncoOut[k+1] = cos(th_k*scale + adj),
 //      ncoOutQ[k+1] = sin(th_k*scale + adj) (fmPll.py:36-37).
 // All phase arithmetic is f64 (SURVEY §7 hard part 5: an fp32 NCO drifts).
+//
+// Before the loop kernel, pll_spec_kernel solves each recurrence of up to SDR_PLL_BLOCK_MAX
+// samples in parallel (one workgroup per recurrence) and the loop kernel skips what it
+// completed.  Longer calls (a device-resident span of many of the reference's blocks) are cut
+// into pseudo-blocks, one workgroup each, whose start states are guessed by a warm-up and then
+// chained exactly ("long calls", below).  How every recurrence was solved is counted in the
+// context's device counters (sdr_pll_stats, include/sdr.h).
 #include <stdlib.h>
 
+#include <cmath>
+#include <mutex>
+
 #include "sdr_launch.h"
+#include "../../include/sdr.h"
 
 namespace {
+
+// device counters (nullable): vector atomics on a plain global array
+__device__ __forceinline__ void stat_add(unsigned long long* s, int k, unsigned long long v) {
+  if (s != nullptr) atomicAdd(s + k, v);
+}
+__device__ __forceinline__ void stat_max(unsigned long long* s, int k, double v) {
+  if (s != nullptr && v >= 0.0) atomicMax(s + k, (unsigned long long)__double_as_longlong(v));
+}
 
 // 2*pi split into three parts (Cody-Waite), so n*P1 and n*P2 are exact for |n| < 2^26.
 constexpr double kP1 = 6.2831854820251465;       // float32(2 pi), 24 significant bits
@@ -49,6 +68,15 @@ __device__ inline double reduce_2pi(double a) {
   r = fma(-n, kP2, r);
   r = fma(-n, kP3, r);
   return r;
+}
+
+// The loop's per-sample constant (pll_prep_kernel's, plain form): c_k = (sel_k - w (off + k)) / 2pi
+// + 1/2, offk = off + k exactly; NaN for a 0 / NaN input.  Long calls compute it where it is
+// used instead of storing a row of it.
+__device__ __forceinline__ double pll_c(float x, double w, double offk) {
+  const double cc = (x > 0.f ? 0.0 : kPi) - w * offk;
+  const double cv = fma(cc, kInv2Pi, 0.5);
+  return (x > 0.f || x < 0.f) ? cv : __builtin_nan("");
 }
 
 // Steps per group: the next group's inputs are loaded (registers) while this one runs,
@@ -188,6 +216,8 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
     st[3] = sin(arg);
     st[4] = cos(arg * cfg.scale + cfg.adj);
     st[5] = off + (double)n;
+    stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
+    stat_add(P.stats, SDR_PLL_ST_SEQUENTIAL, 1);
   }
 }
 
@@ -374,6 +404,8 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
       st[3] = sin(arg);
       st[4] = cos(arg * cfg.scale + cfg.adj);
       st[5] = off + (double)n;
+      stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
+      stat_add(P.stats, SDR_PLL_ST_SEQUENTIAL, 1);
     }
   }
 }
@@ -407,28 +439,69 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 // never read it, and the prep kernel rewrites it every call).
 constexpr int SPEC_W = 256;          // warm-up samples before each chunk
 constexpr int SPEC_IT = 3;           // solve / check rounds before the sequential kernel takes over
-constexpr int SPEC_NMAX = 16384 + 1; // samples per call (the constants of steps 1.. in LDS: 128 KiB)
+constexpr int SPEC_NMAX = SDR_PLL_BLOCK_MAX; // samples per call (the constants of steps 1.. in LDS: 128 KiB)
+static_assert(SPEC_NMAX == 16384 + 1, "LDS sizing");
+
+// ---- long calls: pseudo-block bookkeeping (device scratch P.work) --------------------
+// Per recurrence r = job * nstreams + stream: a header (the chain's position and the exact
+// state at it), then one LongBlk per pseudo-block: its start guess g (warm-up), its chained
+// start x (when re-solved), the end state e of its latest solve, the 2 pi shift the chain
+// found for it, and its status.  States are in fmPll's 6-double order.
+enum { LB_NEED_G = 0, LB_DONE_G = 1, LB_NEED_X = 2, LB_DONE_X = 3, LB_ACCEPTED = 4 };
+constexpr int SOLVER_SEQ = 3;        // solver codes: 0..2 = parallel solve round, 3 = sequential
+// u: the start (phaseEst, integrator) the current solution (theta row, e) was solved from.
+struct LongBlk { double g[6]; double x[6]; double e[6]; double u[2]; double shift; int status; int solver; };
+struct LongHdr { double sp, si; int pos; int pad; double pad2; };
+static_assert(sizeof(LongBlk) == 176 && sizeof(LongHdr) == 32, "long-call scratch layout");
+__device__ __forceinline__ LongHdr* long_hdr(const PllJobs& P, int r) { return static_cast<LongHdr*>(P.work) + r; }
+__device__ __forceinline__ LongBlk* long_blk(const PllJobs& P, int r, int b) {
+  return reinterpret_cast<LongBlk*>(static_cast<char*>(P.work) + (int64_t)P.njobs * P.nstreams * sizeof(LongHdr)) +
+         (int64_t)r * P.lg.nb + b;
+}
+__device__ __forceinline__ int64_t long_len(const PllJobs& P, int b) {
+  return b < P.lg.nb - 1 ? P.lg.pb : P.n - (int64_t)(P.lg.nb - 1) * P.lg.pb;
+}
 
 // SPEC_T threads (chunks) per recurrence: 256 (one wave per SIMD) up to 10 240 samples, 512
 // beyond (the warm-up is the same length either way; 512 halves the chunks, and a second
-// wave per SIMD then pays: c5 blocks 56 -> ~50 us, c4 blocks slower)
-template <int SPEC_T>
+// wave per SIMD then pays: c5 blocks 56 -> ~50 us, c4 blocks slower).
+// LONG: one workgroup per pseudo-block of a long call, from its start guess (status
+// LB_NEED_G) or its chained start (LB_NEED_X); the end state goes to the block's record and
+// the call's own state, trigOffset slot and NCO[0] are left to the long-call kernels.
+template <int SPEC_T, bool LONG>
 __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
 #pragma clang fp contract(off)
   __shared__ double cl[SPEC_NMAX - 1];         // c_k of steps 1 .. n-1 (plain form)
   __shared__ int8_t mrel[SPEC_NMAX - 1];       // m_k - floor(c_k) + jb, jb = floor(phaseEst_1 / 2pi)
   __shared__ d2v yb[SPEC_T];
   __shared__ double x1s[2];
-  const int q = blockIdx.x / P.nstreams;
-  const int s = blockIdx.x - q * P.nstreams;
   const int tid = threadIdx.x;
+  int q, s, status = 0;
+  int64_t n, base = 0;
+  LongBlk* LB = nullptr;
+  if constexpr (LONG) {
+    const int nb = P.lg.nb;
+    const int r = blockIdx.x / nb;
+    const int b = blockIdx.x - r * nb;
+    q = r / P.nstreams;
+    s = r - q * P.nstreams;
+    LB = long_blk(P, r, b);
+    status = LB->status;
+    if (status != LB_NEED_G && status != LB_NEED_X) return;
+    base = (int64_t)b * P.lg.pb;
+    n = long_len(P, b);
+  } else {
+    q = blockIdx.x / P.nstreams;
+    s = blockIdx.x - q * P.nstreams;
+    n = P.n;
+  }
   const PllJob& J = P.j[q];
-  const int64_t n = P.n;
-  const float* in = J.in + (int64_t)s * J.in_stride;
-  double* th = J.theta + (int64_t)s * J.th_stride;
-  double* cr = J.cbuf + (int64_t)s * J.c_stride;
+  const float* in = J.in + (int64_t)s * J.in_stride + base;
+  double* th = J.theta + (int64_t)s * J.th_stride + base;
+  double* cr = J.cbuf + (int64_t)s * J.c_stride + base;
   const PllCfg cfg = J.cfg;
-  double* st = J.state + (int64_t)s * 6;
+  double* st = LONG ? (status == LB_NEED_G ? LB->g : LB->x) : J.state + (int64_t)s * 6;
+  double* st_out = LONG ? LB->e : st;
   const double off = st[5];
   const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
   const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
@@ -460,7 +533,12 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
   const double p1 = x1s[0], v1 = x1s[1];
   const int64_t N = n - 1;                       // steps 1 .. n-1
   // every step reads its constant several times: stage them (plain form) in LDS
-  for (int64_t k = tid; k < N; k += SPEC_T) cl[k] = cplain(k + 1);
+  if constexpr (LONG) {
+    const double w1 = 2.0 * kPi * (cfg.freq / cfg.fs);
+    for (int64_t k = tid; k < N; k += SPEC_T) cl[k] = pll_c(in[k + 1], w1, off + (double)(k + 1));
+  } else {
+    for (int64_t k = tid; k < N; k += SPEC_T) cl[k] = cplain(k + 1);
+  }
   __syncthreads();
   // the integer part relative to floor(c_k) is floor(-phaseEst/2pi + frac(c_k)): near -jb
   // within a block, so it fits a byte once jb is taken off (a drifting phase estimate moves jb)
@@ -470,15 +548,64 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
   const int TE = (int)((N + L - 1) / L);         // chunks in use; chunks 0 .. TE-2 are full
   const int64_t k0 = 1 + (int64_t)tid * L;
   const int64_t k1 = tid < TE ? min<int64_t>(k0 + L, n) : k0;
+  // 0. where the locked phase estimate goes within the block, measured from the input: a
+  // locked loop keeps its angle th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's
+  // phase, so z_j = sum over chunk j of x_k exp(-i w (off + k)) ~ (A/2) exp(i phaseEst) (+ an
+  // image term at twice the carrier, averaged down by summing 5 chunks).  The chunk phases,
+  // unwrapped by a scan of their differences (a chunk drifts by ~0.02 rad at a 30 Hz carrier
+  // offset), give D_j = phaseEst(chunk j) - phaseEst(chunk 0), bias-free.  (A 2 Hz pilot offset
+  // is a 12 Hz RDS carrier offset, 4.8 rad per 15 360-sample block: from the block's first
+  // state alone, the RDS loop's 256-step warm-ups (contraction ~0.7) cannot catch it up.
+  // Extrapolating by integ does worse: integ swings with the loop's own oscillation.)
+  {
+    float zr = 0.f, zi = 0.f;
+    for (int64_t k = k0; k < k1; ++k) {
+      const double c = cl[k - 1];
+      const float xv = in[k];
+      if (!(c == c)) continue;                   // a 0 / NaN input (rejected below anyway)
+      // w (off + k) mod 2 pi = 2 pi fract(sel/2pi + 1/2 - c_k), sel/2pi = 0 (x > 0) or 1/2
+      const float a = (float)(k2Pi * __builtin_amdgcn_fract((xv > 0.f ? 0.5 : 1.0) - c));
+      float sa, ca;
+      __sincosf(a, &sa, &ca);
+      zr = fmaf(xv, ca, zr);
+      zi = fmaf(-xv, sa, zi);
+    }
+    yb[tid] = d2v{(double)zr, (double)zi};
+    __syncthreads();
+    double sr = 0.0, si = 0.0;
+    for (int o = -2; o <= 2; ++o) {
+      const int j = tid + o;
+      if (j >= 0 && j < TE) { sr += yb[j].x; si += yb[j].y; }
+    }
+    const double ang = atan2(si, sr);
+    __syncthreads();
+    yb[tid].x = ang;
+    __syncthreads();
+    double d = 0.0;
+    if (tid >= 1 && tid < TE) {
+      d = ang - yb[tid - 1].x;
+      d -= k2Pi * rint(d * kInv2Pi);
+    }
+    for (int o = 1; o < SPEC_T; o <<= 1) {     // inclusive prefix sum of the differences
+      __syncthreads();
+      yb[tid].y = d;
+      __syncthreads();
+      if (tid >= o) d += yb[tid - o].y;
+    }
+    __syncthreads();
+    yb[tid].x = d;                               // D_j
+    __syncthreads();
+  }
   // 1. guess
   bool bad = false;
   {
-    // from the block's first state: a locked estimate moves little within a block (a 3 Hz
-    // pilot offset: 1.2 rad over 15 360 samples), and 256 steps of the loop shrink that
-    // ~30-fold.  (Extrapolating by integ does worse: integ swings with the loop's own
-    // oscillation, and a 64-step mean of it mispredicts a block's drift by up to 4 rad.)
+    // the true step from a seed on the measured drift: phaseEst ~ p1 + D at the warm-up's
+    // start, integ ~ the measured drift per step; 256 steps of the loop then pull the guess
+    // onto the trajectory
     const int64_t kw = max<int64_t>(1, k0 - SPEC_W);
-    double p = p1, V = v1;
+    const int jw = (int)((kw - 1) / L);
+    double p = p1 + yb[jw].x, V = v1;
+    if (k0 - kw >= 64 && tid < TE) V = (yb[tid].x - yb[jw].x) / (double)(k0 - kw) - kD;
 #pragma unroll 8
     for (int64_t k = kw; k < k0 && tid < TE; ++k) {
       const double t = fma(-kInv2Pi, p, cl[k - 1]);
@@ -556,31 +683,507 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
       th[k] = thval(p, k);
     }
     const int nmiss = __syncthreads_count(miss);
-    if (P.spec_dbg && tid == 0) printf("pll_spec q%d s%d n%ld T%d L%d TE%d round %d: %d chunks missed\n", q, s, (long)n, SPEC_T, L, TE, round, nmiss);
+#ifdef SDR_PLL_SPEC_DEBUG   // A/B builds only (make ... CXXFLAGS+=-DSDR_PLL_SPEC_DEBUG): never in libsdr.so
+    if (tid == 0) printf("pll_spec q%d s%d n%ld T%d L%d TE%d round %d: %d chunks missed\n", q, s, (long)n, SPEC_T, L, TE, round, nmiss);
+#endif
     if (nmiss == 0) {
       // done: the caller-visible results exactly as the loop kernels leave them
       if (tid == 0) {
         th[0] = thval(p1, 0);
-        J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];
-        if (J.nco_q)
-          J.nco_q[(int64_t)s * J.out_stride] =
-              (float)((off > 0.0) ? sin((w * off + st[1]) * cfg.scale + cfg.adj) : 0.0);
+        if constexpr (!LONG) {
+          J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];
+          if (J.nco_q)
+            J.nco_q[(int64_t)s * J.out_stride] =
+                (float)((off > 0.0) ? sin((w * off + st[1]) * cfg.scale + cfg.adj) : 0.0);
+        }
       }
       __syncthreads();                           // st[1], st[4] read before the last chunk writes st
       if (tid == TE - 1) {
         const double arg = w * ((off + (double)(n - 1)) + 1.0) + p;
-        th[n] = off;
-        st[0] = V + kD;
-        st[1] = p;
-        st[2] = cos(arg);
-        st[3] = sin(arg);
-        st[4] = cos(arg * cfg.scale + cfg.adj);
-        st[5] = off + (double)n;
+        if constexpr (!LONG) th[n] = off;
+        st_out[0] = V + kD;
+        st_out[1] = p;
+        st_out[2] = cos(arg);
+        st_out[3] = sin(arg);
+        st_out[4] = cos(arg * cfg.scale + cfg.adj);
+        st_out[5] = off + (double)n;
       }
-      if (tid == 0) cr[0] = __builtin_inf();      // the loop kernel skips this recurrence
+      if (tid == 0) {
+        if constexpr (LONG) {                    // counted when the chain accepts the block
+          LB->u[0] = st[0];
+          LB->u[1] = st[1];
+          LB->status = status + 1;               // LB_NEED_G -> LB_DONE_G, LB_NEED_X -> LB_DONE_X
+          LB->solver = round;
+        } else {
+          cr[0] = __builtin_inf();               // the loop kernel skips this recurrence
+          stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
+          stat_add(P.stats, SDR_PLL_ST_SPEC_R0 + round, 1);
+        }
+      }
       return;
     }
   }
+}
+
+// ================================================================================
+// Long calls (n > SDR_PLL_BLOCK_MAX): a device-resident span of many blocks is one recurrence
+// of n steps, cut into nb pseudo-blocks of pb <= 16 384 steps so that every pseudo-block is one
+// pll_spec_kernel workgroup and the whole span fills the GPU.  A pseudo-block's start state is
+// the previous one's end state, unknown until that one is solved, so:
+//   1. pll_warm_kernel: each pseudo-block's start is GUESSED by running the loop's true step
+//      over the `warm` samples before it, from the span's start frequency (one wave each).
+//      The loop contracts errors by sqrt(1 - Kp) per step, and its dynamics are invariant
+//      under phaseEst -> phaseEst + 2 pi, so the guess converges to the true state up to a
+//      whole number of turns.
+//   2. pll_spec_kernel<..., LONG> (+ pll_long_seq_kernel for what it cannot complete): every
+//      pseudo-block solved from its guess.
+//   3. pll_long_chain_kernel (one wave per recurrence, serial over the pseudo-blocks, all in
+//      f64 scalars): from the exact state at the chain's position, the 2 pi shift n between
+//      the exact start and the guess is taken out, and the remaining start error (dp, dV)
+//      bounds the phase deviation of the block's solution by err = c1 |dp| + c2 |dV| (c1, c2:
+//      the largest phase excursion the loop's linear form makes from a unit start error).
+//        err <= 1e-9 rad: accepted -- its phases + 2 pi n are the recurrence's (to a deviation
+//                         below the reference's own rounding of its ~1e6 rad angle), and its
+//                         end state + 2 pi n is the next block's exact start;
+//        err <= 0.3 rad:  re-solve it from the exact start (step 2 again, LB_NEED_X); its end
+//                         state follows by the linear form, e + 2 pi n + Phi (dp, dV) (Phi =
+//                         the loop matrix to the block's length: the next start, provisional
+//                         until the re-solve confirms it);
+//        else:            re-solve it, and stop the chain there this round.
+//      Blocks are accepted only while the chain is exact; provisional ones are checked again.
+//   Steps 2-3 run SPEC_ROUNDS times; pll_long_tail_kernel then runs whatever is left
+//   sequentially from the chain's exact position (never on a locked signal: counted).
+//   The NCO kernel adds 2 pi n to an accepted guessed block's phases.
+constexpr double LONG_ACCEPT = 1e-9;   // rad: accepted deviation bound
+constexpr double LONG_LINEAR = 0.3;    // rad: deviation bound under which the integers m_k are kept
+constexpr int LONG_ROUNDS = 4;
+
+// 1. Start guesses: one lane per pseudo-block (WARM_LPW lanes of one recurrence per wave,
+// all with the same number of steps), each running the loop's true step over its `warm`
+// constants, fetched 16 at a time two groups ahead of use.
+constexpr int WARM_LPW = 16;
+constexpr int WARM_G = 16;
+constexpr int WARM_Z = 256;       // samples of the phase measurement that seeds a warm-up
+__global__ __launch_bounds__(64) void pll_warm_kernel(PllJobs P) {
+#pragma clang fp contract(off)
+  const int nb = P.lg.nb;
+  const int wpr = (nb + WARM_LPW - 1) / WARM_LPW;
+  const int r = blockIdx.x / wpr;
+  const int b = (blockIdx.x - r * wpr) * WARM_LPW + (int)threadIdx.x;
+  if ((int)threadIdx.x >= WARM_LPW || b >= nb) return;
+  const int q = r / P.nstreams, s = r - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const PllCfg cfg = J.cfg;
+  const double* st = J.state + (int64_t)s * 6;
+  LongBlk* B = long_blk(P, r, b);
+  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  const double off0 = st[5];
+  const int64_t pb = P.lg.pb;
+  B->shift = 0.0;
+  B->status = LB_NEED_G;
+  B->solver = -1;
+  if (b == 0) {                                  // the span's own start: exact
+    for (int i = 0; i < 6; ++i) B->g[i] = st[i];
+    LongHdr* H = long_hdr(P, r);
+    H->sp = st[1];
+    H->si = st[0];
+    H->pos = 0;
+    J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];       // ncoOut[0] (as the per-call kernels)
+    if (J.nco_q)
+      J.nco_q[(int64_t)s * J.out_stride] =
+          (float)((off0 > 0.0) ? sin((w * off0 + st[1]) * cfg.scale + cfg.adj) : 0.0);
+    J.theta[(int64_t)s * J.th_stride + P.n] = off0;         // the NCO kernel's trigOffset
+    return;
+  }
+  const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
+  const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
+  const int64_t kend = (int64_t)b * pb;
+  const int64_t k0 = max<int64_t>(1, kend - P.lg.warm[q]);
+  const float* xin = J.in + (int64_t)s * J.in_stride + k0;
+  const int64_t nst = kend - k0;
+  // seed: the phase the loop locks to, measured from the WARM_Z samples before the warm-up (a
+  // locked loop keeps th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's phase, so
+  // arg sum x_k exp(-i w (off + k)) ~ phaseEst, modulo 2 pi: only that has to converge; the
+  // chain finds the turns).  The integrator from the span's start.  (Extrapolating the start
+  // phase by the integrator does not work: a locked loop balances its integrator with a
+  // static phase error, so the estimate does not move by it -- 20 rad off across a span.)
+  double p, V = st[0] - kD;
+  {
+    double zr = 0.0, zi = 0.0;
+    const float* xz = J.in + (int64_t)s * J.in_stride;
+    for (int64_t k = max<int64_t>(1, k0 - WARM_Z); k < k0; ++k) {
+      const double c = pll_c(xz[k], w, off0 + (double)k);
+      if (!(c == c)) continue;
+      const float a = (float)(k2Pi * __builtin_amdgcn_fract((xz[k] > 0.f ? 0.5 : 1.0) - c));
+      float sa, ca;
+      __sincosf(a, &sa, &ca);
+      zr += (double)(xz[k] * ca);
+      zi -= (double)(xz[k] * sa);
+    }
+    p = (zr != 0.0 || zi != 0.0) ? atan2(zi, zr) : st[1];
+  }
+  const int64_t ng = (nst + WARM_G - 1) / WARM_G;
+  auto ld = [&](double (&v)[WARM_G], int64_t g) {
+#pragma unroll
+    for (int i = 0; i < WARM_G; ++i) {
+      const int64_t k = g * WARM_G + i;
+      v[i] = (g < ng && k < nst) ? pll_c(xin[k], w, off0 + (double)(k0 + k)) : __builtin_nan("");
+    }
+  };
+  double c0[WARM_G], c1[WARM_G], c2[WARM_G];
+  ld(c0, 0);
+  ld(c1, 1);
+  for (int64_t g = 0; g < ng; ++g) {
+    ld(c2, g + 2);
+#pragma unroll
+    for (int i = 0; i < WARM_G; ++i) {
+      const double c = c0[i];
+      if (c == c) {                              // NaN: past the end, or a 0 / NaN input (skipped)
+        const double t = fma(-kInv2Pi, p, c);
+        const double f = __builtin_amdgcn_fract(t);
+        const double S = p + V;
+        V = fma(kA, f, V - kB);
+        p = fma(kC, f, S);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WARM_G; ++i) { c0[i] = c1[i]; c1[i] = c2[i]; }
+  }
+  const double offp = off0 + (double)((int64_t)(b - 1) * pb);      // the previous block's trigOffset
+  const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + p;
+  B->g[0] = V + kD;
+  B->g[1] = p;
+  B->g[2] = cos(arg);
+  B->g[3] = sin(arg);
+  B->g[4] = 0.0;
+  B->g[5] = off0 + (double)kend;
+}
+
+// The reference's recurrence run sequentially from state st over n steps (the general form:
+// literal first step from the state's (fI, fQ); 0 / NaN inputs by atan2 on the products; the
+// rest by the constants pll_c).  Phases into th[0..n), the end state into so.
+__device__ void seq_run(const PllCfg& cfg, const float* in, double* th, int64_t n, const double* st, double* so) {
+#pragma clang fp contract(off)
+  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  double integ = st[0], phase = st[1];
+  const double off = st[5];
+  // inputs 16 at a time, one group ahead (a load per step would wait out the memory latency)
+  constexpr int G = 16;
+  float xa[G], xn[G];
+  auto ld = [&](float (&v)[G], int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) v[i] = k0 + i < n ? in[k0 + i] : 0.f;
+  };
+  ld(xa, 0);
+  for (int64_t k0 = 0; k0 < n; k0 += G) {
+    ld(xn, k0 + G);
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int64_t k = k0 + i;
+      if (k >= n) break;
+      const float xf = xa[i];
+      const double xv = (double)xf;
+      double e;
+      if (k == 0 || !(xv > 0.0 || xv < 0.0)) {
+        double fI = st[2], fQ = st[3];
+        if (k > 0) {
+          const double arg = w * ((off + (double)(k - 1)) + 1.0) + phase;
+          fI = cos(arg);
+          fQ = sin(arg);
+        }
+        e = atan2(xv * (-fQ), xv * fI);
+      } else {
+        const double t = fma(-kInv2Pi, phase, pll_c(xf, w, off + (double)k));
+        e = k2Pi * (__builtin_amdgcn_fract(t) - 0.5);
+      }
+      integ = integ + cfg.ki * e;
+      phase = phase + cfg.kp * e + integ;
+      th[k] = phase;
+    }
+#pragma unroll
+    for (int i = 0; i < G; ++i) xa[i] = xn[i];
+  }
+  const double arg = w * ((off + (double)(n - 1)) + 1.0) + phase;
+  so[0] = integ;
+  so[1] = phase;
+  so[2] = cos(arg);
+  so[3] = sin(arg);
+  so[4] = cos(arg * cfg.scale + cfg.adj);
+  so[5] = off + (double)n;
+}
+
+// 2b. Pseudo-blocks pll_spec_kernel did not complete (a 0 / NaN input, no convergence), from
+// the same start: one lane each.
+__global__ __launch_bounds__(64) void pll_long_seq_kernel(PllJobs P) {
+  const int nb = P.lg.nb;
+  const int wpr = (nb + 63) / 64;
+  const int r = blockIdx.x / wpr;
+  const int b = (blockIdx.x - r * wpr) * 64 + threadIdx.x;
+  if (b >= nb) return;
+  const int q = r / P.nstreams, s = r - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  LongBlk* B = long_blk(P, r, b);
+  const int status = B->status;
+  if (status != LB_NEED_G && status != LB_NEED_X) return;
+  const int64_t base = (int64_t)b * P.lg.pb;
+  seq_run(J.cfg, J.in + (int64_t)s * J.in_stride + base, J.theta + (int64_t)s * J.th_stride + base, long_len(P, b),
+          status == LB_NEED_G ? B->g : B->x, B->e);
+  B->u[0] = (status == LB_NEED_G ? B->g : B->x)[0];
+  B->u[1] = (status == LB_NEED_G ? B->g : B->x)[1];
+  B->status = status + 1;
+  B->solver = SOLVER_SEQ;
+}
+
+// 2a. Re-solving a block from its chained start x, when its current solution started from u
+// within the linear bound: the true phases are the current ones + 2 pi n + the loop's linear
+// response to the start error d = (x - u) - 2 pi n, i.e. theta_k += 2 pi n + (A^(k+1) d)_phase --
+// exactly the recurrence's as long as no step's integer m_k changes.  That is checked at every
+// step: the current fract(t_k) moved by the correction of the phase before it must stay inside
+// (0, 1) (the literal first step: its atan2 angle moved by the correction stays inside (-pi,
+// pi)).  One workgroup per pseudo-block, steps in contiguous runs per thread (A^k by
+// squaring, then one step of A per sample).  A block that fails the check keeps LB_NEED_X and
+// is re-solved by pll_spec_kernel in the same round.
+constexpr int FIX_T = 256;
+__global__ __launch_bounds__(FIX_T) void pll_long_fix_kernel(PllJobs P) {
+#pragma clang fp contract(off)
+  const int nb = P.lg.nb;
+  const int r = blockIdx.x / nb;
+  const int b = blockIdx.x - r * nb;
+  LongBlk* LB = long_blk(P, r, b);
+  if (LB->status != LB_NEED_X || LB->solver < 0) return;
+  const int q = r / P.nstreams, s = r - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const PllCfg cfg = J.cfg;
+  const int tid = threadIdx.x;
+  const double d0 = LB->x[1] - LB->u[1];
+  const double nsh = rint(d0 * kInv2Pi);
+  const double dp = fma(-nsh, kP2, fma(-nsh, kP1, d0));
+  const double dv = LB->x[0] - LB->u[0];
+  if (!(P.lg.c1[q] * fabs(dp) + P.lg.c2[q] * fabs(dv) <= LONG_LINEAR)) return;
+  const int64_t n = long_len(P, b);
+  const int64_t base = (int64_t)b * P.lg.pb;
+  double* th = J.theta + (int64_t)s * J.th_stride + base;
+  const float* xin = J.in + (int64_t)s * J.in_stride + base;
+  const double wf = 2.0 * kPi * (cfg.freq / cfg.fs);
+  const double offb = LB->x[5];
+  const double a00 = 1.0 - (k2Pi * (cfg.kp + cfg.ki)) * kInv2Pi, a10 = -(k2Pi * cfg.ki) * kInv2Pi;
+  const int64_t per = (n + FIX_T - 1) / FIX_T;
+  const int64_t ka = min<int64_t>((int64_t)tid * per, n), kb = min<int64_t>(ka + per, n);
+  // A^ka d: the correction of the state before step ka
+  double vp = dp, vv = dv;
+  {
+    double M00 = a00, M01 = 1.0, M10 = a10, M11 = 1.0;
+    for (int64_t e = ka; e > 0; e >>= 1) {
+      if (e & 1) {
+        const double np = M00 * vp + M01 * vv, nv = M10 * vp + M11 * vv;
+        vp = np; vv = nv;
+      }
+      const double n00 = M00 * M00 + M01 * M10, n01 = M00 * M01 + M01 * M11;
+      const double n10 = M10 * M00 + M11 * M10, n11 = M10 * M01 + M11 * M11;
+      M00 = n00; M01 = n01; M10 = n10; M11 = n11;
+    }
+  }
+  // the phase before step ka as solved (read before any thread rewrites the row)
+  double prev = ka > 0 && ka < kb ? th[ka - 1] : 0.0;
+  __syncthreads();
+  bool bad = false;
+  const double tol = 1e-6;
+  for (int64_t k = ka; k < kb; ++k) {
+    if (k == 0) {                                // the literal step: atan2 of the start's (fI, fQ)
+      const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+      const double offp = LB->x[5] - (double)P.lg.pb;
+      const double arg = w * ((offp + (double)(P.lg.pb - 1)) + 1.0) + LB->u[1];
+      const double xv = (double)J.in[(int64_t)s * J.in_stride + base];
+      const double e = atan2(xv * (-sin(arg)), xv * cos(arg));
+      bad |= !(fabs(e - vp) < kPi - tol);
+    } else {
+      const double t = fma(-kInv2Pi, prev, pll_c(xin[k], wf, offb + (double)k));
+      const double f = t - floor(t) - vp * kInv2Pi;
+      bad |= !(f > tol && f < 1.0 - tol);
+    }
+    const double np = a00 * vp + vv, nv = a10 * vp + vv;
+    vp = np; vv = nv;
+    prev = th[k];
+    th[k] = fma(nsh, kP1, fma(nsh, kP2, prev)) + vp;
+  }
+  if (__syncthreads_or(bad)) return;             // the spec kernel re-solves it from x
+  if (tid == 0) {
+    const double* ph = (b == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
+    LB->e[1] = fma(nsh, kP1, fma(nsh, kP2, LB->e[1])) + (ph[0] * dp + ph[1] * dv);
+    LB->e[0] = LB->e[0] + (ph[2] * dp + ph[3] * dv);
+    LB->u[0] = LB->x[0];
+    LB->u[1] = LB->x[1];
+    LB->status = LB_DONE_X;
+  }
+}
+
+// 3. The chain: one wave per recurrence.  A window of pseudo-block records is staged in LDS
+// by all lanes; the walk over it is serial (every lane runs it alike; lane 0 publishes); the
+// decisions are written back by all lanes.
+constexpr int CHAIN_WIN = 256;
+__global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round) {
+#pragma clang fp contract(off)
+  __shared__ double gp[CHAIN_WIN], gi[CHAIN_WIN], xp[CHAIN_WIN], xi[CHAIN_WIN], ep[CHAIN_WIN], ei[CHAIN_WIN];
+  __shared__ double osp[CHAIN_WIN], osi[CHAIN_WIN], osh[CHAIN_WIN], oerr[CHAIN_WIN];
+  __shared__ int stt[CHAIN_WIN], act[CHAIN_WIN];
+  const int r = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int nb = P.lg.nb;
+  LongHdr* H = long_hdr(P, r);
+  const int pos0 = H->pos;
+  if (pos0 >= nb) return;
+  const int q = r / P.nstreams, s = r - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const PllCfg cfg = J.cfg;
+  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  const double c1 = P.lg.c1[q], c2 = P.lg.c2[q];
+  double* st = J.state + (int64_t)s * 6;
+  const double off0 = st[5];
+  const int64_t pb = P.lg.pb;
+  double Sp = H->sp, Si = H->si;       // the walk's state: exact while `exact`
+  double Xp = Sp, Xi = Si;             // the exact state at the new position
+  int pos = pos0;
+  bool exact = true, stop = false;
+  for (int w0 = pos0; w0 < nb && !stop; w0 += CHAIN_WIN) {
+    const int nw = min(CHAIN_WIN, nb - w0);
+    for (int j = lane; j < nw; j += 64) {
+      const LongBlk* B = long_blk(P, r, w0 + j);
+      gp[j] = B->g[1]; gi[j] = B->g[0];
+      xp[j] = B->x[1]; xi[j] = B->x[0];
+      ep[j] = B->e[1]; ei[j] = B->e[0];
+      stt[j] = B->status;
+      act[j] = 0;
+    }
+    __syncthreads();
+    int j = 0;
+    for (; j < nw; ++j) {
+      const int sj = stt[j];
+      if (sj != LB_DONE_G && sj != LB_DONE_X) { stop = true; break; }   // not solved this round
+      const bool fromg = sj == LB_DONE_G;
+      const double d = Sp - (fromg ? gp[j] : xp[j]);
+      const double nsh = fromg ? rint(d * kInv2Pi) : 0.0;
+      const double dp = fma(-nsh, kP2, fma(-nsh, kP1, d));             // d - 2 pi n
+      const double dv = Si - (fromg ? gi[j] : xi[j]);
+      const double err = c1 * fabs(dp) + c2 * fabs(dv);
+      oerr[j] = err;
+      osh[j] = nsh;
+      const double eps = fma(nsh, kP1, fma(nsh, kP2, ep[j]));           // e + 2 pi n
+      if (err <= LONG_ACCEPT) {
+        Sp = eps;
+        Si = ei[j];
+        if (exact) {
+          act[j] = 1;
+          pos = w0 + j + 1;
+          Xp = Sp;
+          Xi = Si;
+        }
+        continue;
+      }
+      act[j] = 2;                                                      // re-solve from (Sp, Si)
+      osp[j] = Sp;
+      osi[j] = Si;
+      exact = false;
+      if (!(err <= LONG_LINEAR)) {                                     // (a NaN also stops here)
+#ifdef SDR_PLL_LONG_DEBUG
+        if (lane == 0)
+          printf("chain r%d b%d/%d status %d: err %.3e dp %.3e dv %.3e n %.0f (S %.6f %.3e, guess %.6f %.3e)\n", r,
+                 w0 + j, nb, sj, err, dp, dv, nsh, Sp, Si, fromg ? gp[j] : xp[j], fromg ? gi[j] : xi[j]);
+#endif
+        act[j] = 3;
+        ++j;
+        stop = true;
+        break;
+      }
+      const double* ph = (w0 + j == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
+      Sp = eps + (ph[0] * dp + ph[1] * dv);
+      Si = ei[j] + (ph[2] * dp + ph[3] * dv);
+    }
+    __syncthreads();
+    for (int k = lane; k < j; k += 64) {
+      const int bi = w0 + k;
+      LongBlk* B = long_blk(P, r, bi);
+      if (act[k] == 1) {
+        B->status = LB_ACCEPTED;
+        B->shift = osh[k];
+        const int sv = B->solver;
+        stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
+        stat_add(P.stats, sv == SOLVER_SEQ ? SDR_PLL_ST_SEQUENTIAL : SDR_PLL_ST_SPEC_R0 + sv, 1);
+        stat_add(P.stats, stt[k] == LB_DONE_G ? SDR_PLL_ST_LONG_GUESSED : SDR_PLL_ST_LONG_CHAINED, 1);
+        stat_max(P.stats, SDR_PLL_ST_LONG_MAXGAP, oerr[k]);
+      } else if (act[k] >= 2) {
+        if (act[k] == 3) stat_add(P.stats, SDR_PLL_ST_LONG_STOPS, 1);
+        B->u[0] = stt[k] == LB_DONE_G ? gi[k] : xi[k];                 // the start of the current solution
+        B->u[1] = stt[k] == LB_DONE_G ? gp[k] : xp[k];
+        const double offp = off0 + (double)((int64_t)(bi - 1) * pb);
+        const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + osp[k];
+        B->x[0] = osi[k];
+        B->x[1] = osp[k];
+        B->x[2] = cos(arg);
+        B->x[3] = sin(arg);
+        B->x[4] = 0.0;
+        B->x[5] = off0 + (double)((int64_t)bi * pb);
+        B->shift = 0.0;
+        B->status = LB_NEED_X;
+      }
+    }
+    __syncthreads();
+  }
+#ifdef SDR_PLL_LONG_DEBUG
+  if (lane == 0) printf("chain r%d round %d: position %d -> %d of %d\n", r, round, pos0, pos, nb);
+#endif
+  if (lane == 0) {
+    H->pos = pos;
+    H->sp = Xp;
+    H->si = Xi;
+    if (pos == nb) {                                                   // the call's state
+      const double offl = off0 + (double)((int64_t)(nb - 1) * pb);
+      const double arg = w * ((offl + (double)(long_len(P, nb - 1) - 1)) + 1.0) + Xp;
+      st[0] = Xi;
+      st[1] = Xp;
+      st[2] = cos(arg);
+      st[3] = sin(arg);
+      st[4] = cos(arg * cfg.scale + cfg.adj);
+      st[5] = off0 + (double)P.n;
+    }
+  }
+  (void)round;
+}
+
+// 4. Whatever the rounds left: sequential from the chain's exact position to the end.
+__global__ __launch_bounds__(64) void pll_long_tail_kernel(PllJobs P) {
+#pragma clang fp contract(off)
+  const int r = blockIdx.x;
+  const int nb = P.lg.nb;
+  LongHdr* H = long_hdr(P, r);
+  const int pos = H->pos;
+  if (pos >= nb) return;
+  const int q = r / P.nstreams, s = r - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const PllCfg cfg = J.cfg;
+  double* st = J.state + (int64_t)s * 6;
+  for (int b = pos + threadIdx.x; b < nb; b += 64) long_blk(P, r, b)->shift = 0.0;
+  if (threadIdx.x != 0) return;
+  const int64_t pb = P.lg.pb;
+  const int64_t base = (int64_t)pos * pb;
+  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  const double off0 = st[5];
+  double s0[6];
+  if (pos == 0) {
+    for (int i = 0; i < 6; ++i) s0[i] = st[i];
+  } else {
+    const double offp = off0 + (double)(base - pb);
+    const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + H->sp;
+    s0[0] = H->si; s0[1] = H->sp; s0[2] = cos(arg); s0[3] = sin(arg); s0[4] = 0.0; s0[5] = off0 + (double)base;
+  }
+  double so[6];
+  seq_run(cfg, J.in + (int64_t)s * J.in_stride + base, J.theta + (int64_t)s * J.th_stride + base, P.n - base, s0,
+          so);
+  for (int i = 0; i < 5; ++i) st[i] = so[i];
+  st[5] = off0 + (double)P.n;
+  H->pos = nb;
+  stat_add(P.stats, SDR_PLL_ST_RECURRENCES, (unsigned long long)(nb - pos));
+  stat_add(P.stats, SDR_PLL_ST_SEQUENTIAL, (unsigned long long)(nb - pos));
+  stat_add(P.stats, SDR_PLL_ST_LONG_TAIL, (unsigned long long)(nb - pos));
 }
 
 // Per-sample constants of the loop (parallel): c_k = (sel_k - w (off + k)) / 2pi + 1/2 and one flag per
@@ -635,6 +1238,10 @@ __global__ void nco_jobs_kernel(PllJobs P) {
     const double i = (double)(k % PG);
     p = p - (kPi * J.cfg.ki) * ((i + 1.0) * i * 0.5);
   }
+  if (P.n > SPEC_NMAX) {                                // long call: the chain's 2 pi shift of the block
+    const double n2 = long_blk(P, q * P.nstreams + s, (int)(k / P.lg.pb))->shift;
+    p = fma(n2, kP1, fma(n2, kP2, p));
+  }
   const double th = w * ((off + (double)k) + 1.0) + p;
   const double a = th * J.cfg.scale + J.cfg.adj;
   double sv, cv;
@@ -672,12 +1279,106 @@ hipError_t pll_check(const PllJobs& P, bool* vec) {
 }
 }  // namespace
 
+namespace {
+// ---- long calls: host-side setup ---------------------------------------------------
+bool pll_long(const PllJobs& P) { return P.n > SPEC_NMAX; }
+
+void long_geom(int64_t n, int64_t* pb, int* nb) {
+  const int64_t k = (n + 16383) / 16384;          // pseudo-blocks of <= 16 384 steps
+  *nb = (int)k;
+  *pb = (n + k - 1) / k;
+}
+
+// the loop's linear form on the start error (dphaseEst, dV): A = [[1 - kC/2pi, 1], [-kA/2pi, 1]]
+struct M2 { double a, b, c, d; };
+M2 mul(const M2& x, const M2& y) {
+  return {x.a * y.a + x.b * y.c, x.a * y.b + x.b * y.d, x.c * y.a + x.d * y.c, x.c * y.b + x.d * y.d};
+}
+M2 loop_matrix(const PllCfg& c) {
+  const double kA = 2.0 * M_PI * c.ki, kC = 2.0 * M_PI * (c.kp + c.ki);
+  return {1.0 - kC / (2.0 * M_PI), 1.0, -kA / (2.0 * M_PI), 1.0};
+}
+M2 mpow(M2 x, int64_t e) {
+  M2 r{1.0, 0.0, 0.0, 1.0};
+  for (; e > 0; e >>= 1, x = mul(x, x))
+    if (e & 1) r = mul(r, x);
+  return r;
+}
+// c1, c2: the largest |phase deviation| over the steps after a unit start error in phaseEst
+// (c1) or in the integrator (c2), iterated until the loop has damped it (cached per loop)
+struct Bounds { double kp, ki, c1, c2; };
+void loop_bounds(const PllCfg& c, double* c1, double* c2) {
+  static std::mutex mu;
+  static Bounds cache[16];
+  static int ncache = 0;
+  std::lock_guard<std::mutex> g(mu);
+  for (int i = 0; i < ncache; ++i)
+    if (cache[i].kp == c.kp && cache[i].ki == c.ki) { *c1 = cache[i].c1; *c2 = cache[i].c2; return; }
+  const M2 A = loop_matrix(c);
+  double p1 = 1.0, v1 = 0.0, p2 = 0.0, v2 = 1.0, m1 = 1.0, m2 = 0.0;
+  for (int k = 0; k < 400000; ++k) {
+    const double np1 = A.a * p1 + A.b * v1, nv1 = A.c * p1 + A.d * v1;
+    const double np2 = A.a * p2 + A.b * v2, nv2 = A.c * p2 + A.d * v2;
+    p1 = np1; v1 = nv1; p2 = np2; v2 = nv2;
+    m1 = std::max(m1, std::fabs(p1));
+    m2 = std::max(m2, std::fabs(p2));
+    if (k > 64 && std::fabs(p1) + std::fabs(v1) < 1e-6 * m1 && std::fabs(p2) + std::fabs(v2) < 1e-6 * m2) break;
+  }
+  if (ncache < 16) cache[ncache++] = Bounds{c.kp, c.ki, m1, m2};
+  *c1 = m1;
+  *c2 = m2;
+}
+
+// warm-up length: the error contracts by sqrt(1 - Kp) per step; enough steps to bring a
+// start error of pi within LONG_ACCEPT, capped (SDR_PLL_WARM_MAX, default 2560: the stereo loop
+// needs ~1 800; the RDS loop would need ~17 000, and its blocks are re-solved from the chained
+// start instead, for which a start within the linear bound is enough)
+int warm_len(const PllCfg& c, double c1, int64_t pb) {
+  static const int cap = [] {
+    const char* e = getenv("SDR_PLL_WARM_MAX");
+    return e ? std::max(64, atoi(e)) : 2560;
+  }();
+  const double rate = -0.5 * std::log1p(-std::min(std::max(c.kp, 1e-12), 0.999));
+  const double want = std::log(std::max(c1, 1.0) * M_PI / LONG_ACCEPT) / rate;
+  int64_t wl = (int64_t)std::ceil(want / 256.0) * 256;
+  wl = std::min<int64_t>(std::min<int64_t>(wl, cap), 4 * pb);
+  return (int)std::max<int64_t>(wl, 64);
+}
+
+hipError_t long_setup(PllJobs& L) {
+  if (L.work == nullptr) return hipErrorInvalidValue;
+  long_geom(L.n, &L.lg.pb, &L.lg.nb);
+  const int64_t last = L.n - (int64_t)(L.lg.nb - 1) * L.lg.pb;
+  if (last < 2) return hipErrorInvalidValue;
+  for (int q = 0; q < L.njobs; ++q) {
+    const PllCfg& c = L.j[q].cfg;
+    loop_bounds(c, &L.lg.c1[q], &L.lg.c2[q]);
+    const M2 A = loop_matrix(c);
+    const M2 F = mpow(A, L.lg.pb), G = mpow(A, last);
+    const double f[4] = {F.a, F.b, F.c, F.d}, g[4] = {G.a, G.b, G.c, G.d};
+    for (int i = 0; i < 4; ++i) { L.lg.phi[q][i] = f[i]; L.lg.phi_last[q][i] = g[i]; }
+    L.lg.warm[q] = warm_len(c, L.lg.c1[q], L.lg.pb);
+  }
+  return hipSuccess;
+}
+}  // namespace
+
+int64_t sdr_pll_work_bytes(int njobs, int nstreams, int64_t n) {
+  if (n <= SPEC_NMAX) return 0;
+  int64_t pb;
+  int nb;
+  long_geom(n, &pb, &nb);
+  const int64_t R = (int64_t)njobs * nstreams;
+  return R * (int64_t)sizeof(LongHdr) + R * nb * (int64_t)sizeof(LongBlk);
+}
+
 hipError_t sdr_launch_pll_prep(const PllJobs& P, hipStream_t st) {
   bool vec;
   const hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
+  if (pll_long(P)) return hipSuccess;      // long calls compute their constants where they use them (pll_c)
   PllJobs L = P;
-  L.qform = vec && pll_lpw(P) == 1;
+  L.qform = !pll_long(P) && vec && pll_lpw(P) == 1;
   if (P.n > 0)
     hipLaunchKernelGGL(pll_prep_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
                        dim3(256), 0, st, L);
@@ -686,18 +1387,33 @@ hipError_t sdr_launch_pll_prep(const PllJobs& P, hipStream_t st) {
 
 hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
   bool vec;
-  const hipError_t e = pll_check(P, &vec);
+  hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
   PllJobs L = P;
+  if (pll_long(P)) {
+    // long call: warm-up guesses, LONG_ROUNDS x (solve, chain), the sequential tail
+    L.qform = 0;
+    e = long_setup(L);
+    if (e != hipSuccess) return e;
+    const int R = L.njobs * L.nstreams;
+    const unsigned blocks = (unsigned)(R * L.lg.nb);
+    hipLaunchKernelGGL(pll_warm_kernel, dim3((unsigned)(R * ((L.lg.nb + WARM_LPW - 1) / WARM_LPW))), dim3(64), 0, st, L);
+    for (int round = 0; round < LONG_ROUNDS; ++round) {
+      if (round > 0) hipLaunchKernelGGL(pll_long_fix_kernel, dim3(blocks), dim3(FIX_T), 0, st, L);
+      hipLaunchKernelGGL((pll_spec_kernel<512, true>), dim3(blocks), dim3(512), 0, st, L);
+      hipLaunchKernelGGL(pll_long_seq_kernel, dim3((unsigned)(R * ((L.lg.nb + 63) / 64))), dim3(64), 0, st, L);
+      hipLaunchKernelGGL(pll_long_chain_kernel, dim3((unsigned)R), dim3(64), 0, st, L, round);
+    }
+    hipLaunchKernelGGL(pll_long_tail_kernel, dim3((unsigned)R), dim3(64), 0, st, L);
+    return hipGetLastError();
+  }
   L.lpw = pll_lpw(P);
   L.qform = vec && L.lpw == 1;
   const dim3 grid((unsigned)(L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw)));
-  if (pll_spec_enabled() && L.n >= 2 && L.n <= SPEC_NMAX) {
-    PllJobs S = L;
-    S.spec_dbg = getenv("SDR_PLL_SPEC_DEBUG") != nullptr;   // per-round prints (A/B runs)
+  if (pll_spec_enabled() && L.n >= 2) {
     const dim3 g((unsigned)(L.njobs * L.nstreams));
-    if (L.n > 10240) hipLaunchKernelGGL(pll_spec_kernel<512>, g, dim3(512), 0, st, S);
-    else hipLaunchKernelGGL(pll_spec_kernel<256>, g, dim3(256), 0, st, S);
+    if (L.n > 10240) hipLaunchKernelGGL((pll_spec_kernel<512, false>), g, dim3(512), 0, st, L);
+    else hipLaunchKernelGGL((pll_spec_kernel<256, false>), g, dim3(256), 0, st, L);
   }
   if (vec && L.lpw == 1) hipLaunchKernelGGL(pll_chunk_kernel, grid, dim3(128), 0, st, L);
   else if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, L);
@@ -707,10 +1423,14 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
 
 hipError_t sdr_launch_pll_nco(const PllJobs& P, hipStream_t st) {
   bool vec;
-  const hipError_t e = pll_check(P, &vec);
+  hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
   PllJobs L = P;
-  L.qform = vec && pll_lpw(P) == 1;
+  L.qform = !pll_long(P) && vec && pll_lpw(P) == 1;
+  if (pll_long(P)) {
+    e = long_setup(L);
+    if (e != hipSuccess) return e;
+  }
   if (P.n > 0)
     hipLaunchKernelGGL(nco_jobs_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
                        dim3(256), 0, st, L);

@@ -35,10 +35,10 @@ using namespace sdrint;
 namespace {
 
 constexpr int RX_MAXJ = 6;          // jobs per stage launch
-constexpr int RX_NT = 128;          // threads per workgroup
-constexpr int RX_R = 4;             // outputs per thread
-constexpr int RX_TO = RX_NT * RX_R;  // outputs per tile
-constexpr int RX_LDS = 3072;        // floats of LDS per workgroup (largest: 151 taps, decim 5)
+constexpr int RX_NT = 256;          // threads per workgroup
+constexpr int RX_R = 4;             // outputs per thread of the generic tiles (any T, resampler)
+constexpr int RX_TO = RX_NT * RX_R;  // outputs per generic tile
+constexpr int RX_LDS = 5632;        // floats of LDS per workgroup (largest: 151 taps, decim 5)
 
 enum { JK_FIR = 0, JK_RESAMPLE = 1 };
 enum { PRE_NONE = SDR_PRE_NONE, PRE_SQUARE = SDR_PRE_SQUARE, PRE_MIX = SDR_PRE_MIX };
@@ -95,34 +95,44 @@ __device__ __forceinline__ float pre_op(int pre, float x, float c, float g) {
   return pre == PRE_SQUARE ? x * x : pre == PRE_MIX ? (x * c) * g : x;
 }
 
-// The lfilter FIR tile (compile-time T and D): thread t owns R consecutive outputs and slides
-// once over its D(R-1)+T window in LDS; rows padded by one float every D*R samples so the
-// per-lane stride is odd (conflict-free ds_read_b32).  Taps are read through the job's
-// uniform pointer with compile-time indices (scalar loads, SGPR operands).
+// acc += h * x with the tap in an SGPR (v_fmac_f32's scalar operand): the compiler neither
+// moves taps into vector registers nor pairs the FMAs into packed ones (whose tap and sample
+// pairs it had to assemble with a v_mov per FMA)
+__device__ __forceinline__ void fmac_s(float& acc, float h, float x) {
+  asm("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "s"(h), "v"(x));
+}
+typedef const __attribute__((address_space(4))) float* ctaps_t;   // uniform, read-only: scalar loads
+
+// The lfilter FIR tile for compile-time (T, D): lane t owns R consecutive outputs and slides
+// once over its D(R-1)+T-sample window in LDS, R multiply-adds per sample with the taps as
+// SGPR operands (scalar loads through the constant address space, compile-time indices).
+// 16 outputs per lane at D = 1 (16 FMAs per ds_read: VALU-bound, not LDS-bound), 4 at D = 5
+// (a 20x larger window per output; 1/5 of the work).  The tile image has one pad float after
+// every lane's D*R samples (odd lane stride: conflict-free ds_read_b32), and starts DELTA
+// samples early so that its global loads are 16-B aligned.
 template <int T, int D>
 struct FirShape {
-  static constexpr int G = 4, NT = RX_NT, R = RX_R, TO = RX_TO, DR = D * R;
-  static constexpr bool PAD = (DR % 2) == 0;
-  static constexpr int SR = PAD ? DR + 1 : DR;
+  static constexpr int G = 4, NT = RX_NT, R = D == 1 ? 16 : 4, TO = NT * R, DR = D * R;
+  static constexpr int SR = DR + 1;                          // lane stride in LDS (floats)
   static constexpr int DELTA = (G - ((T - 1) % G)) % G;
-  static constexpr int L = ((D * (TO - 1) + T + DELTA) + G - 1) / G * G;
-  static constexpr int NSLOT = PAD ? L + (L + DR - DELTA) / DR + 1 : L;
-  static constexpr int NCHUNK = L / G;
-  static constexpr int NLOAD = (NCHUNK + NT - 1) / NT;
-  static constexpr int NI = D * (R - 1) + T;
+  static constexpr int L = D * (TO - 1) + T + DELTA;         // image samples
+  static constexpr int LG = (L + G - 1) / G * G;
+  static constexpr int NI = D * (R - 1) + T;                 // per-lane window
+  static constexpr int NSLOT = LG + LG / DR + 1;
   static_assert((D * TO) % G == 0, "tile start must stay G-aligned");
   static_assert(NSLOT <= RX_LDS, "tile image fits the stage LDS");
+  static_assert(SR % 2 == 1, "odd lane stride");
+  __device__ static constexpr int slot(int u) { return u < DELTA ? u : u + (u - DELTA) / DR; }
 };
 
 template <int T, int D>
 __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile, float* lds) {
   using S = FirShape<T, D>;
-  constexpr int R = S::R, DR = S::DR, DELTA = S::DELTA, L = S::L;
-  constexpr bool PAD = S::PAD;
+  constexpr int R = S::R, DR = S::DR, DELTA = S::DELTA;
   const int t = threadIdx.x;
   const int64_t m0 = tile * S::TO;
   const int64_t M = (J.n + D - 1) / D;
-  const int64_t n_lo = D * m0 - (T - 1) - DELTA;
+  const int64_t n_lo = D * m0 - (T - 1) - DELTA;           // image sample 0
   const int64_t mf = m0 + (int64_t)t * R;
   const float* xb = J.x + (int64_t)s * J.x_stride;
   const float* cb = J.c ? J.c + (int64_t)s * J.x_stride : nullptr;
@@ -138,56 +148,47 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
     zr[r] = (J.zi != nullptr && nn < T - 1) ? (float)J.zi[(int64_t)s * J.zi_stride + nn] : 0.f;
     mr[r] = (J.mono != nullptr && mf + r < M) ? J.mono[(int64_t)s * J.y_stride + mf + r] : 0.f;
   }
-  auto slot = [](int e) { return PAD ? e + (e + DR - DELTA) / DR : e; };
-  if (n_lo >= 0 && n_lo + L <= J.n) {               // interior: 16-B loads (rows are aligned)
-    float4 v[S::NLOAD], cv[S::NLOAD];
-#pragma unroll
-    for (int j = 0; j < S::NLOAD; ++j) {
-      const int q = t + j * S::NT;
-      if (q < S::NCHUNK) {
-        v[j] = reinterpret_cast<const float4*>(xb + n_lo)[q];
-        cv[j] = pre == PRE_MIX ? reinterpret_cast<const float4*>(cb + n_lo)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < S::NLOAD; ++j) {
-      const int q = t + j * S::NT;
-      if (q < S::NCHUNK) {
-        const int e = q * S::G;
-        lds[slot(e + 0)] = pre_op(pre, v[j].x, cv[j].x, g);
-        lds[slot(e + 1)] = pre_op(pre, v[j].y, cv[j].y, g);
-        lds[slot(e + 2)] = pre_op(pre, v[j].z, cv[j].z, g);
-        lds[slot(e + 3)] = pre_op(pre, v[j].w, cv[j].w, g);
-      }
+  if (n_lo >= 0 && n_lo + S::LG <= J.n) {            // interior: 16-B loads (rows are aligned)
+    constexpr int NCH = S::LG / S::G;
+    for (int q = t; q < NCH; q += S::NT) {
+      const float4 v = reinterpret_cast<const float4*>(xb + n_lo)[q];
+      const float4 cv = pre == PRE_MIX ? reinterpret_cast<const float4*>(cb + n_lo)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int u = q * S::G;
+      lds[S::slot(u + 0)] = pre_op(pre, v.x, cv.x, g);
+      lds[S::slot(u + 1)] = pre_op(pre, v.y, cv.y, g);
+      lds[S::slot(u + 2)] = pre_op(pre, v.z, cv.z, g);
+      lds[S::slot(u + 3)] = pre_op(pre, v.w, cv.w, g);
     }
   } else {
-    for (int e = t; e < L; e += S::NT) {
-      const int64_t nn = n_lo + e;
+    for (int u = t; u < S::LG; u += S::NT) {
+      const int64_t nn = n_lo + u;
       float x = 0.f;
       if (nn >= 0 && nn < J.n) x = pre_op(pre, xb[nn], pre == PRE_MIX ? cb[nn] : 0.f, g);
-      lds[slot(e)] = x;
+      lds[S::slot(u)] = x;
     }
   }
   __syncthreads();
-  const float* h = J.taps;
-  const float* win = lds + (PAD ? (DELTA + 1 + S::SR * t) : (DELTA + DR * t));
+  const ctaps_t h = (ctaps_t)J.taps;
+  const float* win = lds + DELTA + S::SR * t;
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.f;
-#pragma unroll
-  for (int i = 0; i < S::NI; ++i) {
-    const float x = win[PAD ? i + i / DR : i];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int k = D * r + T - 1 - i;
-      if (k >= 0 && k < T) acc[r] = fmaf(h[k], x, acc[r]);
-    }
-  }
+  static_for<0, S::NI>([&](auto I) {
+    constexpr int i = I;
+    const float x = win[i + i / DR];
+    static_for<0, R>([&](auto RR) {
+      constexpr int r = RR;
+      constexpr int k = D * r + T - 1 - i;
+      if constexpr (k >= 0 && k < T) fmac_s(acc[r], h[k], x);
+    });
+  });
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] += zr[r];
   float* yb = J.y + (int64_t)s * J.y_stride;
   if (mf + R <= M) {
-    *reinterpret_cast<float4*>(yb + mf) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+#pragma unroll
+    for (int r = 0; r < R; r += 4)
+      *reinterpret_cast<float4*>(yb + mf + r) = make_float4(acc[r], acc[r + 1], acc[r + 2], acc[r + 3]);
   } else {
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -401,6 +402,15 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
   fir_tile_any(J, s, tile, lds);
 }
 
+// outputs per tile of a job in a launch of tap class `key` (as rx_stage_kernel<key> picks the tile)
+int64_t tile_outputs(const StageJob& j, int key) {
+  if (j.kind == JK_FIR && key == 151 && j.D == 1) return FirShape<151, 1>::TO;
+  if (j.kind == JK_FIR && key == 151 && j.D == 5) return FirShape<151, 5>::TO;
+  if (j.kind == JK_FIR && key == 101 && j.D == 1) return FirShape<101, 1>::TO;
+  if (j.kind == JK_FIR && key == 101 && j.D == 5) return FirShape<101, 5>::TO;
+  return RX_TO;
+}
+
 // Launch the jobs of one stage, one launch per tap-count class.
 hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const FeState* fe = nullptr) {
   auto cls = [](const StageJob& j) { return (j.kind == JK_FIR && (j.T == 101 || j.T == 151)) ? j.T : 0; };
@@ -414,7 +424,8 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
       if (P.njobs == RX_MAXJ) return hipErrorInvalidValue;
       StageJob j = j0;
       const int64_t nout = j.kind == JK_RESAMPLE ? (j.n * j.U + j.D - 1) / j.D : (j.n + j.D - 1) / j.D;
-      j.tiles = (int)std::max<int64_t>((nout + RX_TO - 1) / RX_TO, 0);
+      const int64_t to = tile_outputs(j, key);
+      j.tiles = (int)std::max<int64_t>((nout + to - 1) / to, 0);
       j.b0 = blocks;
       blocks += (int64_t)j.tiles * S;
       if (j.zf != nullptr && j.T > 1) P.zfj[P.nzf++] = P.njobs;
@@ -473,6 +484,8 @@ struct sdr_rx {
   int64_t ths = 0;
   double* pllc = nullptr;              // PLL per-sample constants: 2 x S rows of cst per row set
   int64_t cst = 0;
+  char* pllw = nullptr;                // long blocks (M > SDR_PLL_BLOCK_MAX): the PLL's pseudo-block
+  int64_t pllw_bytes = 0;              //   records, one region per row set
   void* pin_in = nullptr;              // pinned host staging (sdr_rx_run)
   size_t pin_in_cap = 0;
   float* pin_out = nullptr;
@@ -596,7 +609,8 @@ int rx_finalize(sdr_rx* r) {
   const int64_t S2 = round_up(S, 2);                 // keeps the phase rows 16-B aligned
   const int nsets = r->pipe ? 2 : 1;
   const int64_t doubles = 2 * zl + 3 * S2 + 2 * 6 * S2 + nsets * (2 * S * r->ths + 2 * S * r->cst);
-  const size_t bytes = (size_t)floats * 4 + 64 + (size_t)doubles * 8;
+  r->pllw_bytes = round_up(sdr_pll_work_bytes(2, r->S, M), 256);
+  const size_t bytes = (size_t)floats * 4 + 64 + (size_t)doubles * 8 + 256 + (size_t)(nsets * r->pllw_bytes);
   TRY(set_dev(r->c));
   hipError_t e = hipMalloc(&r->mem, bytes);
   if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx: hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
@@ -615,6 +629,7 @@ int rx_finalize(sdr_rx* r) {
   r->pll_state[1] = r->pll_state[0] + 6 * S2;
   r->theta = r->pll_state[1] + 6 * S2;
   r->pllc = r->theta + nsets * 2 * S * r->ths;
+  r->pllw = reinterpret_cast<char*>(round_up((int64_t)(uintptr_t)(r->pllc + nsets * 2 * S * r->cst), 256));
   r->ready = true;
   return sdr_rx_reset(r);
 }
@@ -838,6 +853,8 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   if (plls) {
     P.nstreams = S;
     P.n = M;
+    P.stats = c->pll_stats;
+    P.work = r->pllw_bytes ? r->pllw + (int64_t)q * r->pllw_bytes : nullptr;
     double* th = r->theta + (int64_t)q * 2 * S * r->ths;
     double* pc = r->pllc + (int64_t)q * 2 * S * r->cst;
     const double off = (double)M * (double)r->blocks;
@@ -1094,6 +1111,15 @@ int sdr_rx_stage_ms(sdr_rx* r, float* ms) {
   HIP_TRY(hipEventSynchronize(r->ev[SDR_RX_NSTAGES]));
   for (int k = 0; k < SDR_RX_NSTAGES; ++k) HIP_TRY(hipEventElapsedTime(&ms[k], r->ev[k], r->ev[k + 1]));
   return SDR_OK;
+}
+
+int sdr_rx_pll_stats(sdr_rx* r, int64_t* out, int reset) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  TRY(set_dev(r->c));
+  if (r->front) HIP_TRY(hipStreamSynchronize(r->front));
+  if (r->mid) HIP_TRY(hipStreamSynchronize(r->mid));
+  HIP_TRY(hipStreamSynchronize(r->c->stream));
+  return sdr_pll_stats(r->c, out, reset);
 }
 
 int sdr_rx_state(sdr_rx* r, double* phase, double* pll_stereo, double* pll_rds) {

@@ -16,7 +16,7 @@ namespace sdrint {
 // scratch slots owned by a context (grown on demand, never shrunk)
 enum Slot {
   S_IN, S_IN2, S_OUT, S_OUT2, S_OUT3, S_OUT4, S_STATE, S_STATE2, S_MISC, S_THETA, S_PHI, S_WRAP,
-  S_PSD,
+  S_PSD, S_PLLW,
   S_NSLOT
 };
 
@@ -41,6 +41,9 @@ struct sdr_ctx {
   // is spliced to the back and an overflow evicts the front, so no pointer handed out by
   // a lookup is invalidated by the other lookups of the same entry point (<= 4 per call).
   std::list<sdrint::TapSet> taps;
+  // PLL solve counters (SDR_PLL_NSTATS, device; sdr_pll_stats): every PLL launch of the
+  // context and of its receivers adds to them
+  unsigned long long* pll_stats = nullptr;
 };
 
 namespace sdrint {

@@ -64,7 +64,26 @@ struct PllJob {
   float* nco_i; float* nco_q; int64_t out_stride; PllCfg cfg; double* cbuf; int64_t c_stride;
   double off; int off_given;   // the prep kernel's trigOffset, when not read from state[5]
 };
-struct PllJobs { PllJob j[SDR_PLL_MAXJ]; int njobs; int nstreams; int64_t n; int lpw; int qform; int spec_dbg; };  // lpw, qform, spec_dbg: set by the launchers
+// Long calls (n > SDR_PLL_BLOCK_MAX samples): the recurrence is cut into nb pseudo-blocks of
+// pb samples, solved in parallel from warm-up guesses of their start states and chained
+// (pll.hip, "long calls").  Per job: the warm-up length, the loop matrix's power over a
+// pseudo-block (phi: the start-state error -> end-state error map, for the pb-sample blocks
+// and for the last one) and the bounds c1, c2 on the phase excursion a unit start error in
+// (phaseEst, integrator) causes.  Filled by the launcher.
+#define SDR_PLL_BLOCK_MAX 16385
+struct PllLong {
+  int64_t pb; int nb; int warm[SDR_PLL_MAXJ];
+  double phi[SDR_PLL_MAXJ][4], phi_last[SDR_PLL_MAXJ][4], c1[SDR_PLL_MAXJ], c2[SDR_PLL_MAXJ];
+};
+struct PllJobs {
+  PllJob j[SDR_PLL_MAXJ]; int njobs; int nstreams; int64_t n;
+  int lpw; int qform;                  // set by the launchers
+  unsigned long long* stats;           // device counters (SDR_PLL_NSTATS, include/sdr.h), nullable
+  void* work;                          // long calls: sdr_pll_work_bytes() of device scratch
+  PllLong lg;                          // long calls: set by the launcher
+};
+// device scratch a long call needs (0 when n <= SDR_PLL_BLOCK_MAX)
+int64_t sdr_pll_work_bytes(int njobs, int nstreams, int64_t n);
 // prep (per-sample constants) -> loop (one lane per recurrence) -> NCO; the three launches
 // separately (the receiver puts them on different streams) or together
 hipError_t sdr_launch_pll_prep(const PllJobs& jobs, hipStream_t st);

@@ -47,13 +47,22 @@ def rds_symbols(nbits: int, seed: int = 0) -> np.ndarray:
 
 
 def fm_iq(n_complex: int, seed: int = 0, fs: float = FS, snr_db: float = 30.0, chunk: int = 1 << 22,
-          dtype=np.float32, rds_groups: bool = False, rds_phase: float = 0.0) -> np.ndarray:
+          dtype=np.float32, rds_groups: bool = False, rds_phase: float = 0.0, pilot_offset_hz: float = 0.0,
+          clock_ppm: float = 0.0) -> np.ndarray:
     """Interleaved float32 IQ of `n_complex` samples (generated in chunks to bound memory).
     rds_groups: the 57 kHz subcarrier carries coded RDS groups (rds_symbols) at carrier
-    phase `rds_phase` instead of random symbols."""
+    phase `rds_phase` instead of random symbols.
+    pilot_offset_hz: the transmitter's pilot is 19 kHz + offset, and the 38 / 57 kHz
+    subcarriers derived from it move with it (x2, x3; the RDS PLL's 114 kHz carrier x6).
+    clock_ppm: the receiver's sample clock runs fast by this many ppm (an RTL-SDR crystal's
+    error, src/iofunc.cpp:61-69 reads whatever it delivers): sample k is taken at transmitter
+    time k / (fs (1 + ppm 1e-6)), so every tone, the RDS symbol rate and the FM phase
+    integral are seen slightly slow -- the composite resampled."""
     rng = np.random.default_rng(seed)
     out = np.empty(2 * n_complex, dtype=np.float32)
-    sym_len = fs / 2375.0
+    fs_tx = fs * (1.0 + clock_ppm * 1e-6)       # receiver samples per transmitter second
+    fp = 19e3 + pilot_offset_hz
+    sym_len = fs_tx / 2375.0
     nsym = int(np.ceil(n_complex / sym_len)) + 2
     symbols = rng.choice(np.array([-1.0, 1.0]), size=nsym)
     if rds_groups:
@@ -64,14 +73,14 @@ def fm_iq(n_complex: int, seed: int = 0, fs: float = FS, snr_db: float = 30.0, c
     phase0 = 0.0
     for start in range(0, n_complex, chunk):
         n = min(chunk, n_complex - start)
-        t = (start + np.arange(n, dtype=np.float64)) / fs
+        t = (start + np.arange(n, dtype=np.float64)) / fs_tx
         left = np.sin(2 * np.pi * 1e3 * t)
         right = 0.8 * np.sin(2 * np.pi * 2.5e3 * t)
         rds = symbols[((start + np.arange(n)) / sym_len).astype(np.int64)]
-        mpx = (0.45 * (left + right) / 2 + 0.1 * np.cos(2 * np.pi * 19e3 * t)
-               + 0.45 * (left - right) / 2 * np.cos(2 * np.pi * 38e3 * t)
-               + 0.05 * rds * np.cos(2 * np.pi * 57e3 * t + rds_phase))
-        phi = phase0 + 2 * np.pi * 75e3 * np.cumsum(mpx) / fs
+        mpx = (0.45 * (left + right) / 2 + 0.1 * np.cos(2 * np.pi * fp * t)
+               + 0.45 * (left - right) / 2 * np.cos(2 * np.pi * (2 * fp) * t)
+               + 0.05 * rds * np.cos(2 * np.pi * (3 * fp) * t + rds_phase))
+        phi = phase0 + 2 * np.pi * 75e3 * np.cumsum(mpx) / fs_tx
         phase0 = float(phi[-1])
         noise = noise_rng.standard_normal((n, 2)) * sigma
         out[2 * start:2 * (start + n):2] = (amp * np.cos(phi) + noise[:, 0]).astype(np.float32)

@@ -18,6 +18,9 @@ pytestmark = pytest.mark.gpu
 
 B5 = 153_600
 AUDIO_RMS, AUDIO_MAX = 1e-6, 1e-5
+# stereo NCO (f32 cos of the f64 phase) vs the oracle: 3e-8 is the f32 rounding; ~3x margin
+# over the worst measured on MI355X (tests/test_dropin.py bounds the same quantity at 1e-7)
+NCO_MAX = 1e-7
 
 # (max, rms) relative to max|ref| per RDS intermediate: about 3x the worst errors measured on
 # MI355X over 8 streams x 2 blocks (profiles/r02/rx_tolerances.log).  The Q branch is small
@@ -42,9 +45,18 @@ def test_receiver_c5_eight_streams_match_oracle(sdr, gpu_ctx, oracle):
     rx = sdr.Receiver(S, B5, stereo=True, rds=True, iq_dtype=np.uint8)
     names = ["demod", "audio", "stereo", "left", "right", "bpf_recovery", "nco", "bpf_extraction"] + list(RDS_TOL)
     got = []
+    gpu_ctx.pll_stats(reset=True)
     for k in range(nb):
         got.append(rx.process(iq[:, 2 * k * B5:2 * (k + 1) * B5], fetch=names))
+        if k == 0:
+            first = rx.pll_stats(reset=True)
+    st = rx.pll_stats()
+    print("solver counters, block 0:", first, "block 1:", st)
+    assert first["recurrences"] == 2 * S and st["recurrences"] == 2 * S
+    # after the acquisition block every stereo and RDS recurrence completes in the parallel solve
+    assert st["spec_r0"] + st["spec_r1"] + st["spec_r2"] == 2 * S and st["sequential"] == 0, st
     worst = {}
+    nco_worst = 0.0
     for s in range(S):
         f = (iq[s].astype(np.float64) - 128.0) / 128.0
         mono = oracle.mono_stereo_blocks(f, B5, rf_taps=151, audio_taps=151, nblocks=nb)
@@ -55,14 +67,16 @@ def test_receiver_c5_eight_streams_match_oracle(sdr, gpu_ctx, oracle):
             for key in ("audio", "stereo", "left", "right"):
                 assert rms(g[key][s], mono[k][key]) < AUDIO_RMS, (key, s, k, rms(g[key][s], mono[k][key]))
                 assert maxabs(g[key][s], mono[k][key]) < AUDIO_MAX, (key, s, k)
-            assert maxabs(g["nco"][s], mono[k]["nco"]) < 1e-4
+            nco_worst = max(nco_worst, maxabs(g["nco"][s], mono[k]["nco"]))
+            assert maxabs(g["nco"][s], mono[k]["nco"]) < NCO_MAX, (s, k)
             for key, (tmax, trms) in RDS_TOL.items():
                 ref = rds[k][key]
                 scale = max(float(np.max(np.abs(ref))), 1e-3)
                 em, er = maxabs(g[key][s], ref) / scale, rms(g[key][s], ref) / scale
                 worst[key] = max(worst.get(key, (0, 0))[0], em), max(worst.get(key, (0, 0))[1], er)
                 assert em < tmax and er < trms, (key, s, k, em, er)
-    print("RDS relative errors (max, rms):", {k: (f"{a:.1e}", f"{b:.1e}") for k, (a, b) in worst.items()})
+    print("RDS relative errors (max, rms):", {k: (f"{a:.1e}", f"{b:.1e}") for k, (a, b) in worst.items()},
+          f"stereo NCO max error {nco_worst:.1e}")
 
 
 def test_receiver_streams_equal_single_stream(sdr, gpu_ctx):

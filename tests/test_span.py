@@ -1,0 +1,85 @@
+"""Time-parallel receiver spans (>= 256 device-resident blocks per stream):
+a receiver whose block is K of the reference's 153 600-sample blocks processes the K blocks
+of every stream in ONE chain of launches -- the FE and stage filters as one pass over the
+span (block processing == a single pass, spec p.4), the PLLs as a long call
+(pseudo-blocks solved in parallel and chained, csrc/pll.hip "long calls").
+
+Checked against (a) the per-block receiver over the same K blocks (the reference's block
+loop, model/fmRDSblock.py:127-204 and model/fmMonoBlock.py:80-173) and (b) the oracle, with
+the PLL solver counters asserted (every pseudo-block solved in parallel)."""
+import numpy as np
+import pytest
+
+from conftest import maxabs, rms
+from test_receiver import AUDIO_MAX, AUDIO_RMS, RDS_TOL
+
+pytestmark = pytest.mark.gpu
+
+B5 = 153_600
+NAMES = ["demod", "audio", "stereo", "left", "right", "bpf_recovery", "nco", "bpf_extraction"] + list(RDS_TOL)
+NCO_NAMES = ("nco", "nco_i", "nco_q")
+# span vs per-block receiver: the same f32 kernels; they differ only in how block starts are
+# formed (lfilter zi added in f32 there, the continuous convolution here) and in the PLL's
+# rounding (scan association): relative to each signal's peak
+SPAN_REL = {"demod": 2e-6, "audio": 2e-6, "stereo": 2e-6, "left": 2e-6, "right": 2e-6,
+            "bpf_recovery": 2e-6, "nco": 2e-7, "bpf_extraction": 2e-6, "extract": 2e-6, "pre_pll": 4e-6,
+            "nco_i": 2e-7, "nco_q": 2e-7, "lpf_i": 4e-6, "lpf_q": 3e-5, "resample_i": 4e-6, "resample_q": 3e-5,
+            "rrc_i": 4e-6, "rrc_q": 3e-5}
+
+
+def _concat_blocks(rows, name):
+    """per-block outputs (list over blocks of (S, n)) as one span row; NCO rows carry index 0
+    = the previous block's last value, so block k contributes [0, M) and the last block M too"""
+    if name in NCO_NAMES:
+        return np.concatenate([r[:, :-1] for r in rows] + [rows[-1][:, -1:]], axis=1)
+    return np.concatenate(rows, axis=1)
+
+
+def test_span_receiver_equals_block_loop_and_oracle(sdr, gpu_ctx, oracle):
+    S, K, spans = 2, 4, 2
+    iq = np.stack([sdr.synth.fm_iq(spans * K * B5 + 1, seed=70 + s, dtype=np.uint8) for s in range(S)])
+    kw = dict(stereo=True, rds=True, iq_dtype=np.uint8)
+    per_rx = sdr.Receiver(S, B5, **kw)
+    per = [per_rx.process(iq[:, 2 * k * B5:2 * (k + 1) * B5], fetch=NAMES) for k in range(spans * K)]
+    span_rx = sdr.Receiver(S, K * B5, **kw)
+    worst = {}
+    for sp in range(spans):
+        gpu_ctx.pll_stats(reset=True)
+        got = span_rx.process(iq[:, 2 * sp * K * B5:2 * (sp + 1) * K * B5], fetch=NAMES)
+        st = span_rx.pll_stats()
+        print(f"span {sp} solver counters:", st)
+        nb = -(-K * (B5 // 10) // 16384)
+        assert st["recurrences"] == S * 2 * nb, st
+        assert st["long_guessed"] + st["long_chained"] == S * 2 * nb, st
+        # the first span starts at the stream start (acquisition); the next must be all parallel
+        assert st["sequential"] <= (S * 2 if sp == 0 else 0), st
+        for name in NAMES:
+            want = _concat_blocks([p[name] for p in per[sp * K:(sp + 1) * K]], name)
+            assert got[name].shape == want.shape, (name, got[name].shape, want.shape)
+            scale = max(float(np.max(np.abs(want))), 1e-3)
+            e = maxabs(got[name], want) / scale
+            worst[name] = max(worst.get(name, 0.0), e)
+            assert e < SPAN_REL[name], (name, sp, e)
+    print("span vs block loop, max error relative to peak:", {k: f"{v:.1e}" for k, v in worst.items()})
+    # the span's carried states continue the block loop's
+    for a, b in zip(span_rx.state(), per_rx.state()):
+        assert maxabs(a, b) < 1e-6
+    # against the oracle (stream 0, all blocks)
+    f = (iq[0].astype(np.float64) - 128.0) / 128.0
+    mono = oracle.mono_stereo_blocks(f, B5, rf_taps=151, audio_taps=151, nblocks=spans * K)
+    rds = oracle.rds_blocks(iq[0], 2 * B5, taps=151, nblocks=spans * K)
+    span_rx.reset()
+    for sp in range(spans):
+        got = span_rx.process(iq[:, 2 * sp * K * B5:2 * (sp + 1) * K * B5], fetch=NAMES)
+        blocks = range(sp * K, (sp + 1) * K)
+        for key in ("audio", "stereo", "left", "right"):
+            want = np.concatenate([mono[k][key] for k in blocks])
+            assert rms(got[key][0], want) < AUDIO_RMS and maxabs(got[key][0], want) < AUDIO_MAX, (key, sp)
+        want = _concat_blocks([mono[k]["nco"][None, :] for k in blocks], "nco")[0]
+        assert maxabs(got["nco"][0], want) < 3e-7
+        for key, (tmax, trms) in RDS_TOL.items():
+            want = (_concat_blocks([rds[k][key][None, :] for k in blocks], key)[0] if key in NCO_NAMES else
+                    np.concatenate([rds[k][key] for k in blocks]))
+            scale = max(float(np.max(np.abs(want))), 1e-3)
+            em, er = maxabs(got[key][0], want) / scale, rms(got[key][0], want) / scale
+            assert em < tmax and er < trms, (key, sp, em, er)
