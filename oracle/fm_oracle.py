@@ -188,6 +188,63 @@ def mono_stereo_blocks(iq, block_complex, rf_taps=151, audio_taps=151, stereo=Tr
     return out
 
 
+def mode1_coeffs(rf_taps=151):
+    """Mode 1 (src/fm_radio.cpp:16-21, :150-252: 2.5 MS/s RF, IF 250 kS/s, 24/125 to 48 kS/s).
+    The RF low-pass and the resampler filter are the reference's (cutoff 100 kHz at 2.5 MHz;
+    16 kHz at the 6 MHz upsampled rate, 3 623 taps).  The pilot and stereo band-passes are
+    designed at the 250 kS/s IF they run at -- the INTENDED form: src/fm_radio.cpp:231-240
+    designs them against 6 MHz, which puts both pass-bands far below 19 kHz / 22-54 kHz
+    (parity unpinned)."""
+    fs2 = 250e3 / 2
+    return dict(rf=signal.firwin(rf_taps, 100e3 / 1.25e6, window=("hann")),
+                res=signal.firwin(3623, 16e3 / 3e6, window=("hann")),
+                pilot=signal.firwin(151, [18.5e3 / fs2, 19.5e3 / fs2], window=("hann"), pass_zero="bandpass"),
+                ext=signal.firwin(151, [22e3 / fs2, 54e3 / fs2], window=("hann"), pass_zero="bandpass"))
+
+
+def mode1_stereo_blocks(iq, block_complex=153_600, rf_taps=151, nblocks=None):
+    """Mode-1 stereo in its intended form (parity UNPINNED: the reference's own mode-1 stereo,
+    src/fm_radio.cpp:231-252, is defective -- band-passes designed at 6 MHz, fmPLL at Fs
+    240 kHz on a 250 kS/s IF, mixer without the x2 of model/fmMonoBlock.py:154, stereo
+    low-pass decimating by 5 with no upsampling, so its stereo channel has the wrong rate and
+    length).  Restated here as the mode-0 stereo path (model/fmMonoBlock.py:113-166) moved to
+    the 250 kS/s IF: pilot BPF -> fmPll(19 kHz, Fs 250 kHz, x2) -> stereo BPF -> mixer x2 ->
+    the mode-1 mono resampler (24/125, 3 623 taps, :226-229) -> L/R = (m +- s)/2.  The FE is
+    the reference's mode-1 RF stage (151 taps at 2.5 MHz, decim 10, src/fm_radio.cpp:60-147).
+    iq: interleaved float (x-128)/128.  Per block A = M*24/125 - 1 = 2 949 audio samples (the
+    reference writes floor(M*24/125) of the 2 950 its resampler yields, :226-229)."""
+    co = mode1_coeffs(rf_taps)
+    B = 2 * block_complex
+    M = block_complex // 10
+    A = M * 24 // 125
+    zi_i, zi_q = np.zeros(rf_taps - 1), np.zeros(rf_taps - 1)
+    phase = 0.0
+    zr_m, zr_s = np.zeros(3622), np.zeros(3622)
+    z_p, z_e = np.zeros(150), np.zeros(150)
+    pll_state = [0.0, 0.0, 1.0, 0.0, 1.0, 0.0]
+    out = []
+    k = 0
+    while (k + 1) * B <= len(iq) and (nblocks is None or k < nblocks):
+        blk = iq[k * B:(k + 1) * B]
+        i_f, zi_i = lfilter_fir(co["rf"], blk[0::2], zi_i)
+        q_f, zi_q = lfilter_fir(co["rf"], blk[1::2], zi_q)
+        dm, phase = fm_demod_arctan(i_f[::10], q_f[::10], phase)
+        r = {"demod": dm}
+        m, zr_m = resample(dm, co["res"], zr_m, 24, 125)
+        r["pilot"], z_p = lfilter_fir(co["pilot"], dm, z_p)
+        nco, _, pll_state = fm_pll(r["pilot"], 19e3, 250e3, list(pll_state), 2)
+        r["nco"] = nco
+        r["ext"], z_e = lfilter_fir(co["ext"], dm, z_e)
+        mixed = nco[:M] * r["ext"] * 2
+        s, zr_s = resample(mixed, co["res"], zr_s, 24, 125)
+        r["audio"], r["stereo"] = m[:A], s[:A]
+        r["left"] = (r["audio"] + r["stereo"]) / 2
+        r["right"] = (r["audio"] - r["stereo"]) / 2
+        out.append(r)
+        k += 1
+    return out
+
+
 def rds_blocks(iq_u8, block_values=307200, taps=151, nblocks=None, demod_fn=fm_demod_arctan, pll_fn=fm_pll):
     """Restatement of model/fmRDSblock.py:127-204 (signal path up to the RRC filter).
     iq_u8: interleaved uint8, normalised (x-128)/128 as :59."""

@@ -26,9 +26,12 @@
 // (default 151, the reference's), --blocks N (stop after N blocks), --mode 1 (2.5 MS/s IQ,
 // src/fm_radio.cpp:36; the 250 kS/s IF goes to 48 kHz through the 24/125 resampler with a
 // 6 MHz, 16 kHz filter, :174-180, :228, whose up-gain the reference applies at the int16
-// write, :229, :297; mono only: the reference designs its mode-1 pilot/stereo band-passes
-// at 6 MHz for 250 kS/s data and runs its PLL at 240 kHz, :201-202, :233, so they have no
-// working form to reproduce).  Mode-1 taps: firwin(3623, 16 kHz at 6 MHz); the reference's
+// write, :229, :297).  Mode-1 stereo runs in its intended form: pilot and stereo band-passes
+// designed at the 250 kS/s IF, fmPll at 19 kHz / Fs 250 kHz (x2), mixer x2, the stereo channel
+// through the same 24/125 resampler, L/R = (m +- s)/2 -- the reference designs its mode-1
+// band-passes at 6 MHz and runs its PLL at 240 kHz, :201-202, :231-252, so its own mode-1
+// stereo has no working form to reproduce (parity unpinned; --mono: mono only).
+// Mode-1 taps: firwin(3623, 16 kHz at 6 MHz); the reference's
 // 151*24 = 3624-tap sinc design divides 0/0 at its tap 1812 (src/filter.cpp:29-33) and
 // writes NaN audio, i.e. silence (:290-293).  Per block it writes floor(15360*24/125) =
 // 2 949 samples, as the reference does (src/filter.cpp:264).
@@ -138,7 +141,6 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "fm_radio_gpu: --mode %d: modes 0 (2.4 MS/s) and 1 (2.5 MS/s)\n", mode);
     return 2;
   }
-  if (mode == 1) mono = true;
   if (mode == 1 && rds) {
     std::fprintf(stderr, "fm_radio_gpu: --rds is a mode-0 feature (src/fm_radio.cpp:321-324)\n");
     return 2;
@@ -163,6 +165,10 @@ int main(int argc, char** argv) {
   const std::vector<double> rlp_b = firwin(151, 0.0, 3e3 / 120e3);
   const std::vector<double> ran_b = firwin(151, 0.0, (57000.0 / 2) / ((240000.0 * 19) / 2));
   const std::vector<double> rrc_b = rrc(57000.0, 151);
+  // mode-1 stereo, the intended form at the 250 kS/s IF (src/fm_radio.cpp:231-252 designs these
+  // band-passes at 6 MHz and runs the PLL at Fs 240 kHz: DESIGN.md §8)
+  const std::vector<double> pil1_b = firwin(151, 18.5e3 / 125e3, 19.5e3 / 125e3);
+  const std::vector<double> ext1_b = firwin(151, 22e3 / 125e3, 54e3 / 125e3);
   if (print_taps) {                    // (no GPU) one line per filter, for the design test
     for (const auto* t : {&rf_b, &au_b, &pil_b, &ext_b, &ste_b, &m1_b, &rex_b, &rsq_b, &rlp_b, &ran_b, &rrc_b}) {
       for (size_t k = 0; k < t->size(); ++k) std::printf(k ? " %.17g" : "%.17g", (*t)[k]);
@@ -185,6 +191,28 @@ int main(int argc, char** argv) {
   auto* d_dm = static_cast<float*>(d.alloc(4 * M + 16));
   auto* d_au = static_cast<float*>(d.alloc(4 * AY + 16));
   auto* zi_au = static_cast<double*>(d.alloc(8 * (kM1Taps - 1)));  // mode 1
+  // mode-1 stereo: pilot / stereo band-pass outputs, NCO, mixer, stereo resampler output, L, R,
+  // and the carried states (band-pass zi, PLL, stereo resampler zi)
+  const bool stereo1 = mode == 1 && !mono;
+  float *d_pil = nullptr, *d_ext = nullptr, *d_nco = nullptr, *d_mix = nullptr, *d_side = nullptr, *d_L = nullptr,
+        *d_R = nullptr;
+  double *zi_pil = nullptr, *zi_ext = nullptr, *pll_st = nullptr, *zi_side = nullptr;
+  const double one_tap[1] = {1.0};
+  if (stereo1) {
+    d_pil = static_cast<float*>(d.alloc(4 * M + 16));
+    d_ext = static_cast<float*>(d.alloc(4 * M + 16));
+    d_nco = static_cast<float*>(d.alloc(4 * (M + 1) + 16));
+    d_mix = static_cast<float*>(d.alloc(4 * M + 16));
+    d_side = static_cast<float*>(d.alloc(4 * AY + 16));
+    d_L = static_cast<float*>(d.alloc(4 * AY + 16));
+    d_R = static_cast<float*>(d.alloc(4 * AY + 16));
+    zi_pil = static_cast<double*>(d.alloc(8 * 150));
+    zi_ext = static_cast<double*>(d.alloc(8 * 150));
+    zi_side = static_cast<double*>(d.alloc(8 * (kM1Taps - 1)));
+    pll_st = static_cast<double*>(d.alloc(8 * 6));
+    const double init[6] = {0.0, 0.0, 1.0, 0.0, 1.0, 0.0};            // model/fmMonoBlock.py:76
+    hk(hipMemcpyAsync(pll_st, init, sizeof init, hipMemcpyHostToDevice, st), "H2D");
+  }
   hk(hipStreamSynchronize(st), "hipStreamSynchronize");
 
   // two-slot pinned ring
@@ -284,6 +312,23 @@ int main(int argc, char** argv) {
                              rf_st + Z, Z, rf_st, rf_st + Z, rf_st + 2 * Z, d_dm, M, nullptr, nullptr),
          "front end");
       ck(sdr_resample_dev(c, d_dm, M, m1_b.data(), kM1Taps, kUp, kDown, zi_au, zi_au, d_au), "mode-1 resampler");
+      if (stereo1) {
+        // pilot and stereo band-passes at the IF, the pilot PLL (19 kHz at Fs 250 kHz, x2), the
+        // mixer (x2, a one-tap FIR's pre-op), the stereo channel through the same 24/125
+        // resampler, then L = (m + s)/2, R = (m - s)/2
+        ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, pil1_b.data(), 151, 1, zi_pil, 150, zi_pil,
+                       d_pil, M), "mode-1 pilot BPF");
+        ck(sdr_fir_dev(c, d_dm, nullptr, 1.f, SDR_PRE_NONE, M, M, 0, 1, ext1_b.data(), 151, 1, zi_ext, 150, zi_ext,
+                       d_ext, M), "mode-1 stereo BPF");
+        ck(sdr_pll_dev(c, d_pil, M, M, 1, 19e3, 250e3, 2.0, 0.0, 0.01, pll_st, d_nco, nullptr, M + 1), "mode-1 PLL");
+        ck(sdr_fir_dev(c, d_ext, d_nco, 2.f, SDR_PRE_MIX, M, M, 0, 1, one_tap, 1, 1, nullptr, 0, nullptr, d_mix, M),
+           "mode-1 mixer");
+        ck(sdr_resample_dev(c, d_mix, M, m1_b.data(), kM1Taps, kUp, kDown, zi_side, zi_side, d_side),
+           "mode-1 stereo resampler");
+        ck(sdr_stereo_combine_dev(c, d_au, d_side, A, d_L, d_R), "mode-1 combiner");
+        out_l = d_L;
+        out_r = d_R;
+      }
     }
     if (pending >= 0) {                // before reusing this slot's output buffer
       finish(pending);

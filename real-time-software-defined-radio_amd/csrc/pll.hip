@@ -438,9 +438,12 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 // recurrence is marked by c[0] = +inf (c[0] is the literal sample's slot: the loop kernels
 // never read it, and the prep kernel rewrites it every call).
 constexpr int SPEC_W = 256;          // warm-up samples before each chunk
+constexpr int SPEC_W_LONG = 64;      // ... in a long call's pseudo-block (its start is a converged
+                                     //     guess or the chained state, its drift measured)
 constexpr int SPEC_IT = 3;           // solve / check rounds before the sequential kernel takes over
 constexpr int SPEC_NMAX = SDR_PLL_BLOCK_MAX; // samples per call (the constants of steps 1.. in LDS: 128 KiB)
 static_assert(SPEC_NMAX == 16384 + 1, "LDS sizing");
+constexpr int SPEC_LDS = 32 * 513;           // padded transposed image: 512 chunks of <= 32 steps (or 256 of <= 40)
 
 // ---- long calls: pseudo-block bookkeeping (device scratch P.work) --------------------
 // Per recurrence r = job * nstreams + stream: a header (the chain's position and the exact
@@ -462,6 +465,27 @@ __device__ __forceinline__ int64_t long_len(const PllJobs& P, int b) {
   return b < P.lg.nb - 1 ? P.lg.pb : P.n - (int64_t)(P.lg.nb - 1) * P.lg.pb;
 }
 
+__device__ __forceinline__ double wave_prefix_sum(double v, int lane) {   // inclusive
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// 2x2 matrices (row-major a, b, c, d) for the loop's linear form
+struct Mat2 { double a, b, c, d; };
+__device__ __forceinline__ Mat2 mmul(const Mat2& x, const Mat2& y) {
+  return {x.a * y.a + x.b * y.c, x.a * y.b + x.b * y.d, x.c * y.a + x.d * y.c, x.c * y.b + x.d * y.d};
+}
+__device__ __forceinline__ Mat2 mpow2(Mat2 x, int e) {
+  Mat2 r{1.0, 0.0, 0.0, 1.0};
+  for (; e > 0; e >>= 1, x = mmul(x, x))
+    if (e & 1) r = mmul(r, x);
+  return r;
+}
+
 // SPEC_T threads (chunks) per recurrence: 256 (one wave per SIMD) up to 10 240 samples, 512
 // beyond (the warm-up is the same length either way; 512 halves the chunks, and a second
 // wave per SIMD then pays: c5 blocks 56 -> ~50 us, c4 blocks slower).
@@ -471,10 +495,15 @@ __device__ __forceinline__ int64_t long_len(const PllJobs& P, int b) {
 template <int SPEC_T, bool LONG>
 __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
 #pragma clang fp contract(off)
-  __shared__ double cl[SPEC_NMAX - 1];         // c_k of steps 1 .. n-1 (plain form)
-  __shared__ int8_t mrel[SPEC_NMAX - 1];       // m_k - floor(c_k) + jb, jb = floor(phaseEst_1 / 2pi)
+  // c_k of steps 1 .. n-1 (plain form) and m_k - floor(c_k) + jb (jb = floor(phaseEst_1 / 2pi)),
+  // step i of chunk j at i * CSTR + j (see the staging below)
+  constexpr int CSTR = SPEC_T + 1, NW = SPEC_T / 64;
+  __shared__ double cl[SPEC_LDS];
+  __shared__ int8_t mrel[SPEC_LDS];
   __shared__ d2v yb[SPEC_T];
+  __shared__ d2v wsum[NW];
   __shared__ double x1s[2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int tid = threadIdx.x;
   int q, s, status = 0;
   int64_t n, base = 0;
@@ -532,22 +561,28 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
   __syncthreads();
   const double p1 = x1s[0], v1 = x1s[1];
   const int64_t N = n - 1;                       // steps 1 .. n-1
-  // every step reads its constant several times: stage them (plain form) in LDS
-  if constexpr (LONG) {
+  const int L = (int)((N + SPEC_T - 1) / SPEC_T);
+  const int TE = (int)((N + L - 1) / L);         // chunks in use; chunks 0 .. TE-2 are full
+  const int64_t k0 = 1 + (int64_t)tid * L;
+  const int64_t k1 = tid < TE ? min<int64_t>(k0 + L, n) : k0;
+  // every step reads its constant several times: stage them (plain form) in LDS, transposed --
+  // step i of chunk j at i * CSTR + j -- so that the threads' per-step reads of their own
+  // chunks are consecutive (contiguous chunks put all 64 lanes of a ds_read_b64 on one bank at
+  // L = 32: a 64-way conflict on every step); the odd stride CSTR = SPEC_T + 1 keeps the
+  // coalesced staging writes (consecutive threads: consecutive i) conflict-free too
+  {
     const double w1 = 2.0 * kPi * (cfg.freq / cfg.fs);
-    for (int64_t k = tid; k < N; k += SPEC_T) cl[k] = pll_c(in[k + 1], w1, off + (double)(k + 1));
-  } else {
-    for (int64_t k = tid; k < N; k += SPEC_T) cl[k] = cplain(k + 1);
+    for (int kk = tid; kk < (int)N; kk += SPEC_T) {
+      const int j = kk / L, i = kk - j * L;
+      cl[i * CSTR + j] = LONG ? pll_c(in[kk + 1], w1, off + (double)(kk + 1)) : cplain(kk + 1);
+    }
   }
   __syncthreads();
   // the integer part relative to floor(c_k) is floor(-phaseEst/2pi + frac(c_k)): near -jb
   // within a block, so it fits a byte once jb is taken off (a drifting phase estimate moves jb)
   const double jb = floor(kInv2Pi * p1);
   auto rel_of = [&](double t, double c) { return floor(t) - floor(c) + jb; };
-  const int L = (int)((N + SPEC_T - 1) / SPEC_T);
-  const int TE = (int)((N + L - 1) / L);         // chunks in use; chunks 0 .. TE-2 are full
-  const int64_t k0 = 1 + (int64_t)tid * L;
-  const int64_t k1 = tid < TE ? min<int64_t>(k0 + L, n) : k0;
+  auto own = [&](int64_t k) { return (int)(k - k0) * CSTR + tid; };     // LDS slot of own step k
   // 0. where the locked phase estimate goes within the block, measured from the input: a
   // locked loop keeps its angle th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's
   // phase, so z_j = sum over chunk j of x_k exp(-i w (off + k)) ~ (A/2) exp(i phaseEst) (+ an
@@ -558,17 +593,17 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
   // state alone, the RDS loop's 256-step warm-ups (contraction ~0.7) cannot catch it up.
   // Extrapolating by integ does worse: integ swings with the loop's own oscillation.)
   {
+    // sign(x_k) exp(-i w (off + k)) = exp(-i 2 pi fract(1/2 - c_k)) (c_k carries the sign):
+    // the constants alone, already in LDS (a hard-limited correlation, as the loop's detector)
     float zr = 0.f, zi = 0.f;
     for (int64_t k = k0; k < k1; ++k) {
-      const double c = cl[k - 1];
-      const float xv = in[k];
+      const double c = cl[own(k)];
       if (!(c == c)) continue;                   // a 0 / NaN input (rejected below anyway)
-      // w (off + k) mod 2 pi = 2 pi fract(sel/2pi + 1/2 - c_k), sel/2pi = 0 (x > 0) or 1/2
-      const float a = (float)(k2Pi * __builtin_amdgcn_fract((xv > 0.f ? 0.5 : 1.0) - c));
+      const float a = (float)(k2Pi * __builtin_amdgcn_fract(0.5 - c));
       float sa, ca;
       __sincosf(a, &sa, &ca);
-      zr = fmaf(xv, ca, zr);
-      zi = fmaf(-xv, sa, zi);
+      zr += ca;
+      zi -= sa;
     }
     yb[tid] = d2v{(double)zr, (double)zi};
     __syncthreads();
@@ -586,13 +621,12 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
       d = ang - yb[tid - 1].x;
       d -= k2Pi * rint(d * kInv2Pi);
     }
-    for (int o = 1; o < SPEC_T; o <<= 1) {     // inclusive prefix sum of the differences
-      __syncthreads();
-      yb[tid].y = d;
-      __syncthreads();
-      if (tid >= o) d += yb[tid - o].y;
-    }
+    // inclusive prefix sum of the differences: within each wave by shuffles, then the waves'
+    // totals
+    d = wave_prefix_sum(d, lane);
+    if (lane == 63) wsum[wv].x = d;
     __syncthreads();
+    for (int i = 0; i < wv; ++i) d += wsum[i].x;
     yb[tid].x = d;                               // D_j
     __syncthreads();
   }
@@ -602,24 +636,26 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
     // the true step from a seed on the measured drift: phaseEst ~ p1 + D at the warm-up's
     // start, integ ~ the measured drift per step; 256 steps of the loop then pull the guess
     // onto the trajectory
-    const int64_t kw = max<int64_t>(1, k0 - SPEC_W);
+    const int64_t kw = max<int64_t>(1, k0 - (LONG ? SPEC_W_LONG : SPEC_W));
     const int jw = (int)((kw - 1) / L);
     double p = p1 + yb[jw].x, V = v1;
     if (k0 - kw >= 64 && tid < TE) V = (yb[tid].x - yb[jw].x) / (double)(k0 - kw) - kD;
+    int jc = jw, ic = (int)(kw - 1) - jw * L;     // (chunk, step) of step kw
 #pragma unroll 8
     for (int64_t k = kw; k < k0 && tid < TE; ++k) {
-      const double t = fma(-kInv2Pi, p, cl[k - 1]);
+      const double t = fma(-kInv2Pi, p, cl[ic * CSTR + jc]);
+      if (++ic == L) { ic = 0; ++jc; }
       const double f = __builtin_amdgcn_fract(t);
       const double S = p + V;
       V = fma(kA, f, V - kB);
       p = fma(kC, f, S);
     }
     for (int64_t k = k0; k < k1; ++k) {
-      const double c = cl[k - 1];
+      const double c = cl[own(k)];
       const double t = fma(-kInv2Pi, p, c);
       const double r = rel_of(t, c);
       bad |= !(r >= -127.0 && r <= 127.0);       // also a NaN constant (a 0 / NaN input)
-      mrel[k - 1] = (int8_t)(bad ? 0.0 : r);
+      mrel[own(k)] = (int8_t)(bad ? 0.0 : r);
       const double f = __builtin_amdgcn_fract(t);
       const double S = p + V;
       V = fma(kA, f, V - kB);
@@ -640,42 +676,65 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
     double zp = 0.0, zv = 0.0;
 #pragma unroll 4
     for (int64_t k = k0; k < k1; ++k) {
-      const double c = cl[k - 1];
-      const double d = c - (floor(c) + ((double)mrel[k - 1] - jb));
+      const double c = cl[own(k)];
+      const double d = c - (floor(c) + ((double)mrel[own(k)] - jb));
       const double np = a00 * zp + zv + kC * d;
       const double nv = a10 * zp + zv + (kA * d - kB);
       zp = np; zv = nv;
     }
-    __syncthreads();                             // mrel reads done before the checks below
-    // v_0 = x_1, v_j = z_{j-1}; y_j = sum_{i<=j} (A^L)^(j-i) v_i
-    double vp = 0.0, vv = 0.0;
-    if (tid + 1 < SPEC_T) yb[tid + 1] = d2v{zp, zv};
-    if (tid == 0) yb[0] = d2v{p1, v1};
-    __syncthreads();
-    if (tid < TE) { vp = yb[tid].x; vv = yb[tid].y; }
-    double Q00 = P00, Q01 = P01, Q10 = P10, Q11 = P11;
-    for (int o = 1; o < SPEC_T; o <<= 1) {
-      __syncthreads();
-      yb[tid] = d2v{vp, vv};
-      __syncthreads();
-      if (tid >= o && tid < TE) {
-        const d2v u = yb[tid - o];
-        vp = vp + (Q00 * u.x + Q01 * u.y);
-        vv = vv + (Q10 * u.x + Q11 * u.y);
+    // chunk starts y_j = Q^j x_1 + Y_{j-1}, Y_j = sum_{i<=j} Q^(j-i) z_i (Q = A^L): an inclusive
+    // scan of the z_i within each wave by shuffles (offset o combines with Q^o), then across the
+    // waves through their totals (Y at a wave's end = its total + Q^64 Y at the previous end)
+    const Mat2 Q{P00, P01, P10, P11};
+    double yp = tid < TE ? zp : 0.0, yv = tid < TE ? zv : 0.0;
+    {
+      Mat2 Qo = Q;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double up = __shfl_up(yp, o, 64), uv = __shfl_up(yv, o, 64);
+        if (lane >= o) {
+          yp = yp + (Qo.a * up + Qo.b * uv);
+          yv = yv + (Qo.c * up + Qo.d * uv);
+        }
+        Qo = mmul(Qo, Qo);
       }
-      const double n00 = Q00 * Q00 + Q01 * Q10, n01 = Q00 * Q01 + Q01 * Q11;
-      const double n10 = Q10 * Q00 + Q11 * Q10, n11 = Q10 * Q01 + Q11 * Q11;
-      Q00 = n00; Q01 = n01; Q10 = n10; Q11 = n11;
+      if (lane == 63) wsum[wv] = d2v{yp, yv};
+      __syncthreads();
+      // Y at the end of the previous wave, then Q^(lane+1) of it
+      const Mat2 Q64 = Qo;                         // Q^64 after the six squarings
+      double cp = 0.0, cv = 0.0;
+      for (int i = 0; i < wv; ++i) {
+        const double np = wsum[i].x + (Q64.a * cp + Q64.b * cv), nv = wsum[i].y + (Q64.c * cp + Q64.d * cv);
+        cp = np; cv = nv;
+      }
+      const Mat2 Ql = mpow2(Q, lane + 1);
+      yp = yp + (Ql.a * cp + Ql.b * cv);
+      yv = yv + (Ql.c * cp + Ql.d * cv);
+      __syncthreads();                             // wsum read before the next round writes it
     }
+    // Y_{j-1}: the previous lane's (lane 0: the previous wave's last, via LDS)
+    double vp = __shfl_up(yp, 1, 64), vv = __shfl_up(yv, 1, 64);
+    if (lane == 63) yb[wv] = d2v{yp, yv};
+    __syncthreads();
+    if (lane == 0) {
+      if (wv > 0) { vp = yb[wv - 1].x; vv = yb[wv - 1].y; }
+      else { vp = 0.0; vv = 0.0; }
+    }
+    {
+      const Mat2 Qj = mpow2(Q, tid);               // Q^j x_1
+      vp = vp + (Qj.a * p1 + Qj.b * v1);
+      vv = vv + (Qj.c * p1 + Qj.d * v1);
+    }
+    __syncthreads();                             // yb read before it is reused
     // 3. check: the true step from y_j
     bool miss = false;
     double p = vp, V = vv;
     for (int64_t k = k0; k < k1; ++k) {
-      const double c = cl[k - 1];
+      const double c = cl[own(k)];
       const double t = fma(-kInv2Pi, p, c);
       const double r = rel_of(t, c);
-      miss |= r != (double)mrel[k - 1];          // (out of a byte's range: a miss, and so on)
-      mrel[k - 1] = (int8_t)(r >= -127.0 && r <= 127.0 ? r : 0.0);
+      miss |= r != (double)mrel[own(k)];         // (out of a byte's range: a miss, and so on)
+      mrel[own(k)] = (int8_t)(r >= -127.0 && r <= 127.0 ? r : 0.0);
       const double f = __builtin_amdgcn_fract(t);
       const double S = p + V;
       V = fma(kA, f, V - kB);
@@ -799,7 +858,6 @@ __global__ __launch_bounds__(64) void pll_warm_kernel(PllJobs P) {
   const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
   const int64_t kend = (int64_t)b * pb;
   const int64_t k0 = max<int64_t>(1, kend - P.lg.warm[q]);
-  const float* xin = J.in + (int64_t)s * J.in_stride + k0;
   const int64_t nst = kend - k0;
   // seed: the phase the loop locks to, measured from the WARM_Z samples before the warm-up (a
   // locked loop keeps th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's phase, so
@@ -807,38 +865,48 @@ __global__ __launch_bounds__(64) void pll_warm_kernel(PllJobs P) {
   // chain finds the turns).  The integrator from the span's start.  (Extrapolating the start
   // phase by the integrator does not work: a locked loop balances its integrator with a
   // static phase error, so the estimate does not move by it -- 20 rad off across a span.)
+  const float* xr = J.in + (int64_t)s * J.in_stride;
   double p, V = st[0] - kD;
   {
     double zr = 0.0, zi = 0.0;
-    const float* xz = J.in + (int64_t)s * J.in_stride;
-    for (int64_t k = max<int64_t>(1, k0 - WARM_Z); k < k0; ++k) {
-      const double c = pll_c(xz[k], w, off0 + (double)k);
-      if (!(c == c)) continue;
-      const float a = (float)(k2Pi * __builtin_amdgcn_fract((xz[k] > 0.f ? 0.5 : 1.0) - c));
-      float sa, ca;
-      __sincosf(a, &sa, &ca);
-      zr += (double)(xz[k] * ca);
-      zi -= (double)(xz[k] * sa);
+    const int64_t z0 = max<int64_t>(1, k0 - WARM_Z);
+    for (int64_t kg = z0; kg < k0; kg += WARM_G) {
+      float xv[WARM_G];
+#pragma unroll
+      for (int i = 0; i < WARM_G; ++i) xv[i] = kg + i < k0 ? xr[kg + i] : 0.f;   // all loads first
+#pragma unroll
+      for (int i = 0; i < WARM_G; ++i) {
+        const double c = pll_c(xv[i], w, off0 + (double)(kg + i));
+        if (!(c == c)) continue;                 // 0 (also the padding past k0) / NaN
+        const float a = (float)(k2Pi * __builtin_amdgcn_fract((xv[i] > 0.f ? 0.5 : 1.0) - c));
+        float sa, ca;
+        __sincosf(a, &sa, &ca);
+        zr += (double)(xv[i] * ca);
+        zi -= (double)(xv[i] * sa);
+      }
     }
     p = (zr != 0.0 || zi != 0.0) ? atan2(zi, zr) : st[1];
   }
+  // the warm-up: raw inputs WARM_G at a time, two groups ahead; constants computed at use
+  const float* xin = xr + k0;
   const int64_t ng = (nst + WARM_G - 1) / WARM_G;
-  auto ld = [&](double (&v)[WARM_G], int64_t g) {
+  auto ld = [&](float (&v)[WARM_G], int64_t g) {
 #pragma unroll
     for (int i = 0; i < WARM_G; ++i) {
       const int64_t k = g * WARM_G + i;
-      v[i] = (g < ng && k < nst) ? pll_c(xin[k], w, off0 + (double)(k0 + k)) : __builtin_nan("");
+      v[i] = (g < ng && k < nst) ? xin[k] : 0.f;
     }
   };
-  double c0[WARM_G], c1[WARM_G], c2[WARM_G];
+  float c0[WARM_G], c1[WARM_G], c2[WARM_G];
   ld(c0, 0);
   ld(c1, 1);
   for (int64_t g = 0; g < ng; ++g) {
     ld(c2, g + 2);
 #pragma unroll
     for (int i = 0; i < WARM_G; ++i) {
-      const double c = c0[i];
-      if (c == c) {                              // NaN: past the end, or a 0 / NaN input (skipped)
+      const int64_t k = g * WARM_G + i;
+      const double c = pll_c(c0[i], w, off0 + (double)(k0 + k));
+      if (k < nst && c == c) {                   // past the end, or a 0 / NaN input: skipped
         const double t = fma(-kInv2Pi, p, c);
         const double f = __builtin_amdgcn_fract(t);
         const double S = p + V;
@@ -967,13 +1035,10 @@ __global__ __launch_bounds__(FIX_T) void pll_long_fix_kernel(PllJobs P) {
   const double wf = 2.0 * kPi * (cfg.freq / cfg.fs);
   const double offb = LB->x[5];
   const double a00 = 1.0 - (k2Pi * (cfg.kp + cfg.ki)) * kInv2Pi, a10 = -(k2Pi * cfg.ki) * kInv2Pi;
-  const int64_t per = (n + FIX_T - 1) / FIX_T;
-  const int64_t ka = min<int64_t>((int64_t)tid * per, n), kb = min<int64_t>(ka + per, n);
-  // A^ka d: the correction of the state before step ka
-  double vp = dp, vv = dv;
-  {
+  // thread t takes steps t, t + FIX_T, ... (coalesced); its corrections step by M = A^FIX_T
+  auto apply_pow = [&](int64_t e, double& vp, double& vv) {   // (vp, vv) = A^e (vp, vv)
     double M00 = a00, M01 = 1.0, M10 = a10, M11 = 1.0;
-    for (int64_t e = ka; e > 0; e >>= 1) {
+    for (; e > 0; e >>= 1) {
       if (e & 1) {
         const double np = M00 * vp + M01 * vv, nv = M10 * vp + M11 * vv;
         vp = np; vv = nv;
@@ -982,31 +1047,47 @@ __global__ __launch_bounds__(FIX_T) void pll_long_fix_kernel(PllJobs P) {
       const double n10 = M10 * M00 + M11 * M10, n11 = M10 * M01 + M11 * M11;
       M00 = n00; M01 = n01; M10 = n10; M11 = n11;
     }
+  };
+  double S00 = 1.0, S01 = 0.0, S10 = 0.0, S11 = 1.0;              // M = A^FIX_T
+  {
+    double c0p = 1.0, c0v = 0.0, c1p = 0.0, c1v = 1.0;
+    apply_pow(FIX_T, c0p, c0v);
+    apply_pow(FIX_T, c1p, c1v);
+    S00 = c0p; S10 = c0v; S01 = c1p; S11 = c1v;
   }
-  // the phase before step ka as solved (read before any thread rewrites the row)
-  double prev = ka > 0 && ka < kb ? th[ka - 1] : 0.0;
-  __syncthreads();
-  bool bad = false;
   const double tol = 1e-6;
-  for (int64_t k = ka; k < kb; ++k) {
-    if (k == 0) {                                // the literal step: atan2 of the start's (fI, fQ)
-      const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
-      const double offp = LB->x[5] - (double)P.lg.pb;
-      const double arg = w * ((offp + (double)(P.lg.pb - 1)) + 1.0) + LB->u[1];
-      const double xv = (double)J.in[(int64_t)s * J.in_stride + base];
-      const double e = atan2(xv * (-sin(arg)), xv * cos(arg));
-      bad |= !(fabs(e - vp) < kPi - tol);
-    } else {
-      const double t = fma(-kInv2Pi, prev, pll_c(xin[k], wf, offb + (double)k));
-      const double f = t - floor(t) - vp * kInv2Pi;
-      bad |= !(f > tol && f < 1.0 - tol);
+  bool bad = false;
+  {
+    // check: the correction of the phase before step k moves fract(t_k) inside (0, 1)
+    double vp = dp, vv = dv;
+    apply_pow(tid, vp, vv);                                       // before step tid
+    for (int64_t k = tid; k < n; k += FIX_T) {
+      if (k == 0) {                              // the literal step: atan2 of the start's (fI, fQ)
+        const double offp = offb - (double)P.lg.pb;
+        const double arg = wf * ((offp + (double)(P.lg.pb - 1)) + 1.0) + LB->u[1];
+        const double xv = (double)xin[0];
+        const double e = atan2(xv * (-sin(arg)), xv * cos(arg));
+        bad |= !(fabs(e - vp) < kPi - tol);
+      } else {
+        const double t = fma(-kInv2Pi, th[k - 1], pll_c(xin[k], wf, offb + (double)k));
+        const double f = t - floor(t) - vp * kInv2Pi;
+        bad |= !(f > tol && f < 1.0 - tol);
+      }
+      const double np = S00 * vp + S01 * vv, nv = S10 * vp + S11 * vv;
+      vp = np; vv = nv;
     }
-    const double np = a00 * vp + vv, nv = a10 * vp + vv;
-    vp = np; vv = nv;
-    prev = th[k];
-    th[k] = fma(nsh, kP1, fma(nsh, kP2, prev)) + vp;
   }
   if (__syncthreads_or(bad)) return;             // the spec kernel re-solves it from x
+  {
+    // apply: theta_k += 2 pi n + (A^(k+1) d)_phase
+    double vp = dp, vv = dv;
+    apply_pow(tid + 1, vp, vv);
+    for (int64_t k = tid; k < n; k += FIX_T) {
+      th[k] = fma(nsh, kP1, fma(nsh, kP2, th[k])) + vp;
+      const double np = S00 * vp + S01 * vv, nv = S10 * vp + S11 * vv;
+      vp = np; vv = nv;
+    }
+  }
   if (tid == 0) {
     const double* ph = (b == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
     LB->e[1] = fma(nsh, kP1, fma(nsh, kP2, LB->e[1])) + (ph[0] * dp + ph[1] * dv);
@@ -1017,15 +1098,18 @@ __global__ __launch_bounds__(FIX_T) void pll_long_fix_kernel(PllJobs P) {
   }
 }
 
-// 3. The chain: one wave per recurrence.  A window of pseudo-block records is staged in LDS
-// by all lanes; the walk over it is serial (every lane runs it alike; lane 0 publishes); the
-// decisions are written back by all lanes.
-constexpr int CHAIN_WIN = 256;
+// 3. The chain: one wave per recurrence, one lane per pseudo-block of a 64-block window (the
+// windows in order).  With A_j the start block j's current solution was solved from, E_j its
+// end and S_j the chained start, the residual R_j = S_j - A_j splits into n_j whole turns and
+// rho_j = R_j - 2 pi n_j, and
+//     R_{j+1} = (E_j - A_{j+1}) + 2 pi n_j + Phi_j rho_j.
+// |Phi_j| <= 2e-9 (the loop matrix over a pseudo-block), so the turns are a prefix sum of the
+// local integers rint((E_j - A_{j+1})_phase / 2 pi), and rho_{j+1} = C_j + Phi_j C_{j-1} to f64
+// rounding (C_j = E_j - A_{j+1} less its turns; the term after is Phi^2 ~ 1e-18 rad).  Then per
+// block the bound err = c1 |rho_p| + c2 |rho_v| decides, as described above; a prefix of
+// accepted blocks moves the chain's position.
 __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round) {
 #pragma clang fp contract(off)
-  __shared__ double gp[CHAIN_WIN], gi[CHAIN_WIN], xp[CHAIN_WIN], xi[CHAIN_WIN], ep[CHAIN_WIN], ei[CHAIN_WIN];
-  __shared__ double osp[CHAIN_WIN], osi[CHAIN_WIN], osh[CHAIN_WIN], oerr[CHAIN_WIN];
-  __shared__ int stt[CHAIN_WIN], act[CHAIN_WIN];
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   const int nb = P.lg.nb;
@@ -1040,93 +1124,116 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
   double* st = J.state + (int64_t)s * 6;
   const double off0 = st[5];
   const int64_t pb = P.lg.pb;
-  double Sp = H->sp, Si = H->si;       // the walk's state: exact while `exact`
-  double Xp = Sp, Xi = Si;             // the exact state at the new position
+  double Cp = H->sp, Ci = H->si;     // the carried (chained) start of the window's first block
+  bool cexact = true;                // ... exact (else provisional)
   int pos = pos0;
-  bool exact = true, stop = false;
-  for (int w0 = pos0; w0 < nb && !stop; w0 += CHAIN_WIN) {
-    const int nw = min(CHAIN_WIN, nb - w0);
-    for (int j = lane; j < nw; j += 64) {
-      const LongBlk* B = long_blk(P, r, w0 + j);
-      gp[j] = B->g[1]; gi[j] = B->g[0];
-      xp[j] = B->x[1]; xi[j] = B->x[0];
-      ep[j] = B->e[1]; ei[j] = B->e[0];
-      stt[j] = B->status;
-      act[j] = 0;
-    }
-    __syncthreads();
-    int j = 0;
-    for (; j < nw; ++j) {
-      const int sj = stt[j];
-      if (sj != LB_DONE_G && sj != LB_DONE_X) { stop = true; break; }   // not solved this round
+  double Xp = Cp, Xi = Ci;           // the exact state at `pos`
+  for (int w0 = pos0; w0 < nb; w0 += 64) {
+    const int j = w0 + lane;
+    const bool valid = j < nb;
+    // this block's start, end and status; the next block's start
+    int sj = -1;
+    double ap = 0.0, ai = 0.0, ep = 0.0, ei = 0.0, anp = 0.0, ani = 0.0;
+    int solver = 0;
+    if (valid) {
+      const LongBlk* B = long_blk(P, r, j);
+      sj = B->status;
       const bool fromg = sj == LB_DONE_G;
-      const double d = Sp - (fromg ? gp[j] : xp[j]);
-      const double nsh = fromg ? rint(d * kInv2Pi) : 0.0;
-      const double dp = fma(-nsh, kP2, fma(-nsh, kP1, d));             // d - 2 pi n
-      const double dv = Si - (fromg ? gi[j] : xi[j]);
-      const double err = c1 * fabs(dp) + c2 * fabs(dv);
-      oerr[j] = err;
-      osh[j] = nsh;
-      const double eps = fma(nsh, kP1, fma(nsh, kP2, ep[j]));           // e + 2 pi n
-      if (err <= LONG_ACCEPT) {
-        Sp = eps;
-        Si = ei[j];
-        if (exact) {
-          act[j] = 1;
-          pos = w0 + j + 1;
-          Xp = Sp;
-          Xi = Si;
-        }
-        continue;
-      }
-      act[j] = 2;                                                      // re-solve from (Sp, Si)
-      osp[j] = Sp;
-      osi[j] = Si;
-      exact = false;
-      if (!(err <= LONG_LINEAR)) {                                     // (a NaN also stops here)
-#ifdef SDR_PLL_LONG_DEBUG
-        if (lane == 0)
-          printf("chain r%d b%d/%d status %d: err %.3e dp %.3e dv %.3e n %.0f (S %.6f %.3e, guess %.6f %.3e)\n", r,
-                 w0 + j, nb, sj, err, dp, dv, nsh, Sp, Si, fromg ? gp[j] : xp[j], fromg ? gi[j] : xi[j]);
-#endif
-        act[j] = 3;
-        ++j;
-        stop = true;
-        break;
-      }
-      const double* ph = (w0 + j == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
-      Sp = eps + (ph[0] * dp + ph[1] * dv);
-      Si = ei[j] + (ph[2] * dp + ph[3] * dv);
+      ap = fromg ? B->g[1] : B->x[1];
+      ai = fromg ? B->g[0] : B->x[0];
+      ep = B->e[1];
+      ei = B->e[0];
+      solver = B->solver;
     }
-    __syncthreads();
-    for (int k = lane; k < j; k += 64) {
-      const int bi = w0 + k;
-      LongBlk* B = long_blk(P, r, bi);
-      if (act[k] == 1) {
+    const bool solved = valid && (sj == LB_DONE_G || sj == LB_DONE_X);
+    anp = __shfl_down(ap, 1, 64);
+    ani = __shfl_down(ai, 1, 64);
+    if (lane == 63 && j + 1 < nb) {                 // the next window's first block
+      const LongBlk* B = long_blk(P, r, j + 1);
+      const bool fromg = B->status == LB_DONE_G;
+      anp = fromg ? B->g[1] : B->x[1];
+      ani = fromg ? B->g[0] : B->x[0];
+    }
+    const double* ph = (j == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
+    // C_j = E_j - A_{j+1} less its turns (this lane's outgoing step)
+    const double cd = ep - anp;
+    const double dn = rint(cd * kInv2Pi);
+    const double cp = fma(-dn, kP2, fma(-dn, kP1, cd));
+    const double cv = ei - ani;
+    // lane 0's residual from the carried start
+    const double d0 = Cp - __shfl(ap, 0, 64);
+    const double n0 = rint(d0 * kInv2Pi);
+    const double r0p = fma(-n0, kP2, fma(-n0, kP1, d0)), r0v = Ci - __shfl(ai, 0, 64);
+    // rho_j: lane 0 the carried one; lane l: C_{l-1} + Phi_{l-1} C_{l-2} (lane 1: ... rho_0)
+    const double pcp = __shfl_up(cp, 1, 64), pcv = __shfl_up(cv, 1, 64);     // C_{l-1}
+    const double ppcp = __shfl_up(cp, 2, 64), ppcv = __shfl_up(cv, 2, 64);   // C_{l-2}
+    const double f0 = __shfl_up(ph[0], 1, 64), f1 = __shfl_up(ph[1], 1, 64); // Phi_{l-1}
+    const double f2 = __shfl_up(ph[2], 1, 64), f3 = __shfl_up(ph[3], 1, 64);
+    double rp, rv;
+    if (lane == 0) { rp = r0p; rv = r0v; }
+    else {
+      const double qp = lane == 1 ? r0p : ppcp, qv = lane == 1 ? r0v : ppcv;
+      rp = pcp + (f0 * qp + f1 * qv);
+      rv = pcv + (f2 * qp + f3 * qv);
+    }
+    // whole turns: n_0 from the carry, then the prefix sum of the outgoing integers
+    const double nj = n0 + (wave_prefix_sum(dn, lane) - dn);
+    const double err = c1 * fabs(rp) + c2 * fabs(rv);
+    const bool acc = solved && err <= LONG_ACCEPT;
+    const bool lin = solved && err <= LONG_LINEAR;   // (a NaN fails both)
+    const uint64_t notacc = __ballot(!acc);          // (invalid lanes are never accepted)
+    const uint64_t notlin = __ballot(!lin);
+    const int fa = notacc ? __builtin_ctzll(notacc) : 64;    // accepted prefix (if the carry is exact)
+    const int fs = notlin ? __builtin_ctzll(notlin) : 64;    // the first block the chain cannot pass
+    const int nacc = cexact ? fa : 0;
+    // this block's chained start S_j = A_j + 2 pi n_j + rho_j (exact for lanes <= nacc)
+    const double sp = fma(nj, kP1, fma(nj, kP2, ap)) + rp, si = ai + rv;
+    if (valid && lane <= fs) {
+      LongBlk* B = long_blk(P, r, j);
+      if (lane < nacc) {
         B->status = LB_ACCEPTED;
-        B->shift = osh[k];
-        const int sv = B->solver;
+        B->shift = nj;
         stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
-        stat_add(P.stats, sv == SOLVER_SEQ ? SDR_PLL_ST_SEQUENTIAL : SDR_PLL_ST_SPEC_R0 + sv, 1);
-        stat_add(P.stats, stt[k] == LB_DONE_G ? SDR_PLL_ST_LONG_GUESSED : SDR_PLL_ST_LONG_CHAINED, 1);
-        stat_max(P.stats, SDR_PLL_ST_LONG_MAXGAP, oerr[k]);
-      } else if (act[k] >= 2) {
-        if (act[k] == 3) stat_add(P.stats, SDR_PLL_ST_LONG_STOPS, 1);
-        B->u[0] = stt[k] == LB_DONE_G ? gi[k] : xi[k];                 // the start of the current solution
-        B->u[1] = stt[k] == LB_DONE_G ? gp[k] : xp[k];
-        const double offp = off0 + (double)((int64_t)(bi - 1) * pb);
-        const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + osp[k];
-        B->x[0] = osi[k];
-        B->x[1] = osp[k];
+        stat_add(P.stats, solver == SOLVER_SEQ ? SDR_PLL_ST_SEQUENTIAL : SDR_PLL_ST_SPEC_R0 + solver, 1);
+        stat_add(P.stats, sj == LB_DONE_G ? SDR_PLL_ST_LONG_GUESSED : SDR_PLL_ST_LONG_CHAINED, 1);
+        stat_max(P.stats, SDR_PLL_ST_LONG_MAXGAP, err);
+      } else if (!acc && solved) {                    // re-solve from the chained start
+        if (lane == fs) stat_add(P.stats, SDR_PLL_ST_LONG_STOPS, 1);
+#ifdef SDR_PLL_LONG_DEBUG
+        if (lane == fs)
+          printf("chain r%d b%d/%d status %d: err %.3e rho %.3e %.3e n %.0f\n", r, j, nb, sj, err, rp, rv, nj);
+#endif
+        B->u[0] = ai;
+        B->u[1] = ap;
+        const double offp = off0 + (double)((int64_t)(j - 1) * pb);
+        const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + sp;
+        B->x[0] = si;
+        B->x[1] = sp;
         B->x[2] = cos(arg);
         B->x[3] = sin(arg);
         B->x[4] = 0.0;
-        B->x[5] = off0 + (double)((int64_t)bi * pb);
+        B->x[5] = off0 + (double)((int64_t)j * pb);
         B->shift = 0.0;
         B->status = LB_NEED_X;
       }
     }
-    __syncthreads();
+    // the state after the accepted prefix; the carry into the next window
+    if (nacc > 0) {
+      const int l = nacc - 1;
+      const double ep_l = __shfl(ep, l, 64), ei_l = __shfl(ei, l, 64), n_l = __shfl(nj, l, 64);
+      Xp = fma(n_l, kP1, fma(n_l, kP2, ep_l));
+      Xi = ei_l;
+      pos = w0 + nacc;
+    }
+    if (fs < 64 || w0 + 64 >= nb) break;              // the chain cannot pass block fs this round
+    // carry: S_{w0+64} = E_63 + 2 pi n_63 + Phi_63 rho_63
+    const double e63p = __shfl(ep, 63, 64), e63i = __shfl(ei, 63, 64), n63 = __shfl(nj, 63, 64);
+    const double r63p = __shfl(rp, 63, 64), r63v = __shfl(rv, 63, 64);
+    const double g0 = __shfl(ph[0], 63, 64), g1 = __shfl(ph[1], 63, 64), g2 = __shfl(ph[2], 63, 64),
+                 g3 = __shfl(ph[3], 63, 64);
+    Cp = fma(n63, kP1, fma(n63, kP2, e63p)) + (g0 * r63p + g1 * r63v);
+    Ci = e63i + (g2 * r63p + g3 * r63v);
+    cexact = cexact && fa == 64;
   }
 #ifdef SDR_PLL_LONG_DEBUG
   if (lane == 0) printf("chain r%d round %d: position %d -> %d of %d\n", r, round, pos0, pos, nb);
@@ -1244,8 +1351,11 @@ __global__ void nco_jobs_kernel(PllJobs P) {
   }
   const double th = w * ((off + (double)k) + 1.0) + p;
   const double a = th * J.cfg.scale + J.cfg.adj;
+  // the reference's angle grows with the stream (~1e7 rad after a minute): reduced here by the
+  // 3-part Cody-Waite step (exact multiples of 2 pi for |n| < 2^26), sincos then takes its
+  // small-argument path instead of the large-argument reduction
   double sv, cv;
-  sincos(a, &sv, &cv);
+  sincos(reduce_2pi(a), &sv, &cv);
   J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
   if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
 }
@@ -1329,19 +1439,20 @@ void loop_bounds(const PllCfg& c, double* c1, double* c2) {
   *c2 = m2;
 }
 
-// warm-up length: the error contracts by sqrt(1 - Kp) per step; enough steps to bring a
-// start error of pi within LONG_ACCEPT, capped (SDR_PLL_WARM_MAX, default 2560: the stereo loop
-// needs ~1 800; the RDS loop would need ~17 000, and its blocks are re-solved from the chained
-// start instead, for which a start within the linear bound is enough)
+// warm-up length: the error contracts by sqrt(1 - Kp) per step; enough steps to bring the seed's
+// error (the measured phase: ~0.1 rad) within LONG_ACCEPT (the stereo loop: ~1 500), unless
+// that exceeds SDR_PLL_WARM_MAX (default 2 048: the RDS loop would need ~15 000) -- then 1 024
+// steps, enough for the linear bound; such blocks are fixed up from the chained start.
 int warm_len(const PllCfg& c, double c1, int64_t pb) {
   static const int cap = [] {
     const char* e = getenv("SDR_PLL_WARM_MAX");
-    return e ? std::max(64, atoi(e)) : 2560;
+    return e ? std::max(64, atoi(e)) : 2048;
   }();
   const double rate = -0.5 * std::log1p(-std::min(std::max(c.kp, 1e-12), 0.999));
-  const double want = std::log(std::max(c1, 1.0) * M_PI / LONG_ACCEPT) / rate;
+  const double want = std::log(std::max(c1, 1.0) * 0.1 / LONG_ACCEPT) / rate;   // from a 0.1 rad seed
   int64_t wl = (int64_t)std::ceil(want / 256.0) * 256;
-  wl = std::min<int64_t>(std::min<int64_t>(wl, cap), 4 * pb);
+  if (wl > cap) wl = 1024;            // cannot reach the acceptance bound: enough for the linear one
+  wl = std::min<int64_t>(wl, pb / 2);
   return (int)std::max<int64_t>(wl, 64);
 }
 

@@ -254,20 +254,48 @@ __device__ __forceinline__ void fir_tile_any(const StageJob& J, int s, int64_t t
 // (D m - k) % U == 0 contribute; the input index walks down by one per term).
 __device__ __forceinline__ void resample_tile(const StageJob& J, int s, int64_t tile, float* lds) {
   const int t = threadIdx.x;
-  for (int k = t; k < J.T; k += RX_NT) lds[k] = J.taps[k];
-  __syncthreads();
   const int U = J.U, D = J.D;
   const int64_t M = (J.n * U + D - 1) / D;
   const float* xb = J.x + (int64_t)s * J.x_stride;
+  // the tile's input window (outputs [m0, m0 + RX_TO) read x[(D m - k) / U] for k < T) and the
+  // taps, staged in LDS: each output is ~T/U multiply-adds, so the tile is bound by how fast its
+  // inputs arrive, not by arithmetic
+  const int64_t m0 = tile * RX_TO;
+  const int64_t xlo = max<int64_t>(0, (D * m0 - (J.T - 1)) / U - 1);
+  const int64_t xhi = min<int64_t>(J.n, (D * (m0 + RX_TO - 1)) / U + 1);
+  const int nx = (int)max<int64_t>(0, xhi - xlo);
+  float* tap = lds;
+  float* xs = lds + SDR_MAX_TAPS;
+  if (J.T <= SDR_MAX_TAPS && nx <= RX_LDS - SDR_MAX_TAPS) {
+    for (int k = t; k < J.T; k += RX_NT) tap[k] = J.taps[k];
+    for (int i = t; i < nx; i += RX_NT) xs[i] = xb[xlo + i];
+    __syncthreads();
+    for (int r = 0; r < RX_R; ++r) {
+      const int64_t m = m0 + t + RX_NT * r;
+      if (m >= M) break;
+      const int64_t j0 = (int64_t)D * m;
+      const int k0 = (int)(j0 % U);
+      const int khi = (int)min<int64_t>(J.T - 1, j0);
+      int xi = (int)((j0 - k0) / U - xlo);
+      float acc = 0.f;
+      for (int k = k0; k <= khi; k += U, --xi) acc = fmaf(tap[k], xs[xi], acc);
+      if (J.zi != nullptr && j0 < J.T - 1) acc += (float)J.zi[(int64_t)s * J.zi_stride + j0];
+      J.y[(int64_t)s * J.y_stride + m] = acc * (float)U;
+      if (J.yh) J.yh[(int64_t)s * J.yh_stride + m] = acc * (float)U;
+    }
+    return;
+  }
+  for (int k = t; k < J.T; k += RX_NT) lds[k] = J.taps[k];     // (taps beyond the LDS window: through the caches)
+  __syncthreads();
   for (int r = 0; r < RX_R; ++r) {
-    const int64_t m = tile * RX_TO + t + RX_NT * r;
+    const int64_t m = m0 + t + RX_NT * r;
     if (m >= M) break;
     const int64_t j0 = (int64_t)D * m;
     const int k0 = (int)(j0 % U);
     const int khi = (int)min<int64_t>(J.T - 1, j0);
     int64_t xi = (j0 - k0) / U;
     float acc = 0.f;
-    for (int k = k0; k <= khi; k += U, --xi) acc = fmaf(lds[k], xb[xi], acc);
+    for (int k = k0; k <= khi; k += U, --xi) acc = fmaf(k < RX_LDS ? lds[k] : J.taps[k], xb[xi], acc);
     if (J.zi != nullptr && j0 < J.T - 1) acc += (float)J.zi[(int64_t)s * J.zi_stride + j0];
     J.y[(int64_t)s * J.y_stride + m] = acc * (float)U;
     if (J.yh) J.yh[(int64_t)s * J.yh_stride + m] = acc * (float)U;

@@ -85,7 +85,8 @@ def test_live_pipeline_mode1(sdr, gpu_ctx, oracle):
     from scipy import signal
     nb = 3
     iq = sdr.synth.fm_iq(nb * B, seed=14, fs=2.5e6, dtype=np.uint8)
-    res = subprocess.run([BIN, "--mode", "1"], input=iq.tobytes(), capture_output=True, check=True, timeout=120)
+    res = subprocess.run([BIN, "--mode", "1", "--mono"], input=iq.tobytes(), capture_output=True, check=True,
+                         timeout=120)
     pcm = np.frombuffer(res.stdout, dtype=np.int16)
     A = (B // 10) * 24 // 125
     assert pcm.shape == (nb * 2 * A,)
@@ -112,6 +113,29 @@ def test_live_pipeline_mode1(sdr, gpu_ctx, oracle):
     o = np.concatenate(ora)
     dd = np.abs(pcm.astype(np.int32) - to_pcm(o, o))
     assert dd.max() <= 1 and np.mean(dd > 0) < 0.01
+
+
+@pytest.mark.gpu
+def test_live_pipeline_mode1_stereo(sdr, gpu_ctx, oracle):
+    """--mode 1 stereo in its intended form (pilot BPF, fmPll at 19 kHz / Fs 250 kHz, stereo BPF,
+    mixer x2, the 24/125 resampler, L/R combiner) against oracle.mode1_stereo_blocks -- parity
+    UNPINNED: the reference's mode-1 stereo (src/fm_radio.cpp:231-252) is defective and not
+    restated.  int16 L/R within 1 LSB (<1 % of the samples off by one)."""
+    nb = 3
+    iq = sdr.synth.fm_iq(nb * B, seed=15, fs=2.5e6, dtype=np.uint8)
+    res = subprocess.run([BIN, "--mode", "1"], input=iq.tobytes(), capture_output=True, check=True, timeout=120)
+    pcm = np.frombuffer(res.stdout, dtype=np.int16)
+    A = (B // 10) * 24 // 125
+    assert pcm.shape == (nb * 2 * A,)
+    x = (iq.astype(np.float64) - 128.0) / 128.0
+    orc = oracle.mode1_stereo_blocks(x, B, nblocks=nb)
+    ref = np.concatenate([to_pcm(r["left"], r["right"]) for r in orc])
+    dd = np.abs(pcm.astype(np.int32) - ref)
+    print(f"mode-1 stereo int16: max |diff| {dd.max()}, {np.mean(dd > 0) * 100:.3f} % off by one")
+    assert dd.max() <= 1 and np.mean(dd > 0) < 0.01
+    # the channels separate: L and R differ by the stereo channel, which carries real signal
+    left, right = pcm[0::2].astype(np.float64), pcm[1::2].astype(np.float64)
+    assert np.sqrt(np.mean((left - right) ** 2)) > 0.05 * np.sqrt(np.mean(left ** 2))
 
 
 def _syndrome_lines(stderr):
