@@ -438,12 +438,18 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 // recurrence is marked by c[0] = +inf (c[0] is the literal sample's slot: the loop kernels
 // never read it, and the prep kernel rewrites it every call).
 constexpr int SPEC_W = 256;          // warm-up samples before each chunk
-constexpr int SPEC_W_LONG = 64;      // ... in a long call's pseudo-block (its start is a converged
-                                     //     guess or the chained state, its drift measured)
+#ifndef SDR_SPEC_W_LONG
+#define SDR_SPEC_W_LONG 16
+#endif
+// ... in a long call's pseudo-block: its start is a converged guess or the chained state and
+// its drift is measured, so the guess needs little settling (r03 A/B on the S8 K256 span: 0,
+// 16, 32 and 64 steps all solve every pseudo-block in round 0; 16 is the fastest)
+constexpr int SPEC_W_LONG = SDR_SPEC_W_LONG;
 constexpr int SPEC_IT = 3;           // solve / check rounds before the sequential kernel takes over
-constexpr int SPEC_NMAX = SDR_PLL_BLOCK_MAX; // samples per call (the constants of steps 1.. in LDS: 128 KiB)
+constexpr int SPEC_NMAX = SDR_PLL_BLOCK_MAX; // samples per call (the sign codes of steps 1.. in LDS: 16 KiB)
 static_assert(SPEC_NMAX == 16384 + 1, "LDS sizing");
-constexpr int SPEC_LDS = 32 * 513;           // padded transposed image: 512 chunks of <= 32 steps (or 256 of <= 40)
+constexpr int SPEC_LDS = 32 * 513;           // padded transposed bytes: 512 chunks of <= 32 steps (or 256 of <= 40)
+constexpr int SB = 8;                        // steps per batch of LDS reads in the step loops
 
 // ---- long calls: pseudo-block bookkeeping (device scratch P.work) --------------------
 // Per recurrence r = job * nstreams + stream: a header (the chain's position and the exact
@@ -493,16 +499,24 @@ __device__ __forceinline__ Mat2 mpow2(Mat2 x, int e) {
 // LB_NEED_G) or its chained start (LB_NEED_X); the end state goes to the block's record and
 // the call's own state, trigOffset slot and NCO[0] are left to the long-call kernels.
 template <int SPEC_T, bool LONG>
-__global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
+__global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(4))) void pll_spec_kernel(PllJobs P) {
 #pragma clang fp contract(off)
-  // c_k of steps 1 .. n-1 (plain form) and m_k - floor(c_k) + jb (jb = floor(phaseEst_1 / 2pi)),
-  // step i of chunk j at i * CSTR + j (see the staging below)
-  constexpr int CSTR = SPEC_T + 1, NW = SPEC_T / 64;
-  __shared__ double cl[SPEC_LDS];
+  // Per step k = 1 .. n-1, at slot i * CSTR + j (step i of chunk j, see the staging below):
+  // the sign code of x_k (0: x > 0, 1: x < 0, 2: 0 / NaN) -- the constant c_k is a function
+  // of it and k alone (pll_c), recomputed where it is used, which keeps the workgroup's LDS
+  // at ~68 KB (two per CU) instead of a 128 KiB f64 image -- and m_k - floor(c_k) + jb
+  // (jb = floor(phaseEst_1 / 2pi)).  tb: per wave, SB steps x 64 chunks of phases on their
+  // way to coalesced theta stores (stride TBS = 4 mod 32 doubles: both its write and its
+  // transposed read are conflict-free); the chunk scans' scratch (yb) shares its space.
+  constexpr int CSTR = SPEC_T + 1, NW = SPEC_T / 64, TBS = 68;
+  static_assert(NW * SB * TBS >= 2 * SPEC_T, "yb fits in tb");
+  __shared__ int8_t code[SPEC_LDS];
   __shared__ int8_t mrel[SPEC_LDS];
-  __shared__ d2v yb[SPEC_T];
+  __shared__ double tb[NW * SB * TBS];
   __shared__ d2v wsum[NW];
+  __shared__ Mat2 qp[10];
   __shared__ double x1s[2];
+  d2v* yb = reinterpret_cast<d2v*>(tb);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int tid = threadIdx.x;
   int q, s, status = 0;
@@ -529,25 +543,30 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
   double* th = J.theta + (int64_t)s * J.th_stride + base;
   double* cr = J.cbuf + (int64_t)s * J.c_stride + base;
   const PllCfg cfg = J.cfg;
+#ifdef SDR_PLL_SPEC_PROF    // phase timers (diagnostic builds only, tools/build_dbg.sh)
+  long long tp[8];
+  int ntp = 0;
+  tp[ntp++] = clock64();
+#define SPEC_TP() do { if (ntp < 8) tp[ntp++] = clock64(); } while (0)
+#else
+#define SPEC_TP() do {} while (0)
+#endif
   double* st = LONG ? (status == LB_NEED_G ? LB->g : LB->x) : J.state + (int64_t)s * 6;
   double* st_out = LONG ? LB->e : st;
   const double off = st[5];
   const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
   const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
   const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
-  // the prep kernel's constants are in the Q-form when the chunk kernel is the loop kernel
-  auto cplain = [&](int64_t k) {
-    double c = cr[k];
-    if (P.qform) {
-      const double i = (double)(k % PG);
-      c = c - (kPi * cfg.ki) * kInv2Pi * (i * (i - 1.0) * 0.5);
-    }
-    return c;
-  };
   auto thval = [&](double ph, int64_t k) {       // what the theta row holds for step k
     if (!P.qform) return ph;
     const double i = (double)(k % PG);
     return ph + kB * ((i + 1.0) * i * 0.5);
+  };
+  // c_k from the sign code: pll_c's arithmetic exactly (the prep kernel's plain form)
+  auto cval = [&](int cd, int k) {
+    const double cc = (cd == 0 ? 0.0 : kPi) - w * (off + (double)k);
+    const double cv = fma(cc, kInv2Pi, 0.5);
+    return cd == 2 ? __builtin_nan("") : cv;
   };
   // sample 0: the literal general step (thread 0), as the loop kernels' general()
   if (tid == 0) {
@@ -558,31 +577,40 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
     x1s[0] = phase;
     x1s[1] = integ - kD;
   }
-  __syncthreads();
-  const double p1 = x1s[0], v1 = x1s[1];
-  const int64_t N = n - 1;                       // steps 1 .. n-1
-  const int L = (int)((N + SPEC_T - 1) / SPEC_T);
-  const int TE = (int)((N + L - 1) / L);         // chunks in use; chunks 0 .. TE-2 are full
-  const int64_t k0 = 1 + (int64_t)tid * L;
-  const int64_t k1 = tid < TE ? min<int64_t>(k0 + L, n) : k0;
-  // every step reads its constant several times: stage them (plain form) in LDS, transposed --
-  // step i of chunk j at i * CSTR + j -- so that the threads' per-step reads of their own
-  // chunks are consecutive (contiguous chunks put all 64 lanes of a ds_read_b64 on one bank at
-  // L = 32: a 64-way conflict on every step); the odd stride CSTR = SPEC_T + 1 keeps the
-  // coalesced staging writes (consecutive threads: consecutive i) conflict-free too
+  const int N = (int)n - 1;                      // steps 1 .. n-1
+  // chunk length: a multiple of SB (the step loops run in batches of SB, their LDS reads issued
+  // ahead of the dependent steps; a step past a chunk's end is computed and discarded)
+  const int L = (N + SPEC_T * SB - 1) / (SPEC_T * SB) * SB;
+  const int TE = (N + L - 1) / L;                // chunks in use; chunks 0 .. TE-2 are full
+  const int k0 = 1 + tid * L;
+  const int len = tid < TE ? min(L, (int)n - k0) : 0;   // steps of this thread's chunk
+  // stage the sign codes, transposed -- step i of chunk j at i * CSTR + j -- so that the
+  // threads' per-step reads of their own chunks are consecutive bytes; the global loads go
+  // out SG at a time before the first is used.  (Slots of steps past N hold whatever was
+  // there: only discarded steps read them, and every slot is in the array.)
   {
-    const double w1 = 2.0 * kPi * (cfg.freq / cfg.fs);
-    for (int kk = tid; kk < (int)N; kk += SPEC_T) {
-      const int j = kk / L, i = kk - j * L;
-      cl[i * CSTR + j] = LONG ? pll_c(in[kk + 1], w1, off + (double)(kk + 1)) : cplain(kk + 1);
+    constexpr int SG = 32;
+    for (int b0 = tid; b0 < N; b0 += SG * SPEC_T) {
+      float xv[SG];
+#pragma unroll
+      for (int u = 0; u < SG; ++u) xv[u] = b0 + u * SPEC_T < N ? in[b0 + u * SPEC_T + 1] : 0.f;
+#pragma unroll
+      for (int u = 0; u < SG; ++u) {
+        const int kk = b0 + u * SPEC_T;
+        if (kk < N) {
+          const int j = kk / L, i = kk - j * L;
+          code[i * CSTR + j] = (int8_t)(xv[u] > 0.f ? 0 : (xv[u] < 0.f ? 1 : 2));
+        }
+      }
     }
   }
   __syncthreads();
+  SPEC_TP();
+  const double p1 = x1s[0], v1 = x1s[1];
   // the integer part relative to floor(c_k) is floor(-phaseEst/2pi + frac(c_k)): near -jb
   // within a block, so it fits a byte once jb is taken off (a drifting phase estimate moves jb)
   const double jb = floor(kInv2Pi * p1);
   auto rel_of = [&](double t, double c) { return floor(t) - floor(c) + jb; };
-  auto own = [&](int64_t k) { return (int)(k - k0) * CSTR + tid; };     // LDS slot of own step k
   // 0. where the locked phase estimate goes within the block, measured from the input: a
   // locked loop keeps its angle th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's
   // phase, so z_j = sum over chunk j of x_k exp(-i w (off + k)) ~ (A/2) exp(i phaseEst) (+ an
@@ -593,17 +621,23 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
   // state alone, the RDS loop's 256-step warm-ups (contraction ~0.7) cannot catch it up.
   // Extrapolating by integ does worse: integ swings with the loop's own oscillation.)
   {
-    // sign(x_k) exp(-i w (off + k)) = exp(-i 2 pi fract(1/2 - c_k)) (c_k carries the sign):
-    // the constants alone, already in LDS (a hard-limited correlation, as the loop's detector)
+    // sign(x_k) exp(-i w (off + k)) = exp(-i 2 pi fract(1/2 - c_k)): a hard-limited
+    // correlation, as the loop's detector
     float zr = 0.f, zi = 0.f;
-    for (int64_t k = k0; k < k1; ++k) {
-      const double c = cl[own(k)];
-      if (!(c == c)) continue;                   // a 0 / NaN input (rejected below anyway)
-      const float a = (float)(k2Pi * __builtin_amdgcn_fract(0.5 - c));
-      float sa, ca;
-      __sincosf(a, &sa, &ca);
-      zr += ca;
-      zi -= sa;
+    for (int i0 = 0; i0 < L; i0 += SB) {
+      int cd[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) cd[u] = code[(i0 + u) * CSTR + tid];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const double c = cval(cd[u], k0 + i0 + u);
+        const float a = (float)(k2Pi * __builtin_amdgcn_fract(0.5 - c));
+        float sa, ca;
+        __sincosf(a, &sa, &ca);
+        const bool use = i0 + u < len && cd[u] != 2;   // (a 0 / NaN input is rejected below anyway)
+        zr += use ? ca : 0.f;
+        zi -= use ? sa : 0.f;
+      }
     }
     yb[tid] = d2v{(double)zr, (double)zi};
     __syncthreads();
@@ -630,118 +664,200 @@ __global__ __launch_bounds__(SPEC_T) void pll_spec_kernel(PllJobs P) {
     yb[tid].x = d;                               // D_j
     __syncthreads();
   }
+  SPEC_TP();
   // 1. guess
   bool bad = false;
   {
     // the true step from a seed on the measured drift: phaseEst ~ p1 + D at the warm-up's
     // start, integ ~ the measured drift per step; 256 steps of the loop then pull the guess
     // onto the trajectory
-    const int64_t kw = max<int64_t>(1, k0 - (LONG ? SPEC_W_LONG : SPEC_W));
-    const int jw = (int)((kw - 1) / L);
+    const int kw = max(1, k0 - (LONG ? SPEC_W_LONG : SPEC_W));
+    const int jw = (kw - 1) / L;
     double p = p1 + yb[jw].x, V = v1;
     if (k0 - kw >= 64 && tid < TE) V = (yb[tid].x - yb[jw].x) / (double)(k0 - kw) - kD;
-    int jc = jw, ic = (int)(kw - 1) - jw * L;     // (chunk, step) of step kw
-#pragma unroll 8
-    for (int64_t k = kw; k < k0 && tid < TE; ++k) {
-      const double t = fma(-kInv2Pi, p, cl[ic * CSTR + jc]);
-      if (++ic == L) { ic = 0; ++jc; }
-      const double f = __builtin_amdgcn_fract(t);
-      const double S = p + V;
-      V = fma(kA, f, V - kB);
-      p = fma(kC, f, S);
+    const int W = tid < TE ? k0 - kw : 0;        // warm-up steps (over the chunks before this one)
+    int jc = jw, ic = (kw - 1) - jw * L;         // (chunk, step) of step kw
+    for (int i0 = 0; i0 < W; i0 += SB) {
+      int cd[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {             // (past the warm-up: slots of this chunk, unused)
+        cd[u] = code[ic * CSTR + jc];
+        if (++ic == L) { ic = 0; ++jc; }
+      }
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const double t = fma(-kInv2Pi, p, cval(cd[u], kw + i0 + u));
+        const double f = __builtin_amdgcn_fract(t);
+        const double S = p + V;
+        const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
+        const bool act = i0 + u < W;
+        V = act ? nV : V;
+        p = act ? np : p;
+      }
     }
-    for (int64_t k = k0; k < k1; ++k) {
-      const double c = cl[own(k)];
-      const double t = fma(-kInv2Pi, p, c);
-      const double r = rel_of(t, c);
-      bad |= !(r >= -127.0 && r <= 127.0);       // also a NaN constant (a 0 / NaN input)
-      mrel[own(k)] = (int8_t)(bad ? 0.0 : r);
-      const double f = __builtin_amdgcn_fract(t);
-      const double S = p + V;
-      V = fma(kA, f, V - kB);
-      p = fma(kC, f, S);
+    __syncthreads();                             // yb (D_j) read before tb reuses its space
+    for (int i0 = 0; i0 < L; i0 += SB) {
+      int cd[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) cd[u] = code[(i0 + u) * CSTR + tid];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int i = i0 + u;
+        const double c = cval(cd[u], k0 + i);
+        const double t = fma(-kInv2Pi, p, c);
+        const double r = rel_of(t, c);
+        const bool act = i < len;
+        bad |= act && !(r >= -127.0 && r <= 127.0);  // also a NaN constant (a 0 / NaN input)
+        if (act) mrel[i * CSTR + tid] = (int8_t)(bad ? 0.0 : r);
+        const double f = __builtin_amdgcn_fract(t);
+        const double S = p + V;
+        const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
+        V = act ? nV : V;
+        p = act ? np : p;
+      }
     }
   }
   if (__syncthreads_or(bad)) return;             // a 0 / NaN input (the general form's case)
-  // A^L and its squarings (every thread the same operations)
+  SPEC_TP();
+  // Q = A^L and its squarings Q^(2^i), i < 10 (thread 0, into LDS: the scans read them as
+  // broadcasts instead of holding them in registers)
   const double a00 = 1.0 - kC * kInv2Pi, a10 = -kA * kInv2Pi;
-  double P00 = 1.0, P01 = 0.0, P10 = 0.0, P11 = 1.0;
-  for (int i = 0; i < L; ++i) {                  // P = A P
-    const double n00 = a00 * P00 + P10, n01 = a00 * P01 + P11;
-    const double n10 = a10 * P00 + P10, n11 = a10 * P01 + P11;
-    P00 = n00; P01 = n01; P10 = n10; P11 = n11;
+  if (tid == 0) {
+    double P00 = 1.0, P01 = 0.0, P10 = 0.0, P11 = 1.0;
+    for (int i = 0; i < L; ++i) {                // P = A P
+      const double n00 = a00 * P00 + P10, n01 = a00 * P01 + P11;
+      const double n10 = a10 * P00 + P10, n11 = a10 * P01 + P11;
+      P00 = n00; P01 = n01; P10 = n10; P11 = n11;
+    }
+    Mat2 x{P00, P01, P10, P11};
+    for (int i = 0; i < 10; ++i, x = mmul(x, x)) qp[i] = x;
   }
+  __syncthreads();
+  auto qpow = [&](int e) {                       // Q^e, e < 1024
+    Mat2 r{1.0, 0.0, 0.0, 1.0};
+    for (int i = 0; e > 0; ++i, e >>= 1)
+      if (e & 1) r = mmul(r, qp[i]);
+    return r;
+  };
+  double* tw = tb + wv * SB * TBS;               // this wave's transpose tile
   for (int round = 0; round < SPEC_IT; ++round) {
     // 2. solve: the chunk's response from zero state
     double zp = 0.0, zv = 0.0;
-#pragma unroll 4
-    for (int64_t k = k0; k < k1; ++k) {
-      const double c = cl[own(k)];
-      const double d = c - (floor(c) + ((double)mrel[own(k)] - jb));
-      const double np = a00 * zp + zv + kC * d;
-      const double nv = a10 * zp + zv + (kA * d - kB);
-      zp = np; zv = nv;
+    for (int i0 = 0; i0 < L; i0 += SB) {
+      int cd[SB];
+      int8_t mm[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        cd[u] = code[(i0 + u) * CSTR + tid];
+        mm[u] = mrel[(i0 + u) * CSTR + tid];
+      }
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const double c = cval(cd[u], k0 + i0 + u);
+        const double d = c - (floor(c) + ((double)mm[u] - jb));
+        const double np = a00 * zp + zv + kC * d;
+        const double nv = a10 * zp + zv + (kA * d - kB);
+        const bool act = i0 + u < len;
+        zp = act ? np : zp;
+        zv = act ? nv : zv;
+      }
     }
     // chunk starts y_j = Q^j x_1 + Y_{j-1}, Y_j = sum_{i<=j} Q^(j-i) z_i (Q = A^L): an inclusive
     // scan of the z_i within each wave by shuffles (offset o combines with Q^o), then across the
     // waves through their totals (Y at a wave's end = its total + Q^64 Y at the previous end)
-    const Mat2 Q{P00, P01, P10, P11};
     double yp = tid < TE ? zp : 0.0, yv = tid < TE ? zv : 0.0;
     {
-      Mat2 Qo = Q;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
+      for (int i = 0; i < 6; ++i) {
+        const int o = 1 << i;
         const double up = __shfl_up(yp, o, 64), uv = __shfl_up(yv, o, 64);
         if (lane >= o) {
+          const Mat2 Qo = qp[i];
           yp = yp + (Qo.a * up + Qo.b * uv);
           yv = yv + (Qo.c * up + Qo.d * uv);
         }
-        Qo = mmul(Qo, Qo);
       }
       if (lane == 63) wsum[wv] = d2v{yp, yv};
       __syncthreads();
       // Y at the end of the previous wave, then Q^(lane+1) of it
-      const Mat2 Q64 = Qo;                         // Q^64 after the six squarings
       double cp = 0.0, cv = 0.0;
       for (int i = 0; i < wv; ++i) {
+        const Mat2 Q64 = qp[6];
         const double np = wsum[i].x + (Q64.a * cp + Q64.b * cv), nv = wsum[i].y + (Q64.c * cp + Q64.d * cv);
         cp = np; cv = nv;
       }
-      const Mat2 Ql = mpow2(Q, lane + 1);
+      const Mat2 Ql = qpow(lane + 1);
       yp = yp + (Ql.a * cp + Ql.b * cv);
       yv = yv + (Ql.c * cp + Ql.d * cv);
-      __syncthreads();                             // wsum read before the next round writes it
+      __syncthreads();                             // wsum read before it is rewritten
     }
     // Y_{j-1}: the previous lane's (lane 0: the previous wave's last, via LDS)
     double vp = __shfl_up(yp, 1, 64), vv = __shfl_up(yv, 1, 64);
-    if (lane == 63) yb[wv] = d2v{yp, yv};
+    if (lane == 63) wsum[wv] = d2v{yp, yv};
     __syncthreads();
     if (lane == 0) {
-      if (wv > 0) { vp = yb[wv - 1].x; vv = yb[wv - 1].y; }
+      if (wv > 0) { vp = wsum[wv - 1].x; vv = wsum[wv - 1].y; }
       else { vp = 0.0; vv = 0.0; }
     }
     {
-      const Mat2 Qj = mpow2(Q, tid);               // Q^j x_1
+      const Mat2 Qj = qpow(tid);                   // Q^j x_1
       vp = vp + (Qj.a * p1 + Qj.b * v1);
       vv = vv + (Qj.c * p1 + Qj.d * v1);
     }
-    __syncthreads();                             // yb read before it is reused
-    // 3. check: the true step from y_j
+    __syncthreads();                             // wsum read before the next round writes it
+    SPEC_TP();
+    // 3. check: the true step from y_j.  The phases go out as the theta row on every round (a
+    // later round or the sequential kernel overwrites a failed one): each batch of SB steps
+    // of the wave's 64 chunks turns through tw so that a store covers 8 chunks x SB steps
+    // (64-B runs) instead of 64 scattered doubles
     bool miss = false;
     double p = vp, V = vv;
-    for (int64_t k = k0; k < k1; ++k) {
-      const double c = cl[own(k)];
-      const double t = fma(-kInv2Pi, p, c);
-      const double r = rel_of(t, c);
-      miss |= r != (double)mrel[own(k)];         // (out of a byte's range: a miss, and so on)
-      mrel[own(k)] = (int8_t)(r >= -127.0 && r <= 127.0 ? r : 0.0);
-      const double f = __builtin_amdgcn_fract(t);
-      const double S = p + V;
-      V = fma(kA, f, V - kB);
-      p = fma(kC, f, S);
-      th[k] = thval(p, k);
+    for (int i0 = 0; i0 < L; i0 += SB) {
+      int cd[SB];
+      int8_t mm[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        cd[u] = code[(i0 + u) * CSTR + tid];
+        mm[u] = mrel[(i0 + u) * CSTR + tid];
+      }
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int i = i0 + u;
+        const double c = cval(cd[u], k0 + i);
+        const double t = fma(-kInv2Pi, p, c);
+        const double r = rel_of(t, c);
+        const bool act = i < len;
+        miss |= act && r != (double)mm[u];       // (out of a byte's range: a miss, and so on)
+        const double f = __builtin_amdgcn_fract(t);
+        const double S = p + V;
+        const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
+        V = act ? nV : V;
+        p = act ? np : p;
+        if (act) mrel[i * CSTR + tid] = (int8_t)(r >= -127.0 && r <= 127.0 ? r : 0.0);
+        tw[u * TBS + lane] = thval(p, k0 + i);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int u = lane & (SB - 1), cw = lane / SB;   // this lane stores step i0 + u of chunk 8 r + cw
+#pragma unroll
+      for (int r8 = 0; r8 < 64 / SB; ++r8) {
+        const int ch = r8 * SB + cw;                   // chunk within the wave
+        const int k = 1 + (wv * 64 + ch) * L + i0 + u;
+        const double v = tw[u * TBS + ch];
+        if (k < (int)n) th[k] = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     const int nmiss = __syncthreads_count(miss);
+    SPEC_TP();
+#ifdef SDR_PLL_SPEC_PROF
+    if (tid == 0 && nmiss == 0 && (blockIdx.x % 479) == 3)
+      printf("spec_prof blk %d L %d: stage %lld corr %lld guess %lld solve %lld check %lld (%d marks)\n", (int)blockIdx.x, L,
+             tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], ntp);
+#endif
 #ifdef SDR_PLL_SPEC_DEBUG   // A/B builds only (make ... CXXFLAGS+=-DSDR_PLL_SPEC_DEBUG): never in libsdr.so
     if (tid == 0) printf("pll_spec q%d s%d n%ld T%d L%d TE%d round %d: %d chunks missed\n", q, s, (long)n, SPEC_T, L, TE, round, nmiss);
 #endif
