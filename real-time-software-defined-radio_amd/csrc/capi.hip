@@ -91,9 +91,13 @@ int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T) 
   for (int k = 0; k < T; ++k) f[k] = (float)b[k];
   for (int k = 0; k < std::min(T, SDR_MAX_TAPS); ++k) t.h.h[k] = f[k];
   const int cap = std::max(T, SDR_MAX_TAPS);
-  HIP_TRY(hipMalloc(&t.dev_f32, sizeof(float) * cap));
+  std::vector<float> fr(cap + T + 4, 0.f);          // forward | pad, 0, reversed, 0, 0
+  std::copy(f.begin(), f.end(), fr.begin());
+  for (int j = 0; j < T; ++j) fr[cap + 2 + j] = f[T - 1 - j];
+  HIP_TRY(hipMalloc(&t.dev_f32, sizeof(float) * fr.size()));
   HIP_TRY(hipMalloc(&t.dev_f64, sizeof(double) * cap));
-  HIP_TRY(hipMemcpy(t.dev_f32, f.data(), sizeof(float) * T, hipMemcpyHostToDevice));
+  t.dev_rev = t.dev_f32 + cap + 2;
+  HIP_TRY(hipMemcpy(t.dev_f32, fr.data(), sizeof(float) * fr.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(t.dev_f64, b, sizeof(double) * T, hipMemcpyHostToDevice));
   c->taps.push_back(std::move(t));
   *out = &c->taps.back();

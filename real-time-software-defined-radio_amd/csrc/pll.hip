@@ -499,7 +499,7 @@ __device__ __forceinline__ Mat2 mpow2(Mat2 x, int e) {
 // LB_NEED_G) or its chained start (LB_NEED_X); the end state goes to the block's record and
 // the call's own state, trigOffset slot and NCO[0] are left to the long-call kernels.
 template <int SPEC_T, bool LONG>
-__global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(4))) void pll_spec_kernel(PllJobs P) {
+__global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T == 512 ? 4 : 2))) void pll_spec_kernel(PllJobs P) {
 #pragma clang fp contract(off)
   // Per step k = 1 .. n-1, at slot i * CSTR + j (step i of chunk j, see the staging below):
   // the sign code of x_k (0: x > 0, 1: x < 0, 2: 0 / NaN) -- the constant c_k is a function

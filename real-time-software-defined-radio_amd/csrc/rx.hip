@@ -38,7 +38,7 @@ constexpr int RX_MAXJ = 6;          // jobs per stage launch
 constexpr int RX_NT = 256;          // threads per workgroup
 constexpr int RX_R = 4;             // outputs per thread of the generic tiles (any T, resampler)
 constexpr int RX_TO = RX_NT * RX_R;  // outputs per generic tile
-constexpr int RX_LDS = 5632;        // floats of LDS per workgroup (largest: 151 taps, decim 5)
+constexpr int RX_LDS = 6144;        // floats of LDS per workgroup (largest: 151 taps, decim 5: 5 796)
 
 enum { JK_FIR = 0, JK_RESAMPLE = 1 };
 enum { PRE_NONE = SDR_PRE_NONE, PRE_SQUARE = SDR_PRE_SQUARE, PRE_MIX = SDR_PRE_MIX };
@@ -48,6 +48,7 @@ struct StageJob {
   const float* x;        // input rows, x_stride apart
   const float* c;        // PRE_MIX second operand (same indexing as x)
   const float* taps;     // f32 taps (device)
+  const float* rtaps;    // the same reversed, zero at [-1] and [T] (TapSet::dev_rev: fir_tile's pairs)
   const double* taps64;  // f64 taps (device, for zf)
   const double* zi;      // lfilter state in (T-1 per stream, zi_stride apart), nullable
   double* zf;            // lfilter state out (same layout), nullable
@@ -95,34 +96,41 @@ __device__ __forceinline__ float pre_op(int pre, float x, float c, float g) {
   return pre == PRE_SQUARE ? x * x : pre == PRE_MIX ? (x * c) * g : x;
 }
 
-// acc += h * x with the tap in an SGPR (v_fmac_f32's scalar operand): the compiler neither
-// moves taps into vector registers nor pairs the FMAs into packed ones (whose tap and sample
-// pairs it had to assemble with a v_mov per FMA)
-__device__ __forceinline__ void fmac_s(float& acc, float h, float x) {
-  asm("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "s"(h), "v"(x));
-}
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
 typedef const __attribute__((address_space(4))) float* ctaps_t;   // uniform, read-only: scalar loads
+typedef const __attribute__((address_space(4))) f2a4* ctaps2_t;
+
+// acc.xy += h.xy * x.xy in one v_pk_fma_f32, the tap pair as a 64-bit SGPR operand (a scalar
+// load of two consecutive reversed taps): the compiler neither moves taps into vector
+// registers nor assembles packed operands with a v_mov per FMA
+__device__ __forceinline__ void pk_fma_s(f2& acc, f2 h, f2 x) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(acc) : "s"(h), "v"(x));
+}
 
 // The lfilter FIR tile for compile-time (T, D): lane t owns R consecutive outputs and slides
-// once over its D(R-1)+T-sample window in LDS, R multiply-adds per sample with the taps as
-// SGPR operands (scalar loads through the constant address space, compile-time indices).
-// 16 outputs per lane at D = 1 (16 FMAs per ds_read: VALU-bound, not LDS-bound), 4 at D = 5
-// (a 20x larger window per output; 1/5 of the work).  The tile image has one pad float after
-// every lane's D*R samples (odd lane stride: conflict-free ds_read_b32), and starts DELTA
-// samples early so that its global loads are 16-B aligned.
+// once over its D(R-1)+T-sample window in LDS two samples at a time (ds_read_b64), each
+// output's two partial sums -- even and odd window samples -- in one packed register:
+//   acc_r.xy += (g[j], g[j+1]) * (x_i, x_{i+1}),  j = i - D r,  g = the taps reversed
+// (g[j] = h[T-1-j], zero at j = -1 and j = T: TapSet::dev_rev), i.e. acc_r.x += h[D r+T-1-i] x_i
+// and acc_r.y += h[D r+T-2-i] x_{i+1}; y_r = acc_r.x + acc_r.y.  16 outputs per lane at D = 1
+// (16 packed FMAs per ds_read_b64: VALU-bound), 4 at D = 5.  The tile image has two pad
+// floats after every lane's D*R samples (even lane stride SR = 2 mod 4 dwords: 8-B aligned,
+// conflict-free ds_read_b64), and starts DELTA samples early so that its global loads are
+// 16-B aligned.
 template <int T, int D>
 struct FirShape {
   static constexpr int G = 4, NT = RX_NT, R = D == 1 ? 16 : 4, TO = NT * R, DR = D * R;
-  static constexpr int SR = DR + 1;                          // lane stride in LDS (floats)
+  static constexpr int SR = DR + 2;                          // lane stride in LDS (floats)
   static constexpr int DELTA = (G - ((T - 1) % G)) % G;
   static constexpr int L = D * (TO - 1) + T + DELTA;         // image samples
   static constexpr int LG = (L + G - 1) / G * G;
   static constexpr int NI = D * (R - 1) + T;                 // per-lane window
-  static constexpr int NSLOT = LG + LG / DR + 1;
+  static constexpr int NSLOT = LG + 2 * (LG / DR) + 2;
   static_assert((D * TO) % G == 0, "tile start must stay G-aligned");
   static_assert(NSLOT <= RX_LDS, "tile image fits the stage LDS");
-  static_assert(SR % 2 == 1, "odd lane stride");
-  __device__ static constexpr int slot(int u) { return u < DELTA ? u : u + (u - DELTA) / DR; }
+  static_assert(SR % 4 == 2 && DELTA % 2 == 0 && NI % 2 == 0, "8-B aligned, conflict-free sample pairs");
+  __device__ static constexpr int slot(int u) { return u < DELTA ? u : u + 2 * ((u - DELTA) / DR); }
 };
 
 template <int T, int D>
@@ -168,22 +176,26 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
     }
   }
   __syncthreads();
-  const ctaps_t h = (ctaps_t)J.taps;
+  const ctaps_t gr = (ctaps_t)J.rtaps;
   const float* win = lds + DELTA + S::SR * t;
-  float acc[R];
+  f2 pacc[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.f;
-  static_for<0, S::NI>([&](auto I) {
-    constexpr int i = I;
-    const float x = win[i + i / DR];
+  for (int r = 0; r < R; ++r) pacc[r] = f2{0.f, 0.f};
+  static_for<0, S::NI / 2>([&](auto I) {
+    constexpr int i = 2 * I;
+    const f2 x = *reinterpret_cast<const f2*>(win + i + 2 * (i / DR));
     static_for<0, R>([&](auto RR) {
       constexpr int r = RR;
-      constexpr int k = D * r + T - 1 - i;
-      if constexpr (k >= 0 && k < T) fmac_s(acc[r], h[k], x);
+      constexpr int j = i - D * r;
+      if constexpr (j >= -1 && j <= T - 1) {
+        const f2a4 hp = *(ctaps2_t)(gr + j);         // (g[j], g[j+1]): float-indexed pair
+        pk_fma_s(pacc[r], f2{hp.x, hp.y}, x);
+      }
     });
   });
+  float acc[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] += zr[r];
+  for (int r = 0; r < R; ++r) acc[r] = (pacc[r].x + pacc[r].y) + zr[r];
   float* yb = J.y + (int64_t)s * J.y_stride;
   if (mf + R <= M) {
 #pragma unroll
@@ -841,7 +853,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   auto fir = [&](int f, int z, const float* x, int64_t n, int64_t xs, float* y, int64_t ys, int D, int pre = PRE_NONE,
                  const float* cmix = nullptr) {
     StageJob j{};
-    j.x = x; j.c = cmix; j.taps = ts[f]->dev_f32; j.taps64 = ts[f]->dev_f64;
+    j.x = x; j.c = cmix; j.taps = ts[f]->dev_f32; j.rtaps = ts[f]->dev_rev; j.taps64 = ts[f]->dev_f64;
     j.zi = zin(z); j.zf = zout(z); j.zi_stride = r->zlen[z];
     j.y = y; j.y_stride = ys; j.n = n; j.x_stride = xs;
     j.gain = 2.0f;                      // the reference's mixer gain (fmMonoBlock.py:156, fmRDSblock.py:173)

@@ -23,7 +23,8 @@ enum Slot {
 struct TapSet {
   std::vector<double> b;
   TapsF32 h;
-  float* dev_f32 = nullptr;
+  float* dev_f32 = nullptr;   // [0, cap): the taps; then, from dev_rev - 1: 0, the taps reversed, 0, 0
+  float* dev_rev = nullptr;   // dev_rev[j] = h[T-1-j], dev_rev[-1] = dev_rev[T] = 0 (packed FIR tiles)
   double* dev_f64 = nullptr;
 };
 
