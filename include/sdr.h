@@ -141,21 +141,24 @@ int sdr_pll(sdr_ctx* ctx, const float* in, int64_t n, double freq, double fs, do
  *   RECURRENCES   recurrences solved
  *   SPEC_R0..R2   ... by the parallel solve (guess + scan + check) in its 1st / 2nd / 3rd round
  *   SEQUENTIAL    ... by the sequential kernel (the fallback: acquisition, 0 / NaN input)
- *   LONG_GUESSED  long calls: pseudo-blocks kept as solved from their warm-up start guess
+ *   LONG_GUESSED  long calls: pseudo-blocks kept as solved from their pre-roll start guess
  *                 (start within the acceptance bound of the chained state after a 2 pi shift)
- *   LONG_CHAINED  long calls: pseudo-blocks solved again from the start the chain computed
- *   LONG_MAXGAP   largest accepted bound on the phase deviation between a pseudo-block's
- *                 solved start and the chained state (radians, the bits of an f64)
+ *   LONG_CHAINED  long calls: pseudo-blocks completed from the start the chain computed (the
+ *                 linear response to the start error added, or solved again from it)
+ *   LONG_MAXGAP   largest bound on the phase deviation between a pseudo-block's solved start
+ *                 and the chained state among those kept as solved (radians, the bits of an f64)
  *   LONG_STOPS    long calls: pseudo-blocks whose start guess was beyond the linear bound (the
  *                 chain stopped there that round and re-solved it from the exact start)
  *   LONG_TAIL     long calls: pseudo-blocks left after the rounds, solved sequentially from the
  *                 chain's exact position (also counted in SEQUENTIAL)
+ *   LONG_LINEAR   long calls: pseudo-blocks completed by the linear response to their start
+ *                 error (every step's wrap further than the deviation bound: also in CHAINED)
  * out: SDR_PLL_NSTATS int64 (LONG_MAXGAP: reinterpret as double).  Synchronises the context
  * stream; reset != 0 zeroes the counters after reading. */
 enum {
   SDR_PLL_ST_RECURRENCES, SDR_PLL_ST_SPEC_R0, SDR_PLL_ST_SPEC_R1, SDR_PLL_ST_SPEC_R2, SDR_PLL_ST_SEQUENTIAL,
   SDR_PLL_ST_LONG_GUESSED, SDR_PLL_ST_LONG_CHAINED, SDR_PLL_ST_LONG_MAXGAP, SDR_PLL_ST_LONG_STOPS,
-  SDR_PLL_ST_LONG_TAIL, SDR_PLL_NSTATS
+  SDR_PLL_ST_LONG_TAIL, SDR_PLL_ST_LONG_LINEAR, SDR_PLL_NSTATS
 };
 int sdr_pll_stats(sdr_ctx* ctx, int64_t* out, int reset);
 

@@ -29,7 +29,7 @@ RX_OUTPUTS = ("demod", "audio", "bpf_recovery", "nco", "bpf_extraction", "stereo
 RX_STAGES = ("fe", "filters_of_demod", "rds_square", "pll", "mix_lpf", "resample", "rrc")
 # PLL solve counters (include/sdr.h SDR_PLL_ST_*)
 PLL_STATS = ("recurrences", "spec_r0", "spec_r1", "spec_r2", "sequential", "long_guessed", "long_chained",
-             "long_maxgap", "long_stops", "long_tail")
+             "long_maxgap", "long_stops", "long_tail", "long_linear")
 
 
 class SdrUnavailable(RuntimeError):

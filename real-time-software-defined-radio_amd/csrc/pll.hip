@@ -459,9 +459,15 @@ constexpr int SB = 8;                        // steps per batch of LDS reads in 
 enum { LB_NEED_G = 0, LB_DONE_G = 1, LB_NEED_X = 2, LB_DONE_X = 3, LB_ACCEPTED = 4 };
 constexpr int SOLVER_SEQ = 3;        // solver codes: 0..2 = parallel solve round, 3 = sequential
 // u: the start (phaseEst, integrator) the current solution (theta row, e) was solved from.
-struct LongBlk { double g[6]; double x[6]; double e[6]; double u[2]; double shift; int status; int solver; };
+// shift: the chain's whole turns for the block's phases; d: the start error (dphaseEst, dV)
+// the chain accepted the block with (its stored phases + the loop's linear response to d are
+// the recurrence's, nco_long_kernel adds both); margin: the solve's smallest distance of a
+// step's fract(t_k) from a wrap, in turns (-1: none, the sequential kernels' solves).
+struct LongBlk {
+  double g[6]; double x[6]; double e[6]; double u[2]; double shift; double d[2]; double margin; int status; int solver;
+};
 struct LongHdr { double sp, si; int pos; int pad; double pad2; };
-static_assert(sizeof(LongBlk) == 176 && sizeof(LongHdr) == 32, "long-call scratch layout");
+static_assert(sizeof(LongBlk) == 200 && sizeof(LongHdr) == 32, "long-call scratch layout");
 __device__ __forceinline__ LongHdr* long_hdr(const PllJobs& P, int r) { return static_cast<LongHdr*>(P.work) + r; }
 __device__ __forceinline__ LongBlk* long_blk(const PllJobs& P, int r, int b) {
   return reinterpret_cast<LongBlk*>(static_cast<char*>(P.work) + (int64_t)P.njobs * P.nstreams * sizeof(LongHdr)) +
@@ -478,6 +484,15 @@ __device__ __forceinline__ double wave_prefix_sum(double v, int lane) {   // inc
     if (lane >= o) v += u;
   }
   return v;
+}
+
+// a wave-uniform f64 held in SGPRs (readfirstlane of both halves): the compiler computes
+// uniform f64 values on the VALU and would otherwise keep them in VGPRs
+__device__ __forceinline__ double sgpr_d(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 // 2x2 matrices (row-major a, b, c, d) for the loop's linear form
@@ -516,11 +531,13 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
   __shared__ d2v wsum[NW];
   __shared__ Mat2 qp[10];
   __shared__ double x1s[2];
+  __shared__ float mg[NW + 1];                   // the waves' smallest wrap margins (+ the literal step's)
   d2v* yb = reinterpret_cast<d2v*>(tb);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int tid = threadIdx.x;
   int q, s, status = 0;
   int64_t n, base = 0;
+  int pre = 0;                                   // LONG, guessed start: pre-roll steps (below)
   LongBlk* LB = nullptr;
   if constexpr (LONG) {
     const int nb = P.lg.nb;
@@ -533,6 +550,15 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
     if (status != LB_NEED_G && status != LB_NEED_X) return;
     base = (int64_t)b * P.lg.pb;
     n = long_len(P, b);
+    // a pseudo-block after the first, not yet reached by the chain: its start is unknown, so
+    // the solve runs `pre` steps of the previous pseudo-block's range first, from the phase
+    // the input measures there (mod 2 pi) and the span's start integrator.  The loop contracts
+    // the seed's error by sqrt(1 - Kp) a step, so the state at the block's start converges to
+    // the recurrence's up to whole turns (the chain finds them) -- the sequential warm-up of a
+    // start guess, solved in parallel with the block.  Its phases are not stored.
+    if (status == LB_NEED_G && b > 0) pre = P.lg.warm[q];
+    n += pre;
+    base -= pre;
   } else {
     q = blockIdx.x / P.nstreams;
     s = blockIdx.x - q * P.nstreams;
@@ -553,10 +579,11 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
 #endif
   double* st = LONG ? (status == LB_NEED_G ? LB->g : LB->x) : J.state + (int64_t)s * 6;
   double* st_out = LONG ? LB->e : st;
-  const double off = st[5];
-  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
-  const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
-  const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
+  const double* st_call = J.state + (int64_t)s * 6;
+  const double off = sgpr_d(pre ? st_call[5] + (double)base : st[5]);   // trigOffset of local step 0
+  const double w = sgpr_d(2.0 * kPi * (cfg.freq / cfg.fs));
+  const double kA = sgpr_d(k2Pi * cfg.ki), kB = sgpr_d(kPi * cfg.ki);
+  const double kC = sgpr_d(k2Pi * (cfg.kp + cfg.ki)), kD = sgpr_d(kPi * (cfg.kp + cfg.ki));
   auto thval = [&](double ph, int64_t k) {       // what the theta row holds for step k
     if (!P.qform) return ph;
     const double i = (double)(k % PG);
@@ -568,10 +595,12 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
     const double cv = fma(cc, kInv2Pi, 0.5);
     return cd == 2 ? __builtin_nan("") : cv;
   };
-  // sample 0: the literal general step (thread 0), as the loop kernels' general()
-  if (tid == 0) {
+  // sample 0: the literal general step (thread 0), as the loop kernels' general() (a
+  // pre-roll's seed is set from the measured phase instead, below)
+  if (tid == 0 && pre == 0) {
     const double xv = (double)in[0];
     const double e = atan2(xv * (-st[3]), xv * st[2]);
+    mg[NW] = (float)((kPi - fabs(e)) * kInv2Pi);  // the literal step's distance from the wrap
     const double integ = st[0] + cfg.ki * e;
     const double phase = st[1] + cfg.kp * e + integ;
     x1s[0] = phase;
@@ -606,11 +635,6 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
   }
   __syncthreads();
   SPEC_TP();
-  const double p1 = x1s[0], v1 = x1s[1];
-  // the integer part relative to floor(c_k) is floor(-phaseEst/2pi + frac(c_k)): near -jb
-  // within a block, so it fits a byte once jb is taken off (a drifting phase estimate moves jb)
-  const double jb = floor(kInv2Pi * p1);
-  auto rel_of = [&](double t, double c) { return floor(t) - floor(c) + jb; };
   // 0. where the locked phase estimate goes within the block, measured from the input: a
   // locked loop keeps its angle th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's
   // phase, so z_j = sum over chunk j of x_k exp(-i w (off + k)) ~ (A/2) exp(i phaseEst) (+ an
@@ -647,6 +671,10 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
       if (j >= 0 && j < TE) { sr += yb[j].x; si += yb[j].y; }
     }
     const double ang = atan2(si, sr);
+    if (pre > 0 && tid == 0) {                   // the pre-roll's seed: measured phase, span's integrator
+      x1s[0] = ang;
+      x1s[1] = st_call[0] - kD;
+    }
     __syncthreads();
     yb[tid].x = ang;
     __syncthreads();
@@ -665,6 +693,11 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
     __syncthreads();
   }
   SPEC_TP();
+  const double p1 = x1s[0], v1 = x1s[1];
+  // the integer part relative to floor(c_k) is floor(-phaseEst/2pi + frac(c_k)): near -jb
+  // within a block, so it fits a byte once jb is taken off (a drifting phase estimate moves jb)
+  const double jb = floor(kInv2Pi * p1);
+  auto rel_of = [&](double t, double c) { return floor(t) - floor(c) + jb; };
   // 1. guess
   bool bad = false;
   {
@@ -812,28 +845,33 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
     // (64-B runs) instead of 64 scattered doubles
     bool miss = false;
     double p = vp, V = vv;
+    float mth = 1.f;                             // smallest min(fract, 1 - fract) of the block's own steps
     for (int i0 = 0; i0 < L; i0 += SB) {
-      int cd[SB];
-      int8_t mm[SB];
+      int cd[SB / 2];                            // (half a batch of codes at a time: registers)
+      int8_t mm[SB / 2];
 #pragma unroll
       for (int u = 0; u < SB; ++u) {
-        cd[u] = code[(i0 + u) * CSTR + tid];
-        mm[u] = mrel[(i0 + u) * CSTR + tid];
-      }
+        if (u % (SB / 2) == 0) {
 #pragma unroll
-      for (int u = 0; u < SB; ++u) {
+          for (int v = 0; v < SB / 2; ++v) {
+            cd[v] = code[(i0 + u + v) * CSTR + tid];
+            mm[v] = mrel[(i0 + u + v) * CSTR + tid];
+          }
+        }
         const int i = i0 + u;
-        const double c = cval(cd[u], k0 + i);
+        const double c = cval(cd[u % (SB / 2)], k0 + i);
         const double t = fma(-kInv2Pi, p, c);
         const double r = rel_of(t, c);
         const bool act = i < len;
-        miss |= act && r != (double)mm[u];       // (out of a byte's range: a miss, and so on)
+        miss |= act && r != (double)mm[u % (SB / 2)];   // (out of a byte's range: a miss, and so on)
         const double f = __builtin_amdgcn_fract(t);
         const double S = p + V;
         const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
         V = act ? nV : V;
         p = act ? np : p;
+        if (act && k0 + i >= pre) mth = fminf(mth, (float)fmin(f, 1.0 - f));
         if (act) mrel[i * CSTR + tid] = (int8_t)(r >= -127.0 && r <= 127.0 ? r : 0.0);
+        if (k0 + i == pre - 1) { x1s[0] = p; x1s[1] = V; }   // a pre-roll's state at the block start
         tw[u * TBS + lane] = thval(p, k0 + i);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -845,11 +883,16 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
         const int ch = r8 * SB + cw;                   // chunk within the wave
         const int k = 1 + (wv * 64 + ch) * L + i0 + u;
         const double v = tw[u * TBS + ch];
-        if (k < (int)n) th[k] = v;
+        if (k >= pre && k < (int)n) th[k] = v;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if constexpr (LONG) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mth = fminf(mth, __shfl_xor(mth, o, 64));
+      if (lane == 0) mg[wv] = mth;
     }
     const int nmiss = __syncthreads_count(miss);
     SPEC_TP();
@@ -864,7 +907,7 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
     if (nmiss == 0) {
       // done: the caller-visible results exactly as the loop kernels leave them
       if (tid == 0) {
-        th[0] = thval(p1, 0);
+        if (pre == 0) th[0] = thval(p1, 0);
         if constexpr (!LONG) {
           J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];
           if (J.nco_q)
@@ -885,8 +928,26 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
       }
       if (tid == 0) {
         if constexpr (LONG) {                    // counted when the chain accepts the block
-          LB->u[0] = st[0];
-          LB->u[1] = st[1];
+          if (pre > 0) {                         // the pre-roll's state at the block start: its guess
+            const double gpv = x1s[0], gvv = x1s[1];
+            const double ofs = off + (double)(pre - 1);          // the previous step's trigOffset
+            const double arg = w * (ofs + 1.0) + gpv;
+            LB->g[0] = gvv + kD;
+            LB->g[1] = gpv;
+            LB->g[2] = cos(arg);
+            LB->g[3] = sin(arg);
+            LB->g[4] = 0.0;
+            LB->g[5] = off + (double)pre;
+            LB->u[0] = gvv + kD;
+            LB->u[1] = gpv;
+          } else {
+            LB->u[0] = st[0];
+            LB->u[1] = st[1];
+          }
+          float m = pre == 0 ? mg[NW] : 1.f;
+          for (int i = 0; i < NW; ++i) m = fminf(m, mg[i]);
+          LB->margin = m;
+          LB->d[0] = LB->d[1] = 0.0;             // its phases are its own solve's
           LB->status = status + 1;               // LB_NEED_G -> LB_DONE_G, LB_NEED_X -> LB_DONE_X
           LB->solver = round;
         } else {
@@ -902,16 +963,18 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
 
 // ================================================================================
 // Long calls (n > SDR_PLL_BLOCK_MAX): a device-resident span of many blocks is one recurrence
-// of n steps, cut into nb pseudo-blocks of pb <= 16 384 steps so that every pseudo-block is one
-// pll_spec_kernel workgroup and the whole span fills the GPU.  A pseudo-block's start state is
-// the previous one's end state, unknown until that one is solved, so:
-//   1. pll_warm_kernel: each pseudo-block's start is GUESSED by running the loop's true step
-//      over the `warm` samples before it, from the span's start frequency (one wave each).
-//      The loop contracts errors by sqrt(1 - Kp) per step, and its dynamics are invariant
-//      under phaseEst -> phaseEst + 2 pi, so the guess converges to the true state up to a
-//      whole number of turns.
+// of n steps, cut into nb pseudo-blocks of pb <= LONG_PB (14 336) steps so that every pseudo-block
+// (with its pre-roll) is one pll_spec_kernel workgroup and the whole span fills the GPU.  A
+// pseudo-block's start state is the previous one's end state, unknown until that one is
+// solved, so:
+//   1. pll_long_init_kernel: bookkeeping; the first pseudo-block starts from the call's state.
 //   2. pll_spec_kernel<..., LONG> (+ pll_long_seq_kernel for what it cannot complete): every
-//      pseudo-block solved from its guess.
+//      pseudo-block solved.  One after the first is solved together with a PRE-ROLL: the
+//      `warm` steps before it, from the phase the input measures there and the span's start
+//      integrator; the loop contracts errors by sqrt(1 - Kp) per step, and its dynamics are
+//      invariant under phaseEst -> phaseEst + 2 pi, so the pre-roll's state at the block's
+//      start -- its GUESS -- has converged to the true state up to a whole number of turns
+//      (the parallel form of a sequential warm-up over the same steps).
 //   3. pll_long_chain_kernel (one wave per recurrence, serial over the pseudo-blocks, all in
 //      f64 scalars): from the exact state at the chain's position, the 2 pi shift n between
 //      the exact start and the guess is taken out, and the remaining start error (dp, dV)
@@ -931,116 +994,42 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
 //   The NCO kernel adds 2 pi n to an accepted guessed block's phases.
 constexpr double LONG_ACCEPT = 1e-9;   // rad: accepted deviation bound
 constexpr double LONG_LINEAR = 0.3;    // rad: deviation bound under which the integers m_k are kept
+constexpr double LONG_MARGIN_TOL = 1e-6;   // turns: wrap margin kept clear of rounding
 constexpr int LONG_ROUNDS = 4;
 
-// 1. Start guesses: one lane per pseudo-block (WARM_LPW lanes of one recurrence per wave,
-// all with the same number of steps), each running the loop's true step over its `warm`
-// constants, fetched 16 at a time two groups ahead of use.
-constexpr int WARM_LPW = 16;
-constexpr int WARM_G = 16;
-constexpr int WARM_Z = 256;       // samples of the phase measurement that seeds a warm-up
-__global__ __launch_bounds__(64) void pll_warm_kernel(PllJobs P) {
-#pragma clang fp contract(off)
+// 1. Bookkeeping: every pseudo-block unsolved, no shift; the first starts from the call's
+// state (exact), the others from the guess their solve's pre-roll finds (pll_spec_kernel).
+__global__ __launch_bounds__(256) void pll_long_init_kernel(PllJobs P) {
   const int nb = P.lg.nb;
-  const int wpr = (nb + WARM_LPW - 1) / WARM_LPW;
-  const int r = blockIdx.x / wpr;
-  const int b = (blockIdx.x - r * wpr) * WARM_LPW + (int)threadIdx.x;
-  if ((int)threadIdx.x >= WARM_LPW || b >= nb) return;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (int64_t)P.njobs * P.nstreams * nb) return;
+  const int r = (int)(g / nb), b = (int)(g - (int64_t)r * nb);
   const int q = r / P.nstreams, s = r - q * P.nstreams;
   const PllJob& J = P.j[q];
   const PllCfg cfg = J.cfg;
   const double* st = J.state + (int64_t)s * 6;
   LongBlk* B = long_blk(P, r, b);
-  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
-  const double off0 = st[5];
-  const int64_t pb = P.lg.pb;
   B->shift = 0.0;
+  B->d[0] = B->d[1] = 0.0;
+  B->margin = -1.0;
   B->status = LB_NEED_G;
   B->solver = -1;
-  if (b == 0) {                                  // the span's own start: exact
-    for (int i = 0; i < 6; ++i) B->g[i] = st[i];
-    LongHdr* H = long_hdr(P, r);
-    H->sp = st[1];
-    H->si = st[0];
-    H->pos = 0;
-    J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];       // ncoOut[0] (as the per-call kernels)
-    if (J.nco_q)
-      J.nco_q[(int64_t)s * J.out_stride] =
-          (float)((off0 > 0.0) ? sin((w * off0 + st[1]) * cfg.scale + cfg.adj) : 0.0);
-    J.theta[(int64_t)s * J.th_stride + P.n] = off0;         // the NCO kernel's trigOffset
+  if (b > 0) {
+    for (int i = 0; i < 6; ++i) B->g[i] = __builtin_nan("");
     return;
   }
-  const double kA = k2Pi * cfg.ki, kB = kPi * cfg.ki;
-  const double kC = k2Pi * (cfg.kp + cfg.ki), kD = kPi * (cfg.kp + cfg.ki);
-  const int64_t kend = (int64_t)b * pb;
-  const int64_t k0 = max<int64_t>(1, kend - P.lg.warm[q]);
-  const int64_t nst = kend - k0;
-  // seed: the phase the loop locks to, measured from the WARM_Z samples before the warm-up (a
-  // locked loop keeps th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's phase, so
-  // arg sum x_k exp(-i w (off + k)) ~ phaseEst, modulo 2 pi: only that has to converge; the
-  // chain finds the turns).  The integrator from the span's start.  (Extrapolating the start
-  // phase by the integrator does not work: a locked loop balances its integrator with a
-  // static phase error, so the estimate does not move by it -- 20 rad off across a span.)
-  const float* xr = J.in + (int64_t)s * J.in_stride;
-  double p, V = st[0] - kD;
-  {
-    double zr = 0.0, zi = 0.0;
-    const int64_t z0 = max<int64_t>(1, k0 - WARM_Z);
-    for (int64_t kg = z0; kg < k0; kg += WARM_G) {
-      float xv[WARM_G];
-#pragma unroll
-      for (int i = 0; i < WARM_G; ++i) xv[i] = kg + i < k0 ? xr[kg + i] : 0.f;   // all loads first
-#pragma unroll
-      for (int i = 0; i < WARM_G; ++i) {
-        const double c = pll_c(xv[i], w, off0 + (double)(kg + i));
-        if (!(c == c)) continue;                 // 0 (also the padding past k0) / NaN
-        const float a = (float)(k2Pi * __builtin_amdgcn_fract((xv[i] > 0.f ? 0.5 : 1.0) - c));
-        float sa, ca;
-        __sincosf(a, &sa, &ca);
-        zr += (double)(xv[i] * ca);
-        zi -= (double)(xv[i] * sa);
-      }
-    }
-    p = (zr != 0.0 || zi != 0.0) ? atan2(zi, zr) : st[1];
-  }
-  // the warm-up: raw inputs WARM_G at a time, two groups ahead; constants computed at use
-  const float* xin = xr + k0;
-  const int64_t ng = (nst + WARM_G - 1) / WARM_G;
-  auto ld = [&](float (&v)[WARM_G], int64_t g) {
-#pragma unroll
-    for (int i = 0; i < WARM_G; ++i) {
-      const int64_t k = g * WARM_G + i;
-      v[i] = (g < ng && k < nst) ? xin[k] : 0.f;
-    }
-  };
-  float c0[WARM_G], c1[WARM_G], c2[WARM_G];
-  ld(c0, 0);
-  ld(c1, 1);
-  for (int64_t g = 0; g < ng; ++g) {
-    ld(c2, g + 2);
-#pragma unroll
-    for (int i = 0; i < WARM_G; ++i) {
-      const int64_t k = g * WARM_G + i;
-      const double c = pll_c(c0[i], w, off0 + (double)(k0 + k));
-      if (k < nst && c == c) {                   // past the end, or a 0 / NaN input: skipped
-        const double t = fma(-kInv2Pi, p, c);
-        const double f = __builtin_amdgcn_fract(t);
-        const double S = p + V;
-        V = fma(kA, f, V - kB);
-        p = fma(kC, f, S);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < WARM_G; ++i) { c0[i] = c1[i]; c1[i] = c2[i]; }
-  }
-  const double offp = off0 + (double)((int64_t)(b - 1) * pb);      // the previous block's trigOffset
-  const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + p;
-  B->g[0] = V + kD;
-  B->g[1] = p;
-  B->g[2] = cos(arg);
-  B->g[3] = sin(arg);
-  B->g[4] = 0.0;
-  B->g[5] = off0 + (double)kend;
+  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  const double off0 = st[5];
+  for (int i = 0; i < 6; ++i) B->g[i] = st[i];
+  LongHdr* H = long_hdr(P, r);
+  H->sp = st[1];
+  H->si = st[0];
+  H->pos = 0;
+  J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];       // ncoOut[0] (as the per-call kernels)
+  if (J.nco_q)
+    J.nco_q[(int64_t)s * J.out_stride] =
+        (float)((off0 > 0.0) ? sin((w * off0 + st[1]) * cfg.scale + cfg.adj) : 0.0);
+  J.theta[(int64_t)s * J.th_stride + P.n] = off0;         // the NCO kernel's trigOffset
 }
 
 // The reference's recurrence run sequentially from state st over n steps (the general form:
@@ -1109,109 +1098,16 @@ __global__ __launch_bounds__(64) void pll_long_seq_kernel(PllJobs P) {
   LongBlk* B = long_blk(P, r, b);
   const int status = B->status;
   if (status != LB_NEED_G && status != LB_NEED_X) return;
+  if (status == LB_NEED_G && b > 0) return;      // no start yet: the chain hands it one (LB_NEED_X)
   const int64_t base = (int64_t)b * P.lg.pb;
   seq_run(J.cfg, J.in + (int64_t)s * J.in_stride + base, J.theta + (int64_t)s * J.th_stride + base, long_len(P, b),
           status == LB_NEED_G ? B->g : B->x, B->e);
   B->u[0] = (status == LB_NEED_G ? B->g : B->x)[0];
   B->u[1] = (status == LB_NEED_G ? B->g : B->x)[1];
+  B->d[0] = B->d[1] = 0.0;
+  B->margin = -1.0;                              // (general steps: no linear acceptance)
   B->status = status + 1;
   B->solver = SOLVER_SEQ;
-}
-
-// 2a. Re-solving a block from its chained start x, when its current solution started from u
-// within the linear bound: the true phases are the current ones + 2 pi n + the loop's linear
-// response to the start error d = (x - u) - 2 pi n, i.e. theta_k += 2 pi n + (A^(k+1) d)_phase --
-// exactly the recurrence's as long as no step's integer m_k changes.  That is checked at every
-// step: the current fract(t_k) moved by the correction of the phase before it must stay inside
-// (0, 1) (the literal first step: its atan2 angle moved by the correction stays inside (-pi,
-// pi)).  One workgroup per pseudo-block, steps in contiguous runs per thread (A^k by
-// squaring, then one step of A per sample).  A block that fails the check keeps LB_NEED_X and
-// is re-solved by pll_spec_kernel in the same round.
-constexpr int FIX_T = 256;
-__global__ __launch_bounds__(FIX_T) void pll_long_fix_kernel(PllJobs P) {
-#pragma clang fp contract(off)
-  const int nb = P.lg.nb;
-  const int r = blockIdx.x / nb;
-  const int b = blockIdx.x - r * nb;
-  LongBlk* LB = long_blk(P, r, b);
-  if (LB->status != LB_NEED_X || LB->solver < 0) return;
-  const int q = r / P.nstreams, s = r - q * P.nstreams;
-  const PllJob& J = P.j[q];
-  const PllCfg cfg = J.cfg;
-  const int tid = threadIdx.x;
-  const double d0 = LB->x[1] - LB->u[1];
-  const double nsh = rint(d0 * kInv2Pi);
-  const double dp = fma(-nsh, kP2, fma(-nsh, kP1, d0));
-  const double dv = LB->x[0] - LB->u[0];
-  if (!(P.lg.c1[q] * fabs(dp) + P.lg.c2[q] * fabs(dv) <= LONG_LINEAR)) return;
-  const int64_t n = long_len(P, b);
-  const int64_t base = (int64_t)b * P.lg.pb;
-  double* th = J.theta + (int64_t)s * J.th_stride + base;
-  const float* xin = J.in + (int64_t)s * J.in_stride + base;
-  const double wf = 2.0 * kPi * (cfg.freq / cfg.fs);
-  const double offb = LB->x[5];
-  const double a00 = 1.0 - (k2Pi * (cfg.kp + cfg.ki)) * kInv2Pi, a10 = -(k2Pi * cfg.ki) * kInv2Pi;
-  // thread t takes steps t, t + FIX_T, ... (coalesced); its corrections step by M = A^FIX_T
-  auto apply_pow = [&](int64_t e, double& vp, double& vv) {   // (vp, vv) = A^e (vp, vv)
-    double M00 = a00, M01 = 1.0, M10 = a10, M11 = 1.0;
-    for (; e > 0; e >>= 1) {
-      if (e & 1) {
-        const double np = M00 * vp + M01 * vv, nv = M10 * vp + M11 * vv;
-        vp = np; vv = nv;
-      }
-      const double n00 = M00 * M00 + M01 * M10, n01 = M00 * M01 + M01 * M11;
-      const double n10 = M10 * M00 + M11 * M10, n11 = M10 * M01 + M11 * M11;
-      M00 = n00; M01 = n01; M10 = n10; M11 = n11;
-    }
-  };
-  double S00 = 1.0, S01 = 0.0, S10 = 0.0, S11 = 1.0;              // M = A^FIX_T
-  {
-    double c0p = 1.0, c0v = 0.0, c1p = 0.0, c1v = 1.0;
-    apply_pow(FIX_T, c0p, c0v);
-    apply_pow(FIX_T, c1p, c1v);
-    S00 = c0p; S10 = c0v; S01 = c1p; S11 = c1v;
-  }
-  const double tol = 1e-6;
-  bool bad = false;
-  {
-    // check: the correction of the phase before step k moves fract(t_k) inside (0, 1)
-    double vp = dp, vv = dv;
-    apply_pow(tid, vp, vv);                                       // before step tid
-    for (int64_t k = tid; k < n; k += FIX_T) {
-      if (k == 0) {                              // the literal step: atan2 of the start's (fI, fQ)
-        const double offp = offb - (double)P.lg.pb;
-        const double arg = wf * ((offp + (double)(P.lg.pb - 1)) + 1.0) + LB->u[1];
-        const double xv = (double)xin[0];
-        const double e = atan2(xv * (-sin(arg)), xv * cos(arg));
-        bad |= !(fabs(e - vp) < kPi - tol);
-      } else {
-        const double t = fma(-kInv2Pi, th[k - 1], pll_c(xin[k], wf, offb + (double)k));
-        const double f = t - floor(t) - vp * kInv2Pi;
-        bad |= !(f > tol && f < 1.0 - tol);
-      }
-      const double np = S00 * vp + S01 * vv, nv = S10 * vp + S11 * vv;
-      vp = np; vv = nv;
-    }
-  }
-  if (__syncthreads_or(bad)) return;             // the spec kernel re-solves it from x
-  {
-    // apply: theta_k += 2 pi n + (A^(k+1) d)_phase
-    double vp = dp, vv = dv;
-    apply_pow(tid + 1, vp, vv);
-    for (int64_t k = tid; k < n; k += FIX_T) {
-      th[k] = fma(nsh, kP1, fma(nsh, kP2, th[k])) + vp;
-      const double np = S00 * vp + S01 * vv, nv = S10 * vp + S11 * vv;
-      vp = np; vv = nv;
-    }
-  }
-  if (tid == 0) {
-    const double* ph = (b == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
-    LB->e[1] = fma(nsh, kP1, fma(nsh, kP2, LB->e[1])) + (ph[0] * dp + ph[1] * dv);
-    LB->e[0] = LB->e[0] + (ph[2] * dp + ph[3] * dv);
-    LB->u[0] = LB->x[0];
-    LB->u[1] = LB->x[1];
-    LB->status = LB_DONE_X;
-  }
 }
 
 // 3. The chain: one wave per recurrence, one lane per pseudo-block of a 64-block window (the
@@ -1251,6 +1147,7 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
     int sj = -1;
     double ap = 0.0, ai = 0.0, ep = 0.0, ei = 0.0, anp = 0.0, ani = 0.0;
     int solver = 0;
+    double margin = -1.0;
     if (valid) {
       const LongBlk* B = long_blk(P, r, j);
       sj = B->status;
@@ -1260,6 +1157,7 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
       ep = B->e[1];
       ei = B->e[0];
       solver = B->solver;
+      margin = B->margin;
     }
     const bool solved = valid && (sj == LB_DONE_G || sj == LB_DONE_X);
     anp = __shfl_down(ap, 1, 64);
@@ -1295,7 +1193,12 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
     // whole turns: n_0 from the carry, then the prefix sum of the outgoing integers
     const double nj = n0 + (wave_prefix_sum(dn, lane) - dn);
     const double err = c1 * fabs(rp) + c2 * fabs(rv);
-    const bool acc = solved && err <= LONG_ACCEPT;
+    // accepted: the solve started within LONG_ACCEPT of the chained start, or within the linear
+    // bound with every step's wrap further from the boundary than the largest phase deviation
+    // err (then no integer m_k moves: the block's phases + its linear response to the start
+    // error rho are the recurrence's, up to rounding -- nco_long_kernel adds the response)
+    const bool lina = err <= LONG_LINEAR && k2Pi * (margin - LONG_MARGIN_TOL) > err;
+    const bool acc = solved && (err <= LONG_ACCEPT || lina);
     const bool lin = solved && err <= LONG_LINEAR;   // (a NaN fails both)
     const uint64_t notacc = __ballot(!acc);          // (invalid lanes are never accepted)
     const uint64_t notlin = __ballot(!lin);
@@ -1303,17 +1206,29 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
     const int fs = notlin ? __builtin_ctzll(notlin) : 64;    // the first block the chain cannot pass
     const int nacc = cexact ? fa : 0;
     // this block's chained start S_j = A_j + 2 pi n_j + rho_j (exact for lanes <= nacc)
-    const double sp = fma(nj, kP1, fma(nj, kP2, ap)) + rp, si = ai + rv;
+    double sp = fma(nj, kP1, fma(nj, kP2, ap)) + rp, si = ai + rv;
+    // an unsolved block right after the exact prefix (its solve failed: no start from it): the
+    // exact start is the previous block's end + its turns (lane 0: the carry)
+    {
+      const double pep = __shfl_up(ep, 1, 64), pei = __shfl_up(ei, 1, 64), pnj = __shfl_up(nj, 1, 64);
+      if (lane == nacc && !solved) {
+        if (lane == 0) { sp = Cp; si = Ci; }
+        else { sp = fma(pnj, kP1, fma(pnj, kP2, pep)); si = pei; }
+      }
+    }
     if (valid && lane <= fs) {
       LongBlk* B = long_blk(P, r, j);
       if (lane < nacc) {
         B->status = LB_ACCEPTED;
         B->shift = nj;
+        B->d[0] = err <= LONG_ACCEPT ? 0.0 : rp;      // the linear response the NCO kernel adds
+        B->d[1] = err <= LONG_ACCEPT ? 0.0 : rv;
         stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
         stat_add(P.stats, solver == SOLVER_SEQ ? SDR_PLL_ST_SEQUENTIAL : SDR_PLL_ST_SPEC_R0 + solver, 1);
-        stat_add(P.stats, sj == LB_DONE_G ? SDR_PLL_ST_LONG_GUESSED : SDR_PLL_ST_LONG_CHAINED, 1);
-        stat_max(P.stats, SDR_PLL_ST_LONG_MAXGAP, err);
-      } else if (!acc && solved) {                    // re-solve from the chained start
+        stat_add(P.stats, sj == LB_DONE_G && err <= LONG_ACCEPT ? SDR_PLL_ST_LONG_GUESSED : SDR_PLL_ST_LONG_CHAINED, 1);
+        if (err <= LONG_ACCEPT) stat_max(P.stats, SDR_PLL_ST_LONG_MAXGAP, err);
+        else stat_add(P.stats, SDR_PLL_ST_LONG_LINEAR, 1);
+      } else if (!acc && (solved || (lane == nacc && cexact))) {   // re-solve from the chained start
         if (lane == fs) stat_add(P.stats, SDR_PLL_ST_LONG_STOPS, 1);
 #ifdef SDR_PLL_LONG_DEBUG
         if (lane == fs)
@@ -1321,6 +1236,7 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
 #endif
         B->u[0] = ai;
         B->u[1] = ap;
+        if (!solved) B->solver = -1;                  // (nothing to fix up: re-solved whole)
         const double offp = off0 + (double)((int64_t)(j - 1) * pb);
         const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + sp;
         B->x[0] = si;
@@ -1337,8 +1253,10 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
     if (nacc > 0) {
       const int l = nacc - 1;
       const double ep_l = __shfl(ep, l, 64), ei_l = __shfl(ei, l, 64), n_l = __shfl(nj, l, 64);
-      Xp = fma(n_l, kP1, fma(n_l, kP2, ep_l));
-      Xi = ei_l;
+      const double rp_l = __shfl(rp, l, 64), rv_l = __shfl(rv, l, 64);
+      const double* phl = (w0 + l == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
+      Xp = fma(n_l, kP1, fma(n_l, kP2, ep_l)) + (phl[0] * rp_l + phl[1] * rv_l);
+      Xi = ei_l + (phl[2] * rp_l + phl[3] * rv_l);
       pos = w0 + nacc;
     }
     if (fs < 64 || w0 + 64 >= nb) break;              // the chain cannot pass block fs this round
@@ -1384,7 +1302,10 @@ __global__ __launch_bounds__(64) void pll_long_tail_kernel(PllJobs P) {
   const PllJob& J = P.j[q];
   const PllCfg cfg = J.cfg;
   double* st = J.state + (int64_t)s * 6;
-  for (int b = pos + threadIdx.x; b < nb; b += 64) long_blk(P, r, b)->shift = 0.0;
+  for (int b = pos + threadIdx.x; b < nb; b += 64) {
+    long_blk(P, r, b)->shift = 0.0;
+    long_blk(P, r, b)->d[0] = long_blk(P, r, b)->d[1] = 0.0;
+  }
   if (threadIdx.x != 0) return;
   const int64_t pb = P.lg.pb;
   const int64_t base = (int64_t)pos * pb;
@@ -1461,10 +1382,6 @@ __global__ void nco_jobs_kernel(PllJobs P) {
     const double i = (double)(k % PG);
     p = p - (kPi * J.cfg.ki) * ((i + 1.0) * i * 0.5);
   }
-  if (P.n > SPEC_NMAX) {                                // long call: the chain's 2 pi shift of the block
-    const double n2 = long_blk(P, q * P.nstreams + s, (int)(k / P.lg.pb))->shift;
-    p = fma(n2, kP1, fma(n2, kP2, p));
-  }
   const double th = w * ((off + (double)k) + 1.0) + p;
   const double a = th * J.cfg.scale + J.cfg.adj;
   // the reference's angle grows with the stream (~1e7 rad after a minute): reduced here by the
@@ -1474,6 +1391,69 @@ __global__ void nco_jobs_kernel(PllJobs P) {
   sincos(reduce_2pi(a), &sv, &cv);
   J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
   if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
+}
+
+
+// The NCO of a long call: phaseEst_k = the stored phase + 2 pi (the chain's turns for its
+// pseudo-block) + (A^(kk+1) d)_phase, the loop's linear response to the start error d the
+// chain accepted the pseudo-block with (kk: the step within it; zero for most blocks).
+// Workgroup: 256 x NCO_NR consecutive steps of one recurrence, thread t the steps t + 256 i
+// (coalesced), its responses 256 steps apart by A^256; A^(2^i) in LDS.
+constexpr int NCO_NR = 8;
+__global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
+#pragma clang fp contract(off)
+  __shared__ Mat2 ap[15];
+  const int g = blockIdx.y;                 // uniform: (job, stream) = the recurrence
+  const int q = g / P.nstreams;
+  const int s = g - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const PllCfg cfg = J.cfg;
+  if (threadIdx.x == 0) {
+    Mat2 x{1.0 - (k2Pi * (cfg.kp + cfg.ki)) * kInv2Pi, 1.0, -(k2Pi * cfg.ki) * kInv2Pi, 1.0};
+    for (int i = 0; i < 15; ++i, x = mmul(x, x)) ap[i] = x;
+  }
+  __syncthreads();
+  const double* ph = J.theta + (int64_t)s * J.th_stride;
+  const double off = ph[P.n];
+  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  const int64_t pb = P.lg.pb;
+  int bcur = -1;
+  double sh = 0.0, vp = 0.0, vv = 0.0;
+  bool lin = false;
+  for (int i = 0; i < NCO_NR; ++i) {
+    const int64_t k = ((int64_t)blockIdx.x * NCO_NR + i) * 256 + threadIdx.x;
+    if (k >= P.n) break;
+    const int b = (int)(k / pb);
+    if (b != bcur) {                         // a new pseudo-block: its shift and A^(kk+1) d
+      bcur = b;
+      const LongBlk* B = long_blk(P, g, b);
+      sh = B->shift;
+      vp = B->d[0];
+      vv = B->d[1];
+      lin = vp != 0.0 || vv != 0.0;
+      if (lin) {
+        int e = (int)(k - (int64_t)b * pb) + 1;
+        for (int j = 0; e > 0; ++j, e >>= 1)
+          if (e & 1) {
+            const Mat2 m = ap[j];
+            const double np = m.a * vp + m.b * vv, nv = m.c * vp + m.d * vv;
+            vp = np; vv = nv;
+          }
+      }
+    } else if (lin) {                        // 256 steps on: A^256
+      const Mat2 m = ap[8];
+      const double np = m.a * vp + m.b * vv, nv = m.c * vp + m.d * vv;
+      vp = np; vv = nv;
+    }
+    double p = fma(sh, kP1, fma(sh, kP2, ph[k]));
+    if (lin) p = p + vp;
+    const double th = w * ((off + (double)k) + 1.0) + p;
+    const double a = th * cfg.scale + cfg.adj;
+    double sv, cv;
+    sincos(reduce_2pi(a), &sv, &cv);
+    J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
+    if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
+  }
 }
 
 }  // namespace
@@ -1509,8 +1489,12 @@ namespace {
 // ---- long calls: host-side setup ---------------------------------------------------
 bool pll_long(const PllJobs& P) { return P.n > SPEC_NMAX; }
 
+// pseudo-blocks of <= LONG_PB steps: with a pre-roll of <= LONG_PRE_MAX steps one solve is at
+// most SPEC_NMAX - 1 steps (its LDS image)
+constexpr int LONG_PRE_MAX = 2048;
+constexpr int LONG_PB = SPEC_NMAX - 1 - LONG_PRE_MAX;
 void long_geom(int64_t n, int64_t* pb, int* nb) {
-  const int64_t k = (n + 16383) / 16384;          // pseudo-blocks of <= 16 384 steps
+  const int64_t k = (n + LONG_PB - 1) / LONG_PB;
   *nb = (int)k;
   *pb = (n + k - 1) / k;
 }
@@ -1555,14 +1539,15 @@ void loop_bounds(const PllCfg& c, double* c1, double* c2) {
   *c2 = m2;
 }
 
-// warm-up length: the error contracts by sqrt(1 - Kp) per step; enough steps to bring the seed's
-// error (the measured phase: ~0.1 rad) within LONG_ACCEPT (the stereo loop: ~1 500), unless
-// that exceeds SDR_PLL_WARM_MAX (default 2 048: the RDS loop would need ~15 000) -- then 1 024
-// steps, enough for the linear bound; such blocks are fixed up from the chained start.
+// pre-roll length: the error contracts by sqrt(1 - Kp) per step; enough steps to bring the
+// seed's error (the measured phase: ~0.1 rad) within LONG_ACCEPT (the stereo loop: ~1 500),
+// unless that exceeds SDR_PLL_WARM_MAX (default and most LONG_PRE_MAX = 2 048: the RDS loop
+// would need ~15 000) -- then 1 024 steps, enough for the linear bound; such blocks are fixed
+// up from the chained start.
 int warm_len(const PllCfg& c, double c1, int64_t pb) {
   static const int cap = [] {
     const char* e = getenv("SDR_PLL_WARM_MAX");
-    return e ? std::max(64, atoi(e)) : 2048;
+    return e ? std::min(std::max(64, atoi(e)), LONG_PRE_MAX) : LONG_PRE_MAX;
   }();
   const double rate = -0.5 * std::log1p(-std::min(std::max(c.kp, 1e-12), 0.999));
   const double want = std::log(std::max(c1, 1.0) * 0.1 / LONG_ACCEPT) / rate;   // from a 0.1 rad seed
@@ -1624,9 +1609,8 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     if (e != hipSuccess) return e;
     const int R = L.njobs * L.nstreams;
     const unsigned blocks = (unsigned)(R * L.lg.nb);
-    hipLaunchKernelGGL(pll_warm_kernel, dim3((unsigned)(R * ((L.lg.nb + WARM_LPW - 1) / WARM_LPW))), dim3(64), 0, st, L);
+    hipLaunchKernelGGL(pll_long_init_kernel, dim3((unsigned)(((int64_t)R * L.lg.nb + 255) / 256)), dim3(256), 0, st, L);
     for (int round = 0; round < LONG_ROUNDS; ++round) {
-      if (round > 0) hipLaunchKernelGGL(pll_long_fix_kernel, dim3(blocks), dim3(FIX_T), 0, st, L);
       hipLaunchKernelGGL((pll_spec_kernel<512, true>), dim3(blocks), dim3(512), 0, st, L);
       hipLaunchKernelGGL(pll_long_seq_kernel, dim3((unsigned)(R * ((L.lg.nb + 63) / 64))), dim3(64), 0, st, L);
       hipLaunchKernelGGL(pll_long_chain_kernel, dim3((unsigned)R), dim3(64), 0, st, L, round);
@@ -1658,7 +1642,10 @@ hipError_t sdr_launch_pll_nco(const PllJobs& P, hipStream_t st) {
     e = long_setup(L);
     if (e != hipSuccess) return e;
   }
-  if (P.n > 0)
+  if (pll_long(P))
+    hipLaunchKernelGGL(nco_long_kernel, dim3((unsigned)((P.n + 256 * NCO_NR - 1) / (256 * NCO_NR)), (unsigned)(P.njobs * P.nstreams)),
+                       dim3(256), 0, st, L);
+  else if (P.n > 0)
     hipLaunchKernelGGL(nco_jobs_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
                        dim3(256), 0, st, L);
   return hipGetLastError();

@@ -62,3 +62,13 @@ def maxabs(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.max(np.abs(a - b))) if a.size else 0.0
+
+
+# the long-call PLL's pseudo-block geometry (csrc/pll.hip long_geom: <= 14 336 steps, so that a
+# pseudo-block plus its pre-roll of <= 2 048 steps is one 16 384-step solve)
+LONG_PB = 14336
+
+
+def long_blocks(n):
+    """pseudo-blocks of a PLL call of n samples (1: a per-block call)"""
+    return 1 if n <= 16385 else -(-n // LONG_PB)

@@ -10,7 +10,7 @@ the PLL solver counters asserted (every pseudo-block solved in parallel)."""
 import numpy as np
 import pytest
 
-from conftest import maxabs, rms
+from conftest import long_blocks, maxabs, rms
 from test_receiver import AUDIO_MAX, AUDIO_RMS, RDS_TOL
 
 pytestmark = pytest.mark.gpu
@@ -48,7 +48,7 @@ def test_span_receiver_equals_block_loop_and_oracle(sdr, gpu_ctx, oracle):
         got = span_rx.process(iq[:, 2 * sp * K * B5:2 * (sp + 1) * K * B5], fetch=NAMES)
         st = span_rx.pll_stats()
         print(f"span {sp} solver counters:", st)
-        nb = -(-K * (B5 // 10) // 16384)
+        nb = long_blocks(K * (B5 // 10))
         assert st["recurrences"] == S * 2 * nb, st
         assert st["long_guessed"] + st["long_chained"] == S * 2 * nb, st
         # the first span starts at the stream start: the loops acquire over its first pseudo-blocks
