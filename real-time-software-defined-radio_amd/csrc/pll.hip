@@ -1110,20 +1110,28 @@ __global__ __launch_bounds__(64) void pll_long_seq_kernel(PllJobs P) {
   B->solver = SOLVER_SEQ;
 }
 
-// 3. The chain: one wave per recurrence, one lane per pseudo-block of a 64-block window (the
-// windows in order).  With A_j the start block j's current solution was solved from, E_j its
-// end and S_j the chained start, the residual R_j = S_j - A_j splits into n_j whole turns and
-// rho_j = R_j - 2 pi n_j, and
+// 3. The chain: one workgroup per recurrence, one thread per pseudo-block of a CHAIN_T-block
+// window (the windows in order; one window up to 7 M samples).  With A_j the start block j's
+// current solution was solved from, E_j its end and S_j the chained start, the residual
+// R_j = S_j - A_j splits into n_j whole turns and rho_j = R_j - 2 pi n_j, and
 //     R_{j+1} = (E_j - A_{j+1}) + 2 pi n_j + Phi_j rho_j.
-// |Phi_j| <= 2e-9 (the loop matrix over a pseudo-block), so the turns are a prefix sum of the
+// |Phi_j| <= 1e-8 (the loop matrix over a pseudo-block), so the turns are a prefix sum of the
 // local integers rint((E_j - A_{j+1})_phase / 2 pi), and rho_{j+1} = C_j + Phi_j C_{j-1} to f64
-// rounding (C_j = E_j - A_{j+1} less its turns; the term after is Phi^2 ~ 1e-18 rad).  Then per
+// rounding (C_j = E_j - A_{j+1} less its turns; the term after is Phi^2 ~ 1e-16 rho).  Then per
 // block the bound err = c1 |rho_p| + c2 |rho_v| decides, as described above; a prefix of
 // accepted blocks moves the chain's position.
-__global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round) {
+constexpr int CHAIN_T = 512;
+__global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int round) {
 #pragma clang fp contract(off)
+  constexpr int NWV = CHAIN_T / 64;
+  __shared__ double sA[2][CHAIN_T + 1];    // A_j (phase, integrator), and the next window's first
+  __shared__ double sC[2][CHAIN_T];        // C_j
+  __shared__ double sE[3][CHAIN_T];        // E_j + 2 pi n_j (phase), E_j (integrator), and n_j
+  __shared__ double sR[2][CHAIN_T];        // rho_j
+  __shared__ double wtot[NWV];
+  __shared__ int wfa[NWV], wfs[NWV];
   const int r = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nb = P.lg.nb;
   LongHdr* H = long_hdr(P, r);
   const int pos0 = H->pos;
@@ -1140,14 +1148,11 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
   bool cexact = true;                // ... exact (else provisional)
   int pos = pos0;
   double Xp = Cp, Xi = Ci;           // the exact state at `pos`
-  for (int w0 = pos0; w0 < nb; w0 += 64) {
-    const int j = w0 + lane;
+  for (int w0 = pos0; w0 < nb; w0 += CHAIN_T) {
+    const int j = w0 + tid;
     const bool valid = j < nb;
-    // this block's start, end and status; the next block's start
-    int sj = -1;
-    double ap = 0.0, ai = 0.0, ep = 0.0, ei = 0.0, anp = 0.0, ani = 0.0;
-    int solver = 0;
-    double margin = -1.0;
+    int sj = -1, solver = 0;
+    double ap = 0.0, ai = 0.0, ep = 0.0, ei = 0.0, margin = -1.0;
     if (valid) {
       const LongBlk* B = long_blk(P, r, j);
       sj = B->status;
@@ -1160,38 +1165,50 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
       margin = B->margin;
     }
     const bool solved = valid && (sj == LB_DONE_G || sj == LB_DONE_X);
-    anp = __shfl_down(ap, 1, 64);
-    ani = __shfl_down(ai, 1, 64);
-    if (lane == 63 && j + 1 < nb) {                 // the next window's first block
-      const LongBlk* B = long_blk(P, r, j + 1);
-      const bool fromg = B->status == LB_DONE_G;
-      anp = fromg ? B->g[1] : B->x[1];
-      ani = fromg ? B->g[0] : B->x[0];
+    sA[0][tid] = ap;
+    sA[1][tid] = ai;
+    if (tid == CHAIN_T - 1) {                       // the next window's first block
+      double np = 0.0, ni = 0.0;
+      if (j + 1 < nb) {
+        const LongBlk* B = long_blk(P, r, j + 1);
+        const bool fromg = B->status == LB_DONE_G;
+        np = fromg ? B->g[1] : B->x[1];
+        ni = fromg ? B->g[0] : B->x[0];
+      }
+      sA[0][CHAIN_T] = np;
+      sA[1][CHAIN_T] = ni;
     }
+    __syncthreads();
+    const double anp = sA[0][tid + 1], ani = sA[1][tid + 1];
+    const double a0p = sA[0][0], a0i = sA[1][0];
     const double* ph = (j == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
-    // C_j = E_j - A_{j+1} less its turns (this lane's outgoing step)
+    // C_j = E_j - A_{j+1} less its turns (this block's outgoing step)
     const double cd = ep - anp;
     const double dn = rint(cd * kInv2Pi);
     const double cp = fma(-dn, kP2, fma(-dn, kP1, cd));
     const double cv = ei - ani;
-    // lane 0's residual from the carried start
-    const double d0 = Cp - __shfl(ap, 0, 64);
+    sC[0][tid] = cp;
+    sC[1][tid] = cv;
+    // the first block's residual from the carried start
+    const double d0 = Cp - a0p;
     const double n0 = rint(d0 * kInv2Pi);
-    const double r0p = fma(-n0, kP2, fma(-n0, kP1, d0)), r0v = Ci - __shfl(ai, 0, 64);
-    // rho_j: lane 0 the carried one; lane l: C_{l-1} + Phi_{l-1} C_{l-2} (lane 1: ... rho_0)
-    const double pcp = __shfl_up(cp, 1, 64), pcv = __shfl_up(cv, 1, 64);     // C_{l-1}
-    const double ppcp = __shfl_up(cp, 2, 64), ppcv = __shfl_up(cv, 2, 64);   // C_{l-2}
-    const double f0 = __shfl_up(ph[0], 1, 64), f1 = __shfl_up(ph[1], 1, 64); // Phi_{l-1}
-    const double f2 = __shfl_up(ph[2], 1, 64), f3 = __shfl_up(ph[3], 1, 64);
-    double rp, rv;
-    if (lane == 0) { rp = r0p; rv = r0v; }
-    else {
-      const double qp = lane == 1 ? r0p : ppcp, qv = lane == 1 ? r0v : ppcv;
-      rp = pcp + (f0 * qp + f1 * qv);
-      rv = pcv + (f2 * qp + f3 * qv);
-    }
+    const double r0p = fma(-n0, kP2, fma(-n0, kP1, d0)), r0v = Ci - a0i;
     // whole turns: n_0 from the carry, then the prefix sum of the outgoing integers
-    const double nj = n0 + (wave_prefix_sum(dn, lane) - dn);
+    double pre_dn = wave_prefix_sum(dn, lane);
+    if (lane == 63) wtot[wv] = pre_dn;
+    __syncthreads();
+    for (int i = 0; i < wv; ++i) pre_dn += wtot[i];
+    const double nj = n0 + (pre_dn - dn);
+    // rho_j: block 0 the carried one; block l: C_{l-1} + Phi_{l-1} C_{l-2} (block 1: ... rho_0)
+    double rp, rv;
+    if (tid == 0) { rp = r0p; rv = r0v; }
+    else {
+      const double* pp = P.lg.phi[q];                // Phi_{l-1}: l - 1 < nb - 1
+      const double pcp = sC[0][tid - 1], pcv = sC[1][tid - 1];
+      const double qp = tid == 1 ? r0p : sC[0][tid - 2], qv = tid == 1 ? r0v : sC[1][tid - 2];
+      rp = pcp + (pp[0] * qp + pp[1] * qv);
+      rv = pcv + (pp[2] * qp + pp[3] * qv);
+    }
     const double err = c1 * fabs(rp) + c2 * fabs(rv);
     // accepted: the solve started within LONG_ACCEPT of the chained start, or within the linear
     // bound with every step's wrap further from the boundary than the largest phase deviation
@@ -1200,25 +1217,38 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
     const bool lina = err <= LONG_LINEAR && k2Pi * (margin - LONG_MARGIN_TOL) > err;
     const bool acc = solved && (err <= LONG_ACCEPT || lina);
     const bool lin = solved && err <= LONG_LINEAR;   // (a NaN fails both)
-    const uint64_t notacc = __ballot(!acc);          // (invalid lanes are never accepted)
-    const uint64_t notlin = __ballot(!lin);
-    const int fa = notacc ? __builtin_ctzll(notacc) : 64;    // accepted prefix (if the carry is exact)
-    const int fs = notlin ? __builtin_ctzll(notlin) : 64;    // the first block the chain cannot pass
-    const int nacc = cexact ? fa : 0;
-    // this block's chained start S_j = A_j + 2 pi n_j + rho_j (exact for lanes <= nacc)
-    double sp = fma(nj, kP1, fma(nj, kP2, ap)) + rp, si = ai + rv;
-    // an unsolved block right after the exact prefix (its solve failed: no start from it): the
-    // exact start is the previous block's end + its turns (lane 0: the carry)
+    // the first block not accepted / not within the linear bound (CHAIN_T: none)
     {
-      const double pep = __shfl_up(ep, 1, 64), pei = __shfl_up(ei, 1, 64), pnj = __shfl_up(nj, 1, 64);
-      if (lane == nacc && !solved) {
-        if (lane == 0) { sp = Cp; si = Ci; }
-        else { sp = fma(pnj, kP1, fma(pnj, kP2, pep)); si = pei; }
+      const uint64_t na = __ballot(!acc), nl = __ballot(!lin);   // (invalid blocks are neither)
+      if (lane == 0) {
+        wfa[wv] = na ? wv * 64 + __builtin_ctzll(na) : CHAIN_T;
+        wfs[wv] = nl ? wv * 64 + __builtin_ctzll(nl) : CHAIN_T;
       }
     }
-    if (valid && lane <= fs) {
+    const double ejp = fma(nj, kP1, fma(nj, kP2, ep));  // E_j + 2 pi n_j
+    sE[0][tid] = ejp;
+    sE[1][tid] = ei;
+    sE[2][tid] = nj;
+    sR[0][tid] = rp;
+    sR[1][tid] = rv;
+    __syncthreads();
+    int fa = CHAIN_T, fs = CHAIN_T;
+    for (int i = 0; i < NWV; ++i) {
+      fa = min(fa, wfa[i]);
+      fs = min(fs, wfs[i]);
+    }
+    const int nacc = cexact ? fa : 0;
+    // this block's chained start S_j = A_j + 2 pi n_j + rho_j (exact for blocks <= nacc)
+    double sp = fma(nj, kP1, fma(nj, kP2, ap)) + rp, si = ai + rv;
+    // an unsolved block right after the exact prefix (its solve failed: no start from it): the
+    // exact start is the previous block's end + its turns (block 0: the carry)
+    if (tid == nacc && !solved) {
+      if (tid == 0) { sp = Cp; si = Ci; }
+      else { sp = sE[0][tid - 1]; si = sE[1][tid - 1]; }
+    }
+    if (valid && tid <= fs) {
       LongBlk* B = long_blk(P, r, j);
-      if (lane < nacc) {
+      if (tid < nacc) {
         B->status = LB_ACCEPTED;
         B->shift = nj;
         B->d[0] = err <= LONG_ACCEPT ? 0.0 : rp;      // the linear response the NCO kernel adds
@@ -1228,15 +1258,15 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
         stat_add(P.stats, sj == LB_DONE_G && err <= LONG_ACCEPT ? SDR_PLL_ST_LONG_GUESSED : SDR_PLL_ST_LONG_CHAINED, 1);
         if (err <= LONG_ACCEPT) stat_max(P.stats, SDR_PLL_ST_LONG_MAXGAP, err);
         else stat_add(P.stats, SDR_PLL_ST_LONG_LINEAR, 1);
-      } else if (!acc && (solved || (lane == nacc && cexact))) {   // re-solve from the chained start
-        if (lane == fs) stat_add(P.stats, SDR_PLL_ST_LONG_STOPS, 1);
+      } else if (!acc && (solved || (tid == nacc && cexact))) {   // re-solve from the chained start
+        if (tid == fs) stat_add(P.stats, SDR_PLL_ST_LONG_STOPS, 1);
 #ifdef SDR_PLL_LONG_DEBUG
-        if (lane == fs)
+        if (tid == fs)
           printf("chain r%d b%d/%d status %d: err %.3e rho %.3e %.3e n %.0f\n", r, j, nb, sj, err, rp, rv, nj);
 #endif
         B->u[0] = ai;
         B->u[1] = ap;
-        if (!solved) B->solver = -1;                  // (nothing to fix up: re-solved whole)
+        if (!solved) B->solver = -1;
         const double offp = off0 + (double)((int64_t)(j - 1) * pb);
         const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + sp;
         B->x[0] = si;
@@ -1249,30 +1279,29 @@ __global__ __launch_bounds__(64) void pll_long_chain_kernel(PllJobs P, int round
         B->status = LB_NEED_X;
       }
     }
-    // the state after the accepted prefix; the carry into the next window
+    // the state after the accepted prefix: E + 2 pi n + Phi rho of its last block
     if (nacc > 0) {
       const int l = nacc - 1;
-      const double ep_l = __shfl(ep, l, 64), ei_l = __shfl(ei, l, 64), n_l = __shfl(nj, l, 64);
-      const double rp_l = __shfl(rp, l, 64), rv_l = __shfl(rv, l, 64);
       const double* phl = (w0 + l == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
-      Xp = fma(n_l, kP1, fma(n_l, kP2, ep_l)) + (phl[0] * rp_l + phl[1] * rv_l);
-      Xi = ei_l + (phl[2] * rp_l + phl[3] * rv_l);
+      Xp = sE[0][l] + (phl[0] * sR[0][l] + phl[1] * sR[1][l]);
+      Xi = sE[1][l] + (phl[2] * sR[0][l] + phl[3] * sR[1][l]);
       pos = w0 + nacc;
     }
-    if (fs < 64 || w0 + 64 >= nb) break;              // the chain cannot pass block fs this round
-    // carry: S_{w0+64} = E_63 + 2 pi n_63 + Phi_63 rho_63
-    const double e63p = __shfl(ep, 63, 64), e63i = __shfl(ei, 63, 64), n63 = __shfl(nj, 63, 64);
-    const double r63p = __shfl(rp, 63, 64), r63v = __shfl(rv, 63, 64);
-    const double g0 = __shfl(ph[0], 63, 64), g1 = __shfl(ph[1], 63, 64), g2 = __shfl(ph[2], 63, 64),
-                 g3 = __shfl(ph[3], 63, 64);
-    Cp = fma(n63, kP1, fma(n63, kP2, e63p)) + (g0 * r63p + g1 * r63v);
-    Ci = e63i + (g2 * r63p + g3 * r63v);
-    cexact = cexact && fa == 64;
+    if (fs < CHAIN_T || w0 + CHAIN_T >= nb) break;     // the chain cannot pass block fs this round
+    // carry: S_{w0+CHAIN_T} = E_last + 2 pi n_last + Phi_last rho_last
+    {
+      const int l = CHAIN_T - 1;
+      const double* pp = P.lg.phi[q];
+      Cp = sE[0][l] + (pp[0] * sR[0][l] + pp[1] * sR[1][l]);
+      Ci = sE[1][l] + (pp[2] * sR[0][l] + pp[3] * sR[1][l]);
+    }
+    cexact = cexact && fa == CHAIN_T;
+    __syncthreads();                                    // the window's LDS read before the next writes it
   }
 #ifdef SDR_PLL_LONG_DEBUG
-  if (lane == 0) printf("chain r%d round %d: position %d -> %d of %d\n", r, round, pos0, pos, nb);
+  if (tid == 0) printf("chain r%d round %d: position %d -> %d of %d\n", r, round, pos0, pos, nb);
 #endif
-  if (lane == 0) {
+  if (tid == 0) {
     H->pos = pos;
     H->sp = Xp;
     H->si = Xi;
@@ -1613,7 +1642,7 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     for (int round = 0; round < LONG_ROUNDS; ++round) {
       hipLaunchKernelGGL((pll_spec_kernel<512, true>), dim3(blocks), dim3(512), 0, st, L);
       hipLaunchKernelGGL(pll_long_seq_kernel, dim3((unsigned)(R * ((L.lg.nb + 63) / 64))), dim3(64), 0, st, L);
-      hipLaunchKernelGGL(pll_long_chain_kernel, dim3((unsigned)R), dim3(64), 0, st, L, round);
+      hipLaunchKernelGGL(pll_long_chain_kernel, dim3((unsigned)R), dim3(CHAIN_T), 0, st, L, round);
     }
     hipLaunchKernelGGL(pll_long_tail_kernel, dim3((unsigned)R), dim3(64), 0, st, L);
     return hipGetLastError();

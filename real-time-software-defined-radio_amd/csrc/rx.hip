@@ -157,15 +157,28 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
     mr[r] = (J.mono != nullptr && mf + r < M) ? J.mono[(int64_t)s * J.y_stride + mf + r] : 0.f;
   }
   if (n_lo >= 0 && n_lo + S::LG <= J.n) {            // interior: 16-B loads (rows are aligned)
-    constexpr int NCH = S::LG / S::G;
-    for (int q = t; q < NCH; q += S::NT) {
-      const float4 v = reinterpret_cast<const float4*>(xb + n_lo)[q];
-      const float4 cv = pre == PRE_MIX ? reinterpret_cast<const float4*>(cb + n_lo)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const int u = q * S::G;
-      lds[S::slot(u + 0)] = pre_op(pre, v.x, cv.x, g);
-      lds[S::slot(u + 1)] = pre_op(pre, v.y, cv.y, g);
-      lds[S::slot(u + 2)] = pre_op(pre, v.z, cv.z, g);
-      lds[S::slot(u + 3)] = pre_op(pre, v.w, cv.w, g);
+    // every load of the thread's chunks is issued before the first is used (one memory
+    // round trip per tile, not one per chunk)
+    constexpr int NCH = S::LG / S::G, NQ = (NCH + S::NT - 1) / S::NT;
+    float4 v[NQ], cv[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const int q = t + j * S::NT;
+      if (q < NCH) {
+        v[j] = reinterpret_cast<const float4*>(xb + n_lo)[q];
+        cv[j] = pre == PRE_MIX ? reinterpret_cast<const float4*>(cb + n_lo)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const int q = t + j * S::NT;
+      if (q < NCH) {
+        const int u = q * S::G;
+        lds[S::slot(u + 0)] = pre_op(pre, v[j].x, cv[j].x, g);
+        lds[S::slot(u + 1)] = pre_op(pre, v[j].y, cv[j].y, g);
+        lds[S::slot(u + 2)] = pre_op(pre, v[j].z, cv[j].z, g);
+        lds[S::slot(u + 3)] = pre_op(pre, v[j].w, cv[j].w, g);
+      }
     }
   } else {
     for (int u = t; u < S::LG; u += S::NT) {
