@@ -52,6 +52,18 @@ __device__ __forceinline__ void stat_add(unsigned long long* s, int k, unsigned 
 __device__ __forceinline__ void stat_max(unsigned long long* s, int k, double v) {
   if (s != nullptr && v >= 0.0) atomicMax(s + k, (unsigned long long)__double_as_longlong(v));
 }
+// wave-aggregated: every lane of the wave calls it (uniform control flow); one atomic per wave
+// for the lanes with `on` (thousands of lanes adding to one counter serialise at the L2)
+__device__ __forceinline__ void stat_add_wave(unsigned long long* s, int k, bool on) {
+  const uint64_t m = __ballot(on);
+  if (s != nullptr && m != 0 && (threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(s + k, (unsigned long long)__popcll(m));
+}
+__device__ __forceinline__ void stat_max_wave(unsigned long long* s, int k, bool on, double v) {
+  double x = on ? v : -1.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o, 64));
+  if ((threadIdx.x & 63) == 0) stat_max(s, k, x);
+}
 
 // 2*pi split into three parts (Cody-Waite), so n*P1 and n*P2 are exact for |n| < 2^26.
 constexpr double kP1 = 6.2831854820251465;       // float32(2 pi), 24 significant bits
@@ -68,6 +80,37 @@ __device__ inline double reduce_2pi(double a) {
   r = fma(-n, kP2, r);
   r = fma(-n, kP3, r);
   return r;
+}
+
+// sin and cos of a reduced angle |a| <= pi (+ an ulp), for the NCO outputs (f32: 6e-8 is their
+// rounding): quadrant n = rint(a 2/pi) (a two-part pi/2: exact to ~1e-32 for |n| <= 2), then
+// Taylor polynomials on |y| <= pi/4 to y^13 / y^14 (truncation < 3e-14).  ~35 VALU against
+// the library sincos's general-argument path.
+__device__ __forceinline__ void sincos_red(double a, double* sv, double* cv) {
+  constexpr double kPio2Hi = 1.5707963267948966, kPio2Lo = 6.123233995736766e-17, k2oPi = 0.6366197723675814;
+  const double n = rint(a * k2oPi);
+  double y = fma(-n, kPio2Hi, a);
+  y = fma(-n, kPio2Lo, y);
+  const double z = y * y;
+  double ps = 1.0 / 6227020800.0;                        // 1/13!
+  ps = fma(ps, z, -1.0 / 39916800.0);
+  ps = fma(ps, z, 1.0 / 362880.0);
+  ps = fma(ps, z, -1.0 / 5040.0);
+  ps = fma(ps, z, 1.0 / 120.0);
+  ps = fma(ps, z, -1.0 / 6.0);
+  const double sn = fma(ps * z, y, y);
+  double pc = 1.0 / 87178291200.0;                       // 1/14!
+  pc = fma(pc, z, -1.0 / 479001600.0);
+  pc = fma(pc, z, 1.0 / 3628800.0);
+  pc = fma(pc, z, -1.0 / 40320.0);
+  pc = fma(pc, z, 1.0 / 720.0);
+  pc = fma(pc, z, -1.0 / 24.0);
+  pc = fma(pc, z, 0.5);
+  const double cs = fma(-pc, z, 1.0);
+  const int q = (int)n & 3;
+  const double s0 = (q & 1) ? cs : sn, c0 = (q & 1) ? sn : cs;
+  *sv = (q == 2 || q == 3) ? -s0 : s0;
+  *cv = (q == 1 || q == 2) ? -c0 : c0;
 }
 
 // The loop's per-sample constant (pll_prep_kernel's, plain form): c_k = (sel_k - w (off + k)) / 2pi
@@ -1253,13 +1296,7 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
         B->shift = nj;
         B->d[0] = err <= LONG_ACCEPT ? 0.0 : rp;      // the linear response the NCO kernel adds
         B->d[1] = err <= LONG_ACCEPT ? 0.0 : rv;
-        stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
-        stat_add(P.stats, solver == SOLVER_SEQ ? SDR_PLL_ST_SEQUENTIAL : SDR_PLL_ST_SPEC_R0 + solver, 1);
-        stat_add(P.stats, sj == LB_DONE_G && err <= LONG_ACCEPT ? SDR_PLL_ST_LONG_GUESSED : SDR_PLL_ST_LONG_CHAINED, 1);
-        if (err <= LONG_ACCEPT) stat_max(P.stats, SDR_PLL_ST_LONG_MAXGAP, err);
-        else stat_add(P.stats, SDR_PLL_ST_LONG_LINEAR, 1);
       } else if (!acc && (solved || (tid == nacc && cexact))) {   // re-solve from the chained start
-        if (tid == fs) stat_add(P.stats, SDR_PLL_ST_LONG_STOPS, 1);
 #ifdef SDR_PLL_LONG_DEBUG
         if (tid == fs)
           printf("chain r%d b%d/%d status %d: err %.3e rho %.3e %.3e n %.0f\n", r, j, nb, sj, err, rp, rv, nj);
@@ -1278,6 +1315,17 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
         B->shift = 0.0;
         B->status = LB_NEED_X;
       }
+    }
+    {                                                   // the counters, one atomic per wave each
+      const bool a = valid && tid < nacc, ex = err <= LONG_ACCEPT;
+      stat_add_wave(P.stats, SDR_PLL_ST_RECURRENCES, a);
+      stat_add_wave(P.stats, SDR_PLL_ST_SEQUENTIAL, a && solver == SOLVER_SEQ);
+      for (int r0 = 0; r0 < SPEC_IT; ++r0) stat_add_wave(P.stats, SDR_PLL_ST_SPEC_R0 + r0, a && solver == r0);
+      stat_add_wave(P.stats, SDR_PLL_ST_LONG_GUESSED, a && sj == LB_DONE_G && ex);
+      stat_add_wave(P.stats, SDR_PLL_ST_LONG_CHAINED, a && !(sj == LB_DONE_G && ex));
+      stat_add_wave(P.stats, SDR_PLL_ST_LONG_LINEAR, a && !ex);
+      stat_max_wave(P.stats, SDR_PLL_ST_LONG_MAXGAP, a && ex, err);
+      stat_add_wave(P.stats, SDR_PLL_ST_LONG_STOPS, valid && tid == fs && !acc && (solved || (tid == nacc && cexact)));
     }
     // the state after the accepted prefix: E + 2 pi n + Phi rho of its last block
     if (nacc > 0) {
@@ -1417,7 +1465,7 @@ __global__ void nco_jobs_kernel(PllJobs P) {
   // 3-part Cody-Waite step (exact multiples of 2 pi for |n| < 2^26), sincos then takes its
   // small-argument path instead of the large-argument reduction
   double sv, cv;
-  sincos(reduce_2pi(a), &sv, &cv);
+  sincos_red(reduce_2pi(a), &sv, &cv);
   J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
   if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
 }
@@ -1479,7 +1527,7 @@ __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
     const double th = w * ((off + (double)k) + 1.0) + p;
     const double a = th * cfg.scale + cfg.adj;
     double sv, cv;
-    sincos(reduce_2pi(a), &sv, &cv);
+    sincos_red(reduce_2pi(a), &sv, &cv);
     J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
     if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
   }

@@ -1,6 +1,6 @@
 # r03 iteration: receiver/PLL/span/offset/live tests, c5 benches (block mode 64 streams, S8 span), c5 span rocprof
 set -e
-O=$GRAFT_REPO_ROOT/gpurun_out/r03_iter12
+O=$GRAFT_REPO_ROOT/gpurun_out/r03_iter13
 mkdir -p $O
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread -m gpu tests/test_pll_spec.py tests/test_span.py tests/test_offsets.py tests/test_receiver.py tests/test_dropin.py tests/test_live.py > $O/pytest.txt 2>&1
