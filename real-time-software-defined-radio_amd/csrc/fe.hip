@@ -1266,11 +1266,22 @@ static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
 
 }  // namespace
 
+// SDR_FE_MFMA=0 keeps u8 calls on fe_slot_kernel (A/B runs; read once)
+static bool fe_mfma_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SDR_FE_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Returns hipErrorInvalidValue for an unsupported (taps, decim) pair; the C-ABI
 // reports that as SDR_EUNSUPPORTED.  Supported: the reference's RF configs
 // (151 taps: model/fmMonoBlock.py:24; 101 taps: BASELINE configs) at decim 10.
 hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st) {
   if (a.D != 10) return hipErrorInvalidValue;
+  // u8 IQ: the RF FIR on the int8 matrix cores where it covers the call (fe_mfma.hip)
+  if (a.u8 && fe_mfma_enabled() && sdr_launch_fe_mfma(a, st) == hipSuccess) return hipSuccess;
   switch (a.T) {
     case 101: return launch_fe_t<101>(a, st);
     case 151: return launch_fe_t<151>(a, st);

@@ -70,6 +70,12 @@ __device__ __forceinline__ unsigned bperm(int src_lane, unsigned v) {
   return (unsigned)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
 }
 
+// The taps' fixed-point scale 2^S: the largest S with max|h| 2^S <= 2^23 - 2^16, i.e. the top
+// signed base-256 digit within [-127, 127] -- 22.x bits of the largest tap (one to two more
+// than a power-of-two bound on |h_q|; the RDS chain's pre-PLL signal, the most sensitive to the
+// RF filter, moves by 2.5e-6 of its peak instead of 8e-6: tests/test_gpu_parity.py rds)
+int tap_scale_exp(float hmax) { return (int)std::floor(std::log2((8388608.0 - 65536.0) / (double)hmax)); }
+
 // one signed base-256 digit of a fixed-point tap
 __device__ __forceinline__ int digit(int q, int k) {
   int d = 0;
@@ -300,7 +306,287 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
   }
 }
 
+// ---------------------------------------------------------------------------------
+// The same RF FIR as the FE of the block / span receivers (C5, fm_radio_gpu): demod out,
+// lfilter state in (zi, first outputs), demod phase state in (prev_phase, output 0) and out
+// (last_phi, wraps: finished by the receiver's stage-A workgroups), any stream length.
+//   T = 101: K = 256 (4 steps), OFF = 104;  T = 151: K = 320 (5 steps), OFF = 152
+// (band: 10 x 15 + T - 1 <= K - 1 with OFF >= T - 1; OFF a multiple of 8: 16-B image loads).
+// Work: contiguous runs of 256-output tiles per wave across the streams; a run starting
+// mid-stream first runs the tile before as a warm-up (its last phase is the carry).
+template <int T> struct DemodShape;
+template <> struct DemodShape<101> { static constexpr int KS = 4, OFF = 104; };
+template <> struct DemodShape<151> { static constexpr int KS = 5, OFF = 152; };
+
+struct MfmaDemod {
+  const unsigned char* iq;
+  int64_t n, stride;          // complex samples per stream / between stream bases
+  int64_t M;                  // demod samples per stream
+  int64_t tps, total;         // tiles per stream, over all streams
+  const float* taps;
+  float qscale;               // 2^S
+  const double* zi_i;         // nullable: lfilter states (T - 1 per stream, zi_stride apart)
+  const double* zi_q;
+  int64_t zi_stride;
+  const double* prev_phase;   // nullable (=> 0.0)
+  float* demod;
+  int64_t out_stride;
+  float* last_phi;            // nullable
+  int* wraps;                 // nullable
+  int vec_out;                // demod rows allow 16-B stores
+};
+
+__device__ inline double unwrap_step_f64_m(double dd, int* w) {   // fe.hip unwrap_step_f64
+  *w = 0;
+  if (fabs(dd) < 3.14159265358979323846) return dd;
+  constexpr double kPi = 3.14159265358979323846, k2Pi = 6.28318530717958647692;
+  double m = fmod(dd + kPi, k2Pi);
+  if (m < 0) m += k2Pi;
+  double ddmod = m - kPi;
+  if (ddmod == -kPi && dd > 0) ddmod = kPi;
+  *w = (int)llrint((ddmod - dd) / k2Pi);
+  return ddmod;
+}
+
+template <int T>
+__global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
+  constexpr int KS = DemodShape<T>::KS, OFF = DemodShape<T>::OFF, K = 64 * KS;
+  constexpr int IM = 160 * 15 + K;                 // image samples (16 columns of 160, K deep)
+  constexpr int NC = IM / 8, NL = (NC + 63) / 64;
+  static_assert(IM % 8 == 0 && OFF % 8 == 0 && OFF >= T - 1 && D * 15 + OFF <= K - 1, "image / band layout");
+  __shared__ __attribute__((aligned(16))) signed char img[2][IM + 16];
+
+  const int lane = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * p.total / gridDim.x;
+  const int64_t b1 = ((int64_t)blockIdx.x + 1) * p.total / gridDim.x;
+  if (b0 >= b1) return;
+  const int pl = lane & 15, gl = lane >> 4;
+
+  i4v afr[KS][3];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    int w[3][4] = {};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = D * pl + OFF - (64 * ks + 16 * gl + j);
+      const float h = (k >= 0 && k < T) ? p.taps[k] : 0.f;
+      const int q = (int)rintf(h * p.qscale);
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg) w[dg][j >> 2] |= (digit(q, dg) & 0xff) << (8 * (j & 3));
+    }
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg) afr[ks][dg] = i4v{w[dg][0], w[dg][1], w[dg][2], w[dg][3]};
+  }
+
+  f4v stg[NL];
+  const unsigned voff = 16u * lane;
+  auto n_lo_of = [&](int64_t t) { return (int64_t)TO * D * t - OFF; };
+  auto interior = [&](int64_t t) { return n_lo_of(t) >= 0 && n_lo_of(t) + IM <= p.n; };
+  auto base_of = [&](int s, int64_t t) { return p.iq + 2 * ((int64_t)s * p.stride + n_lo_of(t)); };
+  auto load_image = [&](int s, int64_t t) {
+    const unsigned char* base = base_of(s, t);
+    static_for<0, NL>([&](auto Q) {
+      constexpr int q = Q;
+      if (q < NL - 1 || lane < NC - 64 * (NL - 1)) gload16_nt_v<0>(stg[q], voff, base + 1024 * q);
+    });
+  };
+  auto put_chunk = [&](int c, unsigned w0, unsigned w1, unsigned w2, unsigned w3) {
+    const unsigned i_lo = __builtin_amdgcn_perm(w1, w0, 0x06040200u) ^ 0x80808080u;
+    const unsigned i_hi = __builtin_amdgcn_perm(w3, w2, 0x06040200u) ^ 0x80808080u;
+    const unsigned q_lo = __builtin_amdgcn_perm(w1, w0, 0x07050301u) ^ 0x80808080u;
+    const unsigned q_hi = __builtin_amdgcn_perm(w3, w2, 0x07050301u) ^ 0x80808080u;
+    *reinterpret_cast<uint2*>(&img[0][8 * c]) = make_uint2(i_lo, i_hi);
+    *reinterpret_cast<uint2*>(&img[1][8 * c]) = make_uint2(q_lo, q_hi);
+  };
+  auto store_image = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int q = 0; q < NL; ++q) {
+      const int c = lane + 64 * q;
+      if (c < NC) {
+        asm volatile("" : "+v"(stg[q]));
+        put_chunk(c, __float_as_uint(stg[q].x), __float_as_uint(stg[q].y), __float_as_uint(stg[q].z),
+                  __float_as_uint(stg[q].w));
+      }
+    }
+  };
+  auto build_guarded = [&](int s, int64_t t) {
+    const int64_t n_lo = n_lo_of(t);
+    const unsigned char* base = base_of(s, t);
+    for (int c = lane; c < NC; c += 64) {
+      unsigned w4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t n0 = n_lo + 8 * c + 2 * e;
+        const unsigned lo = (n0 >= 0 && n0 < p.n) ? *reinterpret_cast<const unsigned short*>(base + 2 * (8 * c + 2 * e)) : 0x8080u;
+        const unsigned hi = (n0 + 1 >= 0 && n0 + 1 < p.n) ? *reinterpret_cast<const unsigned short*>(base + 2 * (8 * c + 2 * e + 1)) : 0x8080u;
+        w4[e] = lo | (hi << 16);
+      }
+      put_chunk(c, w4[0], w4[1], w4[2], w4[3]);
+    }
+  };
+
+  int s = (int)(b0 / p.tps);
+  int64_t t = b0 - (int64_t)s * p.tps;
+  const bool warm = t > 0;
+  if (warm) --t;
+  const int64_t U = (b1 - b0) + (warm ? 1 : 0);
+  if (interior(t)) {
+    load_image(s, t);
+    store_image();
+  } else {
+    build_guarded(s, t);
+  }
+  int s_nx = s;
+  int64_t t_nx = t + 1;
+  if (t_nx == p.tps) { t_nx = 0; ++s_nx; }
+  float carry = 0.f;
+  int wsum = 0;
+  const double zscale = (double)p.qscale * 128.0;    // real-domain zi -> the integer sum's scale
+
+  for (int64_t u = 0; u < U; ++u) {
+    const bool more = u + 1 < U;
+    const bool staged = more && interior(t_nx);
+    if (staged) load_image(s_nx, t_nx);
+    lds_order();
+    i4v acc[2][3];
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg) acc[ch][dg] = i4v{0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      i4v bf[2];
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) bf[ch] = *reinterpret_cast<const i4v*>(&img[ch][160 * pl + 64 * ks + 16 * gl]);
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int dg = 0; dg < 3; ++dg)
+          acc[ch][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch], acc[ch][dg], 0, 0, 0);
+    }
+    const int64_t mo = (int64_t)TO * t + 16 * pl + 4 * gl;     // first output of this lane
+    float phi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float yi = fmaf((float)acc[0][2][i], 65536.f, (float)acc[0][1][i] * 256.f) + (float)acc[0][0][i];
+      float yq = fmaf((float)acc[1][2][i], 65536.f, (float)acc[1][1][i] * 256.f) + (float)acc[1][0][i];
+      if (t == 0 && p.zi_i != nullptr && D * (mo + i) < T - 1) {   // lfilter zi (model/fmMonoBlock.py:86-91)
+        yi += (float)(p.zi_i[(int64_t)s * p.zi_stride + D * (mo + i)] * zscale);
+        yq += (float)(p.zi_q[(int64_t)s * p.zi_stride + D * (mo + i)] * zscale);
+      }
+      phi[i] = fast_atan2f(yq, yi);      // atan2 is scale-free: the 2^-S / 128 is never applied
+    }
+    const int src = gl > 0 ? lane - 16 : (pl > 0 ? lane + 47 : 63);
+    const float left = __uint_as_float(bperm(src, __float_as_uint(phi[3])));
+    float prev = (lane == 0) ? carry : left;
+    const bool keep = !(warm && u == 0);
+    float d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t m = mo + i;
+      int wk = 0;
+      if (m == 0) {
+        const double ps = p.prev_phase ? p.prev_phase[s] : 0.0;
+        d[i] = (float)unwrap_step_f64_m((double)phi[i] - ps, &wk);
+      } else {
+        float dd = phi[i] - prev;
+        if (dd > kPiF) { dd -= k2PiF; wk = -1; }
+        else if (dd < -kPiF) { dd += k2PiF; wk = 1; }
+        d[i] = dd;
+      }
+      if (keep && m < p.M) wsum += wk;
+      prev = phi[i];
+    }
+    carry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(phi[3]), 63));
+    if (keep) {
+      float* out = p.demod + (int64_t)s * p.out_stride + mo;
+      if (p.vec_out && mo + 4 <= p.M) {
+        *reinterpret_cast<f4v*>(out) = f4v{d[0], d[1], d[2], d[3]};
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (mo + i < p.M) out[i] = d[i];
+      }
+      if (p.last_phi != nullptr) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (mo + i == p.M - 1) p.last_phi[s] = phi[i];
+      }
+    }
+    // the stream's wrap count leaves with its last tile of this run
+    if (keep && (!more || s_nx != s) && p.wraps != nullptr) {
+      const int w = wave_sum_i(wsum);
+      if (lane == 0 && w != 0) atomicAdd(p.wraps + s, w);
+      wsum = 0;
+    }
+    if (more) {
+      lds_order();
+      if (staged) store_image();
+      else build_guarded(s_nx, t_nx);
+      s = s_nx;
+      t = t_nx;
+      t_nx = t + 1;
+      s_nx = s;
+      if (t_nx == p.tps) { t_nx = 0; ++s_nx; }
+    }
+  }
+}
+
+template <int T>
+hipError_t launch_demod_mfma_t(const FeLaunch& a, hipStream_t st) {
+  float hmax = 0.f;
+  for (int k = 0; k < T; ++k) hmax = std::max(hmax, std::fabs(a.taps->h[k]));
+  if (!(hmax > 0.f) || !std::isfinite(hmax)) return hipErrorInvalidValue;
+  const int S = tap_scale_exp(hmax);
+  MfmaDemod p{};
+  p.iq = static_cast<const unsigned char*>(a.iq);
+  p.n = a.n;
+  p.stride = a.nstreams > 1 ? a.stride : 0;
+  p.M = (a.n + D - 1) / D;
+  p.tps = (p.M + TO - 1) / TO;
+  p.total = p.tps * a.nstreams;
+  if (p.total > 0x7fffffff) return hipErrorInvalidValue;
+  p.taps = a.taps_dev;
+  p.qscale = std::ldexp(1.0f, S);
+  p.zi_i = a.zi_i;
+  p.zi_q = a.zi_q;
+  p.zi_stride = a.zi_stride;
+  p.prev_phase = a.prev_phase;
+  p.demod = a.demod;
+  p.out_stride = a.out_stride;
+  p.last_phi = a.last_phi;
+  p.wraps = a.wraps;
+  p.vec_out = ((a.out_stride % 4) == 0 && ((uintptr_t)a.demod % 16) == 0) ? 1 : 0;
+  static int slots = 0;
+  if (slots == 0) {
+    int dev = 0, per = 0, cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_demod_kernel<T>, 64, 0) != hipSuccess || per <= 0) per = 1;
+    slots = cus * std::min(per, 12);
+  }
+  // the resident waves share the tiles in runs of >= 2 (a run's warm-up tile is at most a third of
+  // its work; at span sizes, 1/60)
+  const int64_t run = std::max<int64_t>(2, (p.total + slots - 1) / slots);
+  const int64_t grid = std::max<int64_t>(1, (p.total + run - 1) / run);
+  hipLaunchKernelGGL(fe_mfma_demod_kernel<T>, dim3((unsigned)grid), dim3(64), 0, st, p);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+// u8 RF front end (FIR + decimate + demod, carried state) on the matrix cores: 101 or 151
+// taps at decim 10, u8 IQ with 16-B aligned stream bases, no history prefix and no
+// decimated I/Q outputs; otherwise hipErrorInvalidValue (the caller runs fe_slot_kernel).
+hipError_t sdr_launch_fe_mfma(const FeLaunch& a, hipStream_t st) {
+  if (!a.u8 || a.D != D || a.hist != 0 || a.i_ds || a.q_ds || a.demod == nullptr) return hipErrorInvalidValue;
+  if (((uintptr_t)a.iq & 15) != 0 || (a.nstreams > 1 && (a.stride % 8) != 0)) return hipErrorInvalidValue;
+  if (a.n <= 0 || a.nstreams <= 0) return hipSuccess;
+  if (a.T == 101) return launch_demod_mfma_t<101>(a, st);
+  if (a.T == 151) return launch_demod_mfma_t<151>(a, st);
+  return hipErrorInvalidValue;
+}
 
 // Fused u8 FE + mono on the matrix cores.  Supported: 101 RF taps at decim 10, 151 audio
 // taps at decim 5, u8 IQ with 16-B aligned stream bases; otherwise hipErrorInvalidValue
@@ -315,8 +601,7 @@ hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps, int TA
   float hmax = 0.f;
   for (int k = 0; k < T; ++k) hmax = std::max(hmax, std::fabs(a.taps->h[k]));
   if (!(hmax > 0.f) || !std::isfinite(hmax)) return hipErrorInvalidValue;
-  // |h_q| <= 2^22: the top digit stays within [-65, 65]
-  const int S = 22 - (int)std::ceil(std::log2((double)hmax));
+  const int S = tap_scale_exp(hmax);
   MfmaFe p{};
   p.iq = static_cast<const unsigned char*>(a.iq);
   p.n = a.n;

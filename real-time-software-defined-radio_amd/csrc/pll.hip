@@ -1224,7 +1224,6 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
     __syncthreads();
     const double anp = sA[0][tid + 1], ani = sA[1][tid + 1];
     const double a0p = sA[0][0], a0i = sA[1][0];
-    const double* ph = (j == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
     // C_j = E_j - A_{j+1} less its turns (this block's outgoing step)
     const double cd = ep - anp;
     const double dn = rint(cd * kInv2Pi);

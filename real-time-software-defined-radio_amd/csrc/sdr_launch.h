@@ -32,6 +32,9 @@ hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int
                               int64_t audio_stride, hipStream_t st);
 // u8 FE + mono with the RF FIR on the int8 matrix cores (fe_mfma.hip); hipErrorInvalidValue
 // when the configuration is not the one it covers
+// u8 FE (FIR + decimate + demod with carried state) on the int8 matrix cores (fe_mfma.hip):
+// 101 / 151 taps; hipErrorInvalidValue when the configuration is not one it covers
+hipError_t sdr_launch_fe_mfma(const FeLaunch& a, hipStream_t st);
 hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
                                    int64_t audio_stride, hipStream_t st);
 hipError_t sdr_launch_iq_zf(const void* iq, int u8, int64_t n, int64_t stride, int nstreams,
