@@ -220,15 +220,17 @@ def cpu_threads():
     return env if env > 0 else cpu_cores()[0]
 
 
-def copy_bandwidth(lib, handle, nbytes: int = 2 << 30, reps: int = 10):
-    """the achieved fraction beside a measured copy kernel on the same box --
-    libsdr's 16-B-per-lane streaming copy (sdr_copy_bandwidth), best of `reps`, GB/s counting
-    read + write.  (torch's own copy kernel cannot be used here: torch bundles its own HIP
-    runtime, which does not initialise in a process that already runs libsdr's.)"""
+def copy_bandwidth(lib, handle, nbytes: int = 2 << 30, reps: int = 10, read_only: bool = False):
+    """the achieved fraction beside a measured stream kernel on the same box --
+    libsdr's 16-B-per-lane nontemporal copy (sdr_copy_bandwidth, GB/s counting read + write) or
+    read-only stream (sdr_read_bandwidth), best of `reps`.  (torch's own copy kernel cannot be
+    used here: torch bundles its own HIP runtime, which does not initialise in a process that
+    already runs libsdr's.)"""
     g = ctypes.c_double()
-    rc = lib.sdr_copy_bandwidth(handle, nbytes, reps, ctypes.byref(g))
+    fn = lib.sdr_read_bandwidth if read_only else lib.sdr_copy_bandwidth
+    rc = fn(handle, nbytes, reps, ctypes.byref(g))
     if rc != 0:
-        print(f"bench: copy bandwidth not measured: {lib.sdr_last_error().decode()}", file=sys.stderr)
+        print(f"bench: stream bandwidth not measured: {lib.sdr_last_error().decode()}", file=sys.stderr)
         return None
     return round(g.value, 1)
 
@@ -415,9 +417,15 @@ def main():
             "settle": {"untimed_steps": settle_steps, "min_ms": args.settle_ms},
         }
     if rank == 0:
+        # the measured ceilings beside the kernel: a copy (read + write) and a read-only stream
+        # (the FE reads 8 B per complex sample and writes 0.04 B); frac_of_copy is against the
+        # higher of the two
         cbw = copy_bandwidth(lib, h)
+        rbw = copy_bandwidth(lib, h, read_only=True)
+        ceil = max([v for v in (cbw, rbw) if v] or [0.0])
         result["roofline"]["copy_kernel_gbs"] = cbw
-        result["roofline"]["frac_of_copy"] = round(achieved / cbw, 4) if cbw else None
+        result["roofline"]["read_stream_gbs"] = rbw
+        result["roofline"]["frac_of_copy"] = round(achieved / ceil, 4) if ceil else None
     if ws == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, rf_b, au_b)
     elif rank == 0:

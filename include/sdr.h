@@ -78,6 +78,10 @@ int sdr_event_destroy(void* ev);
  * a 16-B-per-lane streaming copy of `bytes` on the context stream, best of `reps` after two
  * warm-ups; *gbs counts read + write.  Synchronous; allocates 2 x bytes for the call. */
 int sdr_copy_bandwidth(sdr_ctx* ctx, int64_t bytes, int reps, double* gbs);
+/* The read-only stream: `bytes` read once (16 B per lane, nontemporal, 8 loads in flight per
+ * lane), best of `reps` after two warm-ups, GB/s.  The ceiling for kernels that read their
+ * input once and write little (the front ends). */
+int sdr_read_bandwidth(sdr_ctx* ctx, int64_t bytes, int reps, double* gbs);
 
 /* ================================================================================
  * Host-buffer drop-in entry points (synchronous)

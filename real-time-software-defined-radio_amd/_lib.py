@@ -61,6 +61,7 @@ SIGNATURES = {
     "sdr_memset": (_i32, [_vp, _vp, _i32, _i64]),
     "sdr_event_create": (_i32, [_vp, _c.POINTER(_vp)]),
     "sdr_copy_bandwidth": (_i32, [_vp, _i64, _i32, _c.POINTER(_c.c_double)]),
+    "sdr_read_bandwidth": (_i32, [_vp, _i64, _i32, _c.POINTER(_c.c_double)]),
     "sdr_event_record": (_i32, [_vp, _vp]),
     "sdr_event_elapsed_ms": (_i32, [_vp, _vp, _c.POINTER(_f32)]),
     "sdr_event_destroy": (_i32, [_vp]),

@@ -107,12 +107,38 @@ int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T) 
 }  // namespace sdrint
 
 namespace {
-// streaming copy (16 B per lane, grid-stride): the box's copy-kernel bandwidth, measured beside
-// the path's kernels
+// streaming copy (16 B per lane, nontemporal, 4 loads in flight per lane before their
+// stores, grid-stride): the box's copy-kernel bandwidth, measured beside the path's kernels
+// 
 typedef float cp4 __attribute__((ext_vector_type(4)));
+constexpr int CP_U = 4, RD_U = 8;
 __global__ __launch_bounds__(256) void copy_probe_kernel(const cp4* __restrict__ a, cp4* __restrict__ b, int64_t n4) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
-    __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i);
+  const int64_t step = (int64_t)gridDim.x * 256 * CP_U;
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 * CP_U + threadIdx.x; i0 < n4; i0 += step) {
+    cp4 v[CP_U];
+#pragma unroll
+    for (int u = 0; u < CP_U; ++u)
+      if (i0 + 256 * u < n4) v[u] = __builtin_nontemporal_load(a + i0 + 256 * u);
+#pragma unroll
+    for (int u = 0; u < CP_U; ++u)
+      if (i0 + 256 * u < n4) __builtin_nontemporal_store(v[u], b + i0 + 256 * u);
+  }
+}
+// read-only stream (16 B per lane, nontemporal, 8 loads in flight per lane): the ceiling of a
+// kernel that reads its input once and writes little (the FE: 2 or 8 B in per complex sample,
+// 0.4 B out); the loads feed a sum that is stored only if it is NaN (never, on the zeroed buffer)
+__global__ __launch_bounds__(256) void read_probe_kernel(const cp4* __restrict__ a, int64_t n4, cp4* sink) {
+  const int64_t step = (int64_t)gridDim.x * 256 * RD_U;
+  cp4 acc = cp4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 * RD_U + threadIdx.x; i0 < n4; i0 += step) {
+    cp4 v[RD_U];
+#pragma unroll
+    for (int u = 0; u < RD_U; ++u)
+      v[u] = i0 + 256 * u < n4 ? __builtin_nontemporal_load(a + i0 + 256 * u) : cp4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < RD_U; ++u) acc += v[u];
+  }
+  if (acc.x != acc.x) sink[threadIdx.x] = acc;
 }
 }  // namespace
 
@@ -253,45 +279,61 @@ int sdr_event_destroy(void* ev) {
   return SDR_OK;
 }
 
-int sdr_copy_bandwidth(sdr_ctx* c, int64_t bytes, int reps, double* gbs) {
+namespace {
+// best of `reps` (after two warm-ups) of the copy (read_only = 0: GB/s counting read + write)
+// or read-only probe over `bytes`
+int stream_probe(sdr_ctx* c, int64_t bytes, int reps, double* gbs, bool read_only, const char* name) {
   CHECK_CTX(c);
-  if (gbs == nullptr || bytes < 16 || reps < 1) return fail(SDR_EINVAL, "sdr_copy_bandwidth: bytes %lld, reps %d",
+  if (gbs == nullptr || bytes < 16 || reps < 1) return fail(SDR_EINVAL, "%s: bytes %lld, reps %d", name,
                                                             (long long)bytes, reps);
   TRY(set_dev(c));
   const int64_t n4 = bytes / 16;
   void *a = nullptr, *b = nullptr;
   hipError_t e = hipMalloc(&a, (size_t)n4 * 16);
-  if (e == hipSuccess) e = hipMalloc(&b, (size_t)n4 * 16);
+  if (e == hipSuccess) e = hipMalloc(&b, read_only ? 256 * 16 : (size_t)n4 * 16);
   if (e != hipSuccess) {
     if (a) (void)hipFree(a);
-    return fail(SDR_ENOMEM, "sdr_copy_bandwidth: hipMalloc: %s", hipGetErrorString(e));
+    return fail(SDR_ENOMEM, "%s: hipMalloc: %s", name, hipGetErrorString(e));
   }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) cus = prop.multiProcessorCount;
-  const unsigned grid = (unsigned)std::min<int64_t>((int64_t)cus * 8, (n4 + 255) / 256);
+  const int U = read_only ? RD_U : CP_U;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * 8, (n4 + 256 * U - 1) / (256 * U)));
   float best = 0.f;
   e = hipMemsetAsync(a, 0, (size_t)n4 * 16, c->stream);
   if (e == hipSuccess) e = hipEventCreate(&e0);
   if (e == hipSuccess) e = hipEventCreate(&e1);
   for (int r = 0; r < reps + 2 && e == hipSuccess; ++r) {
     e = hipEventRecord(e0, c->stream);
-    hipLaunchKernelGGL(copy_probe_kernel, dim3(grid), dim3(256), 0, c->stream, (const cp4*)a, (cp4*)b, n4);
+    if (read_only)
+      hipLaunchKernelGGL(read_probe_kernel, dim3(grid), dim3(256), 0, c->stream, (const cp4*)a, n4, (cp4*)b);
+    else
+      hipLaunchKernelGGL(copy_probe_kernel, dim3(grid), dim3(256), 0, c->stream, (const cp4*)a, (cp4*)b, n4);
     if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
     if (e == hipSuccess) e = hipEventSynchronize(e1);
     float ms = 0.f;
     if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-    if (r >= 2 && (best == 0.f || ms < best)) best = ms;    // two warm-up copies
+    if (r >= 2 && (best == 0.f || ms < best)) best = ms;    // two warm-ups
   }
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
   (void)hipFree(a);
   (void)hipFree(b);
-  if (e != hipSuccess) return fail(SDR_EHIP, "sdr_copy_bandwidth: %s", hipGetErrorString(e));
-  *gbs = 2.0 * (double)(n4 * 16) / ((double)best * 1e-3) / 1e9;
+  if (e != hipSuccess) return fail(SDR_EHIP, "%s: %s", name, hipGetErrorString(e));
+  *gbs = (read_only ? 1.0 : 2.0) * (double)(n4 * 16) / ((double)best * 1e-3) / 1e9;
   return SDR_OK;
+}
+}  // namespace
+
+int sdr_copy_bandwidth(sdr_ctx* c, int64_t bytes, int reps, double* gbs) {
+  return stream_probe(c, bytes, reps, gbs, false, "sdr_copy_bandwidth");
+}
+
+int sdr_read_bandwidth(sdr_ctx* c, int64_t bytes, int reps, double* gbs) {
+  return stream_probe(c, bytes, reps, gbs, true, "sdr_read_bandwidth");
 }
 
 // ================================================================================
