@@ -86,10 +86,34 @@ __device__ __forceinline__ int digit(int q, int k) {
   return d;
 }
 
+// y = 65536 acc2 + (256 acc1 + acc0), the last two digits combined in int32 (|256 acc1 + acc0|
+// <= 256 * 127 * 128 * 320 + ... < 2^31) before the one conversion: two roundings, as before
+__device__ __forceinline__ void combine_digits(const i4v (&acc)[2][3], float (&yi)[4], float (&yq)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    yi[i] = fmaf((float)acc[0][2][i], 65536.f, (float)(acc[0][1][i] * 256 + acc[0][0][i]));
+    yq[i] = fmaf((float)acc[1][2][i], 65536.f, (float)(acc[1][1][i] * 256 + acc[1][0][i]));
+  }
+}
+__device__ __forceinline__ void atan2_4(const float (&y)[4], const float (&x)[4], float (&phi)[4]) {
+  const f2v p01 = fast_atan2f_x2(f2v{y[0], y[1]}, f2v{x[0], x[1]});
+  const f2v p23 = fast_atan2f_x2(f2v{y[2], y[3]}, f2v{x[2], x[3]});
+  phi[0] = p01.x; phi[1] = p01.y; phi[2] = p23.x; phi[3] = p23.y;
+}
+// acc += tap2 * {x, x}, the tap pair in SGPRs (scalar loads of the audio taps), x = the low
+// (HI = false) or high half of x2
+template <bool HI>
+__device__ __forceinline__ void pk_fma_sx(f2v& acc, f2v tap2, const f2v& x2) {
+  if (HI)
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(tap2), "v"(x2));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[1,0,1]" : "+v"(acc) : "s"(tap2), "v"(x2));
+}
+typedef const __attribute__((address_space(4))) float* cfp4;   // uniform, read-only: scalar loads
+
 __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
   __shared__ __attribute__((aligned(16))) signed char img[2][IMG + 16];   // I, Q planes
   __shared__ __attribute__((aligned(16))) float dh[HA + AB + 8];
-  __shared__ __attribute__((aligned(16))) f4v ptab[NW + 2];
 
   const int lane = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * p.total / gridDim.x;
@@ -113,16 +137,7 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
 #pragma unroll
     for (int dg = 0; dg < 3; ++dg) afr[ks][dg] = i4v{w[dg][0], w[dg][1], w[dg][2], w[dg][3]};
   }
-  // audio tap quads: ptab[w] = {g[150-w], g[155-w], g[160-w], g[165-w]}
-  for (int w = lane; w < NW + 2; w += 64) {
-    float t4[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = TA - 1 + DA * r - w;
-      t4[r] = (w < NW && k >= 0 && k < TA) ? p.ataps[k] : 0.f;
-    }
-    ptab[w] = f4v{t4[0], t4[1], t4[2], t4[3]};
-  }
+  const cfp4 ga = (cfp4)p.ataps;   // audio taps: SGPR operands (scalar loads, compile-time offsets)
 
   // ---- tile images: chunk c = lane + 64 q (16 raw bytes = 8 complex u8 samples) ----
   // Interior images: hand-issued 16-B loads into stg, waited for (one s_waitcnt) when the
@@ -228,13 +243,10 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
         for (int dg = 0; dg < 3; ++dg)
           acc[ch][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch][ks], acc[ch][dg], 0, 0, 0);
     // combine the digits, phases, predecessor, wrap
+    float yi[4], yq[4];
+    combine_digits(acc, yi, yq);
     float phi[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float yi = fmaf((float)acc[0][2][i], 65536.f, (float)acc[0][1][i] * 256.f) + (float)acc[0][0][i];
-      const float yq = fmaf((float)acc[1][2][i], 65536.f, (float)acc[1][1][i] * 256.f) + (float)acc[1][0][i];
-      phi[i] = fast_atan2f(yq, yi);      // atan2 is scale-free: the 2^-S / 128 is never applied
-    }
+    atan2_4(yq, yi, phi);                // atan2 is scale-free: the 2^-S / 128 is never applied
     const int src = gl > 0 ? lane - 16 : (pl > 0 ? lane + 47 : 63);
     const float left = __uint_as_float(bperm(src, __float_as_uint(phi[3])));
     float prev = (lane == 0) ? carry : left;
@@ -261,17 +273,18 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
     if (!(warm && u == 0) && tb == DA - 1) {
       // audio block jb: a[j] = sum_k g[k] d[5j - k], lane -> j = 256 jb + 4 l + r
       lds_order();
+      // window sample w, outputs r = 0..3: tap g[150 + 5 r - w] (0 outside [0, 151))
       const float* aw = dh + (HA - (TA - 1)) + DA * 4 * lane;
       f2v a01 = f2v{0.f, 0.f}, a23 = f2v{0.f, 0.f}, b01 = f2v{0.f, 0.f}, b23 = f2v{0.f, 0.f};
-#pragma unroll 4
-      for (int w = 0; w < NW; w += 2) {
+      auto tap = [&](int k) { return (k >= 0 && k < TA) ? ga[k] : 0.f; };
+      static_for<0, NW / 2>([&](auto W2) {
+        constexpr int w = 2 * W2;
         const f2v x2 = *reinterpret_cast<const f2v*>(aw + w);
-        const f4v t0 = ptab[w], t1 = ptab[w + 1];
-        pk_fma_bcast_x<false>(a01, f2v{t0.x, t0.y}, x2);
-        pk_fma_bcast_x<false>(a23, f2v{t0.z, t0.w}, x2);
-        pk_fma_bcast_x<true>(b01, f2v{t1.x, t1.y}, x2);
-        pk_fma_bcast_x<true>(b23, f2v{t1.z, t1.w}, x2);
-      }
+        pk_fma_sx<false>(a01, f2v{tap(TA - 1 - w), tap(TA - 1 + DA - w)}, x2);
+        pk_fma_sx<false>(a23, f2v{tap(TA - 1 + 2 * DA - w), tap(TA - 1 + 3 * DA - w)}, x2);
+        pk_fma_sx<true>(b01, f2v{tap(TA - 2 - w), tap(TA - 2 + DA - w)}, x2);
+        pk_fma_sx<true>(b23, f2v{tap(TA - 2 + 2 * DA - w), tap(TA - 2 + 3 * DA - w)}, x2);
+      });
       const f2v r01 = a01 + b01, r23 = a23 + b23;
       const int64_t jb = t / DA;
       const int64_t j = TO * jb + 4 * lane;
@@ -466,17 +479,18 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
           acc[ch][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch], acc[ch][dg], 0, 0, 0);
     }
     const int64_t mo = (int64_t)TO * t + 16 * pl + 4 * gl;     // first output of this lane
-    float phi[4];
+    float yi[4], yq[4];
+    combine_digits(acc, yi, yq);
+    if (t == 0 && p.zi_i != nullptr) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float yi = fmaf((float)acc[0][2][i], 65536.f, (float)acc[0][1][i] * 256.f) + (float)acc[0][0][i];
-      float yq = fmaf((float)acc[1][2][i], 65536.f, (float)acc[1][1][i] * 256.f) + (float)acc[1][0][i];
-      if (t == 0 && p.zi_i != nullptr && D * (mo + i) < T - 1) {   // lfilter zi (model/fmMonoBlock.py:86-91)
-        yi += (float)(p.zi_i[(int64_t)s * p.zi_stride + D * (mo + i)] * zscale);
-        yq += (float)(p.zi_q[(int64_t)s * p.zi_stride + D * (mo + i)] * zscale);
-      }
-      phi[i] = fast_atan2f(yq, yi);      // atan2 is scale-free: the 2^-S / 128 is never applied
+      for (int i = 0; i < 4; ++i)
+        if (D * (mo + i) < T - 1) {      // lfilter zi (model/fmMonoBlock.py:86-91)
+          yi[i] += (float)(p.zi_i[(int64_t)s * p.zi_stride + D * (mo + i)] * zscale);
+          yq[i] += (float)(p.zi_q[(int64_t)s * p.zi_stride + D * (mo + i)] * zscale);
+        }
     }
+    float phi[4];
+    atan2_4(yq, yi, phi);                // atan2 is scale-free: the 2^-S / 128 is never applied
     const int src = gl > 0 ? lane - 16 : (pl > 0 ? lane + 47 : 63);
     const float left = __uint_as_float(bperm(src, __float_as_uint(phi[3])));
     float prev = (lane == 0) ? carry : left;

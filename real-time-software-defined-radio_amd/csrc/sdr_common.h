@@ -240,6 +240,46 @@ __device__ __forceinline__ float fast_atan2f(float y, float x) {
   return (x != x || y != y) ? __builtin_nanf("") : r;
 }
 
+// fast_atan2f on two (y, x) pairs at once: the quotient's Newton step and the polynomial as
+// packed FMAs (v_pk_fma_f32 / v_pk_mul_f32), the octant reduction and the IEEE selects per
+// element -- the same arithmetic per element (every packed op rounds as its scalar twin)
+__device__ __forceinline__ f2v fast_atan2f_x2(f2v y, f2v x) {
+  const float ax0 = fabsf(x.x), ay0 = fabsf(y.x), ax1 = fabsf(x.y), ay1 = fabsf(y.y);
+  const float mn0 = fminf(ax0, ay0), mx0 = fmaxf(ax0, ay0), mn1 = fminf(ax1, ay1), mx1 = fmaxf(ax1, ay1);
+  const f2v mn = f2v{mn0, mn1};
+  const f2v mxs = f2v{fmaxf(mx0, 1e-30f), fmaxf(mx1, 1e-30f)};
+  const f2v rc = f2v{__builtin_amdgcn_rcpf(mxs.x), __builtin_amdgcn_rcpf(mxs.y)};
+  f2v a = mn * rc;
+  a = __builtin_elementwise_fma(__builtin_elementwise_fma(-mxs, a, mn), rc, a);
+  a.x = (mx0 == INFINITY) ? ((mn0 == INFINITY) ? 1.f : 0.f) : a.x;
+  a.y = (mx1 == INFINITY) ? ((mn1 == INFINITY) ? 1.f : 0.f) : a.y;
+  const f2v s = a * a;
+  auto c = [](float v) { return f2v{v, v}; };
+  f2v r = c(0.002849547192454338f);
+  r = __builtin_elementwise_fma(r, s, c(-0.01606736145913601f));
+  r = __builtin_elementwise_fma(r, s, c(0.04268963634967804f));
+  r = __builtin_elementwise_fma(r, s, c(-0.0750415101647377f));
+  r = __builtin_elementwise_fma(r, s, c(0.1064087525010109f));
+  r = __builtin_elementwise_fma(r, s, c(-0.1420363187789917f));
+  r = __builtin_elementwise_fma(r, s, c(0.19992618262767792f));
+  r = __builtin_elementwise_fma(r, s, c(-0.3333307206630707f));
+  r = __builtin_elementwise_fma(r, s, c(1.0f));
+  r = r * a;
+  float r0 = r.x, r1 = r.y;
+  r0 = (ay0 > ax0) ? 1.57079632679489662f - r0 : r0;
+  r1 = (ay1 > ax1) ? 1.57079632679489662f - r1 : r1;
+  r0 = (x.x < 0.f) ? 3.14159265358979324f - r0 : r0;
+  r1 = (x.y < 0.f) ? 3.14159265358979324f - r1 : r1;
+  asm volatile("" : "+v"(r0), "+v"(r1));
+  r0 = (mx0 == 0.f) ? (__builtin_signbitf(x.x) ? 3.14159265358979324f : 0.f) : r0;
+  r1 = (mx1 == 0.f) ? (__builtin_signbitf(x.y) ? 3.14159265358979324f : 0.f) : r1;
+  r0 = copysignf(r0, y.x);
+  r1 = copysignf(r1, y.y);
+  r0 = (x.x != x.x || y.x != y.x) ? __builtin_nanf("") : r0;
+  r1 = (x.y != x.y || y.y != y.y) ? __builtin_nanf("") : r1;
+  return f2v{r0, r1};
+}
+
 // Deferred per-lane output queue: Q entries of 3 floats held in registers, written to HBM
 // in one burst at the end of a wave's run.  Output stores interleaved with a streaming
 // read lower the read rate far more than their bytes (tools/pipe_probe.hip, r02: one 768-B
