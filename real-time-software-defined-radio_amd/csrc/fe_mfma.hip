@@ -223,25 +223,23 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
     const bool staged = more && interior(t_nx);
     if (staged) load_image(s_nx, t_nx);
     lds_order();                                              // image of tile t written
-    // B fragments of both channels, all four K-steps
-    i4v bf[2][4];
-#pragma unroll
-    for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-        bf[ch][ks] = *reinterpret_cast<const i4v*>(&img[ch][160 * pl + 64 * ks + 16 * gl]);
+    // B fragments of both channels, one K-step at a time (registers: occupancy)
     i4v acc[2][3];
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
       for (int dg = 0; dg < 3; ++dg) acc[ch][dg] = i4v{0, 0, 0, 0};
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+    for (int ks = 0; ks < 4; ++ks) {
+      i4v bf[2];
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) bf[ch] = *reinterpret_cast<const i4v*>(&img[ch][160 * pl + 64 * ks + 16 * gl]);
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
         for (int dg = 0; dg < 3; ++dg)
-          acc[ch][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch][ks], acc[ch][dg], 0, 0, 0);
+          acc[ch][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch], acc[ch][dg], 0, 0, 0);
+    }
     // combine the digits, phases, predecessor, wrap
     float yi[4], yq[4];
     combine_digits(acc, yi, yq);
