@@ -63,6 +63,7 @@ struct StageJob {
   int64_t b0;            // first workgroup of this job's tiles
   float gain;
   int pre, D, U, kind, T, tiles;
+  int small;             // D = 1 FIR: 4 outputs per lane (a launch with few tiles: more workgroups)
 };
 
 // The front end's carried state, finished by the first stage launch after the FE kernel:
@@ -118,9 +119,9 @@ __device__ __forceinline__ void pk_fma_s(f2& acc, f2 h, f2 x) {
 // floats after every lane's D*R samples (even lane stride SR = 2 mod 4 dwords: 8-B aligned,
 // conflict-free ds_read_b64), and starts DELTA samples early so that its global loads are
 // 16-B aligned.
-template <int T, int D>
+template <int T, int D, int R_ = (D == 1 ? 16 : 4)>
 struct FirShape {
-  static constexpr int G = 4, NT = RX_NT, R = D == 1 ? 16 : 4, TO = NT * R, DR = D * R;
+  static constexpr int G = 4, NT = RX_NT, R = R_, TO = NT * R, DR = D * R;
   static constexpr int SR = DR + 2;                          // lane stride in LDS (floats)
   static constexpr int DELTA = (G - ((T - 1) % G)) % G;
   static constexpr int L = D * (TO - 1) + T + DELTA;         // image samples
@@ -133,9 +134,9 @@ struct FirShape {
   __device__ static constexpr int slot(int u) { return u < DELTA ? u : u + 2 * ((u - DELTA) / DR); }
 };
 
-template <int T, int D>
+template <int T, int D, int R_ = (D == 1 ? 16 : 4)>
 __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile, float* lds) {
-  using S = FirShape<T, D>;
+  using S = FirShape<T, D, R_>;
   constexpr int R = S::R, DR = S::DR, DELTA = S::DELTA;
   const int t = threadIdx.x;
   const int64_t m0 = tile * S::TO;
@@ -449,7 +450,11 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
     return;
   }
   if constexpr (T > 0) {
-    if (J.D == 1) { fir_tile<T, 1>(J, s, tile, lds); return; }
+    if (J.D == 1) {
+      if (J.small) fir_tile<T, 1, 4>(J, s, tile, lds);
+      else fir_tile<T, 1>(J, s, tile, lds);
+      return;
+    }
     if (J.D == 5) { fir_tile<T, 5>(J, s, tile, lds); return; }
   }
   fir_tile_any(J, s, tile, lds);
@@ -457,6 +462,8 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
 
 // outputs per tile of a job in a launch of tap class `key` (as rx_stage_kernel<key> picks the tile)
 int64_t tile_outputs(const StageJob& j, int key) {
+  if (j.kind == JK_FIR && key == 151 && j.D == 1 && j.small) return FirShape<151, 1, 4>::TO;
+  if (j.kind == JK_FIR && key == 101 && j.D == 1 && j.small) return FirShape<101, 1, 4>::TO;
   if (j.kind == JK_FIR && key == 151 && j.D == 1) return FirShape<151, 1>::TO;
   if (j.kind == JK_FIR && key == 151 && j.D == 5) return FirShape<151, 5>::TO;
   if (j.kind == JK_FIR && key == 101 && j.D == 1) return FirShape<101, 1>::TO;
@@ -472,11 +479,22 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
     StageJobs P{};
     P.nstreams = S;
     int64_t blocks = 0;
+    // a launch whose tiles would give fewer than ~2.5 workgroups per CU (C5 per-block at 64
+    // streams: RDS x^2 + BPF, mixers + LPFs, RRC; not the 4-filter stage A) runs its D = 1 jobs
+    // in 1 024-output tiles (4 per lane): latency-bound launches get 4x the waves
+    int64_t big = 0;
+    for (const StageJob& j : jobs)
+      if (cls(j) == key) {
+        const int64_t nout = j.kind == JK_RESAMPLE ? (j.n * j.U + j.D - 1) / j.D : (j.n + j.D - 1) / j.D;
+        big += (nout + 1023) / 1024 * S;
+      }
+    const bool small = key > 0 && big < 10 * 256;
     for (const StageJob& j0 : jobs) {
       if (cls(j0) != key) continue;
       if (P.njobs == RX_MAXJ) return hipErrorInvalidValue;
       StageJob j = j0;
       const int64_t nout = j.kind == JK_RESAMPLE ? (j.n * j.U + j.D - 1) / j.D : (j.n + j.D - 1) / j.D;
+      j.small = (small && j.kind == JK_FIR && j.D == 1) ? 1 : 0;
       const int64_t to = tile_outputs(j, key);
       j.tiles = (int)std::max<int64_t>((nout + to - 1) / to, 0);
       j.b0 = blocks;
