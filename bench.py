@@ -382,7 +382,7 @@ def main():
         kernels = {"fe": round(k_avg, 5), "mono": round(stage_ms[1], 5),
                    "mono_gbs": round(mono_bytes / (stage_ms[1] * 1e-3) / 1e9, 1)}
     achieved = k_bytes / (k_avg * 1e-3) / 1e9
-    traffic = load_traffic(args.traffic, args.taps, args.blocks, args.path) if args.iq == "f32" else None
+    traffic = load_traffic(args.traffic, args.taps, args.blocks, args.path if args.iq == "f32" else "u8_mfma")
 
     result = None
     if rank == 0:
@@ -439,8 +439,11 @@ def main():
             "c5": c5_measure(ctx, 8, 256, 5, 2, rank, ws, cpu=(ws == 1 and not args.no_cpu and rank == 0),
                              args=args),
             "c5_1stream": c5_measure(ctx, 1, 256, 10, 2, rank, ws),
-            "u8": u8_measure(ctx, 64, 50, 10, rank),
+            "u8": u8_measure(ctx, 128, 50, 10, rank),
         }
+        cb = extras["c5"].get("cpu_baseline")
+        if cb is not None:                       # the CPU leg runs one stream per host thread either way
+            extras["c5_1stream"]["cpu_baseline"] = dict(cb, note="the c5 leg (one stream per host thread)")
         if rank == 0:
             result.update(extras)
     if rank == 0:
@@ -783,7 +786,9 @@ def u8_measure(ctx, blocks, steps, warmup, rank):
     return {"value": round(n / (k_ms * 1e-3) / 1e6, 1), "unit": "MS/s", "avg_launch_ms": round(k_ms, 5),
             "config": {"blocks": blocks, "block_complex": BLOCK, "iq": "u8", "rf_taps": 101, "audio_taps": 151},
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic(os.path.join(ROOT, "profiles", "fe_pmc_traffic.json"), 101, blocks,
+                                                 "u8_mfma"),
                          "kernel": "fe_mfma_mono_kernel (RF FIR on v_mfma_i32_16x16x64_i8) + audio FIR",
                          "algorithmic_bytes_per_launch": k_bytes}}
 

@@ -30,6 +30,7 @@
 // (151 taps, f32) runs on the VALU at the block's end.  Each wave owns whole audio blocks
 // (a run starting mid-stream first runs the previous tile as a warm-up: history + carry).
 #include <cmath>
+#include <cstdlib>
 
 #include "sdr_launch.h"
 
@@ -111,7 +112,12 @@ __device__ __forceinline__ void pk_fma_sx(f2v& acc, f2v tap2, const f2v& x2) {
 }
 typedef const __attribute__((address_space(4))) float* cfp4;   // uniform, read-only: scalar loads
 
-__global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
+// DEPTH = tiles of image loads in flight per wave (1: the next tile's, issued at the top of a
+// tile and waited for at its end; 2: the next two -- two staging register sets, alternating,
+// so each tile's loads have two tiles' compute to land)
+template <int DEPTH>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe_mfma_mono_kernel(MfmaFe p) {
+  static_assert(DEPTH == 1 || DEPTH == 2, "image loads in flight: one or two tiles");
   __shared__ __attribute__((aligned(16))) signed char img[2][IMG + 16];   // I, Q planes
   __shared__ __attribute__((aligned(16))) float dh[HA + AB + 8];
 
@@ -140,22 +146,35 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
   const cfp4 ga = (cfp4)p.ataps;   // audio taps: SGPR operands (scalar loads, compile-time offsets)
 
   // ---- tile images: chunk c = lane + 64 q (16 raw bytes = 8 complex u8 samples) ----
-  // Interior images: hand-issued 16-B loads into stg, waited for (one s_waitcnt) when the
-  // image is written, at the end of the tile before (compiler-placed waits serialised the
-  // loads one at a time).  Only the asm loads write stg: a second, compiler-visible writer
-  // made the compiler merge the two through register copies taken before the data landed.
-  // Boundary images (stream head / tail: zeros, 0x80, outside [0, n)) are built at write
-  // time from guarded 2-B loads.
-  f4v stg[NLD];
+  // Interior images: hand-issued 16-B loads into a staging set, waited for by a counted
+  // s_waitcnt when the image is written (compiler-placed waits serialised the loads one at a
+  // time).  Only the asm loads write a staging set: a second, compiler-visible writer made the
+  // compiler merge the two through register copies taken before the data landed.  Boundary
+  // images (stream head / tail: zeros, 0x80, outside [0, n)) are built at write time from
+  // guarded 2-B loads.
+  f4v sa[NLD], sb[NLD];
   const unsigned voff = 16u * lane;
   auto n_lo_of = [&](int64_t t) { return (int64_t)TO * D * t - OFF; };
   auto interior = [&](int64_t t) { return n_lo_of(t) >= 0 && n_lo_of(t) + IMG <= p.n; };
   auto base_of = [&](int s, int64_t t) { return p.iq + 2 * ((int64_t)s * p.stride + n_lo_of(t)); };
-  auto load_image = [&](int s, int64_t t) {
-    const unsigned char* base = base_of(s, t);
+  // halo: the tile follows the one in LDS in the same stream -- its first HC chunks are that
+  // image's last HC (moved LDS -> LDS at store time), so only the 320 new chunks (5 per lane)
+  // are read: HBM reads = the stream's bytes, not 2 656 / 2 560 of them
+  constexpr int HC = (IMG - D * TO) / 8;
+  static_assert(D * TO / 8 == 5 * 64, "5 new chunks per lane");
+  // ONE load site per staging register for both cases (the first chunk a uniform offset, the
+  // last load masked by lane count): 5 full loads with the halo, 6 without
+  // (the set is a compile-time index: a runtime reference to it made the compiler shuffle both
+  // sets through copies -- 130 -> 245 VGPRs)
+  using Set0 = std::integral_constant<int, 0>;
+  using Set1 = std::integral_constant<int, 1>;
+  auto load_image = [&](auto SET, int s, int64_t t, bool halo) {
+    f4v (&stg)[NLD] = *(decltype(SET)::value == 0 ? &sa : &sb);
+    const int cf = halo ? HC : 0;
+    const unsigned char* base = base_of(s, t) + 16 * cf;
     static_for<0, NLD>([&](auto Q) {
       constexpr int q = Q;
-      if (q < NLD - 1 || lane < NCH - 64 * (NLD - 1)) gload16_nt_v<0>(stg[q], voff, base + 1024 * q);
+      if (lane < NCH - cf - 64 * q) gload16_nt_v<0>(stg[q], voff, base + 1024 * q);
     });
   };
   // de-interleave (I0 Q0 I1 Q1 ...) into the int8 planes: x - 128 = u8 ^ 0x80
@@ -167,11 +186,23 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
     *reinterpret_cast<uint2*>(&img[0][8 * c]) = make_uint2(i_lo, i_hi);
     *reinterpret_cast<uint2*>(&img[1][8 * c]) = make_uint2(q_lo, q_hi);
   };
-  auto store_image = [&]() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // write the staged image; `younger` = loads issued after this set's (the next set's, all
+  // 16-B loads of one tile; loads return in order, so vmcnt(5) retires this set whatever
+  // stores were issued in between -- a 6th load of the younger set only makes it wait longer)
+  auto store_image = [&](auto SET, bool halo, bool younger) {
+    f4v (&stg)[NLD] = *(decltype(SET)::value == 0 ? &sa : &sb);
+    if (younger) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cf = halo ? HC : 0;
+    if (halo && lane < 2 * HC) {                 // the halo to the front (both planes), before the new chunks
+      const int ch = lane / HC, k = lane - ch * HC;
+      const uint2 v = *reinterpret_cast<const uint2*>(&img[ch][D * TO + 8 * k]);
+      *reinterpret_cast<uint2*>(&img[ch][8 * k]) = v;
+    }
+    lds_order();
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
-      const int c = lane + 64 * q;
+      const int c = cf + lane + 64 * q;
       if (c < NCH) {
         asm volatile("" : "+v"(stg[q]));
         put_chunk(c, __float_as_uint(stg[q].x), __float_as_uint(stg[q].y), __float_as_uint(stg[q].z),
@@ -204,24 +235,20 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
   const int64_t U = (b1 - b0) * DA + (warm ? 1 : 0);
   for (int e = lane; e < HA; e += 64) dh[e] = 0.f;          // zero history at a stream start
   if (interior(t)) {
-    load_image(s, t);
-    store_image();
+    load_image(Set0{}, s, t, false);
+    store_image(Set0{}, false, false);
   } else {
     build_guarded(s, t);
   }
-  int s_nx = s;
-  int64_t t_nx = t + 1;
-  if (t_nx == tps) { t_nx = 0; ++s_nx; }
+  auto next_s = [&](int s_, int64_t t_) { return t_ + 1 == tps ? s_ + 1 : s_; };
+  auto next_t = [&](int64_t t_) { return t_ + 1 == tps ? (int64_t)0 : t_ + 1; };
+  int s1 = next_s(s, t);
+  int64_t t1 = next_t(t);
   float carry = 0.f;
   float d4[4] = {0.f, 0.f, 0.f, 0.f};
 
-  for (int64_t u = 0; u < U; ++u) {
-    // the next tile's loads fly during this tile's MFMAs, epilogue and audio; they are
-    // waited for and written to LDS at the end of the iteration (an in-flight register
-    // never crosses the loop's back edge, where the compiler may copy it)
-    const bool more = u + 1 < U;
-    const bool staged = more && interior(t_nx);
-    if (staged) load_image(s_nx, t_nx);
+  // one tile from the image in LDS: MFMAs, demod, the audio block at its end
+  auto tile = [&](int64_t u) __attribute__((always_inline)) {
     lds_order();                                              // image of tile t written
     // B fragments of both channels, one K-step at a time (registers: occupancy)
     i4v acc[2][3];
@@ -299,20 +326,63 @@ __global__ __launch_bounds__(64) void fe_mfma_mono_kernel(MfmaFe p) {
       // this block's last 150 demod samples become the next block's history
       if (o >= TO - HA) *reinterpret_cast<f4v*>(&dh[HA - TO + o]) = f4v{d4[0], d4[1], d4[2], d4[3]};
     }
-    // advance: the next image replaces this one (its B reads returned long ago)
-    if (more) {
+  };
+  // the next image replaces this one (its B reads returned long ago); new stream: zero history
+  auto advance = [&]() __attribute__((always_inline)) {
+    s = s1;
+    t = t1;
+    if (t == 0) {
       lds_order();
-      if (staged) store_image();
-      else build_guarded(s_nx, t_nx);
-      s = s_nx;
-      t = t_nx;
-      if (t == 0) {                                           // new stream: zero history
+      for (int e = lane; e < HA; e += 64) dh[e] = 0.f;
+    }
+    s1 = next_s(s, t);
+    t1 = next_t(t);
+  };
+
+  if constexpr (DEPTH == 1) {
+    for (int64_t u = 0; u < U; ++u) {
+      // the next tile's loads fly during this tile's MFMAs, epilogue and audio; they are
+      // waited for and written to LDS at the end of the iteration (an in-flight register
+      // never crosses the loop's back edge, where the compiler may copy it)
+      const bool more = u + 1 < U;
+      const bool staged = more && interior(t1);
+      const bool halo = staged && s1 == s && t1 == t + 1 && interior(t);
+      if (staged) load_image(Set1{}, s1, t1, halo);
+      tile(u);
+      if (more) {
         lds_order();
-        for (int e = lane; e < HA; e += 64) dh[e] = 0.f;
+        if (staged) store_image(Set1{}, halo, false);
+        else build_guarded(s1, t1);
+        advance();
       }
-      t_nx = t + 1;
-      s_nx = s;
-      if (t_nx == tps) { t_nx = 0; ++s_nx; }
+    }
+  } else {
+    // tile u+1's loads (set Y) were issued during tile u-1; tile u issues tile u+2's (set X),
+    // computes, then waits for Y only.  Two steps per trip with the sets swapped keep each
+    // set's registers fixed (the set in flight across the back edge is always sb).
+    bool st1 = U > 1 && interior(t1);
+    bool h1 = st1 && s1 == s && t1 == t + 1 && interior(t);
+    if (st1) load_image(Set1{}, s1, t1, h1);
+    auto step = [&](int64_t u, auto X, auto Y) __attribute__((always_inline)) {
+      const bool more = u + 1 < U;
+      const int s2 = next_s(s1, t1);
+      const int64_t t2 = next_t(t1);
+      const bool st2 = u + 2 < U && interior(t2);
+      const bool h2 = st2 && s2 == s1 && t2 == t1 + 1 && interior(t1);
+      if (st2) load_image(X, s2, t2, h2);
+      tile(u);
+      if (more) {
+        lds_order();
+        if (st1) store_image(Y, h1, st2);
+        else build_guarded(s1, t1);
+        advance();
+        st1 = st2;
+        h1 = h2;
+      }
+    };
+    for (int64_t u = 0; u < U; u += 2) {
+      step(u, Set0{}, Set1{});
+      if (u + 1 < U) step(u + 1, Set1{}, Set0{});
     }
   }
 }
@@ -394,11 +464,14 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
   auto n_lo_of = [&](int64_t t) { return (int64_t)TO * D * t - OFF; };
   auto interior = [&](int64_t t) { return n_lo_of(t) >= 0 && n_lo_of(t) + IM <= p.n; };
   auto base_of = [&](int s, int64_t t) { return p.iq + 2 * ((int64_t)s * p.stride + n_lo_of(t)); };
-  auto load_image = [&](int s, int64_t t) {
-    const unsigned char* base = base_of(s, t);
+  constexpr int HC = (IM - D * TO) / 8;          // halo chunks (as in fe_mfma_mono_kernel)
+  static_assert(D * TO / 8 == 5 * 64, "5 new chunks per lane");
+  auto load_image = [&](int s, int64_t t, bool halo) {   // one load site per register (above)
+    const int cf = halo ? HC : 0;
+    const unsigned char* base = base_of(s, t) + 16 * cf;
     static_for<0, NL>([&](auto Q) {
       constexpr int q = Q;
-      if (q < NL - 1 || lane < NC - 64 * (NL - 1)) gload16_nt_v<0>(stg[q], voff, base + 1024 * q);
+      if (lane < NC - cf - 64 * q) gload16_nt_v<0>(stg[q], voff, base + 1024 * q);
     });
   };
   auto put_chunk = [&](int c, unsigned w0, unsigned w1, unsigned w2, unsigned w3) {
@@ -409,11 +482,18 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
     *reinterpret_cast<uint2*>(&img[0][8 * c]) = make_uint2(i_lo, i_hi);
     *reinterpret_cast<uint2*>(&img[1][8 * c]) = make_uint2(q_lo, q_hi);
   };
-  auto store_image = [&]() {
+  auto store_image = [&](bool halo) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cf = halo ? HC : 0;
+    if (halo && lane < 2 * HC) {
+      const int ch = lane / HC, k = lane - ch * HC;
+      const uint2 v = *reinterpret_cast<const uint2*>(&img[ch][D * TO + 8 * k]);
+      *reinterpret_cast<uint2*>(&img[ch][8 * k]) = v;
+    }
+    lds_order();
 #pragma unroll
     for (int q = 0; q < NL; ++q) {
-      const int c = lane + 64 * q;
+      const int c = cf + lane + 64 * q;
       if (c < NC) {
         asm volatile("" : "+v"(stg[q]));
         put_chunk(c, __float_as_uint(stg[q].x), __float_as_uint(stg[q].y), __float_as_uint(stg[q].z),
@@ -443,8 +523,8 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
   if (warm) --t;
   const int64_t U = (b1 - b0) + (warm ? 1 : 0);
   if (interior(t)) {
-    load_image(s, t);
-    store_image();
+    load_image(s, t, false);
+    store_image(false);
   } else {
     build_guarded(s, t);
   }
@@ -458,7 +538,8 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
   for (int64_t u = 0; u < U; ++u) {
     const bool more = u + 1 < U;
     const bool staged = more && interior(t_nx);
-    if (staged) load_image(s_nx, t_nx);
+    const bool halo = staged && s_nx == s && t_nx == t + 1 && interior(t);
+    if (staged) load_image(s_nx, t_nx, halo);
     lds_order();
     i4v acc[2][3];
 #pragma unroll
@@ -534,7 +615,7 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
     }
     if (more) {
       lds_order();
-      if (staged) store_image();
+      if (staged) store_image(halo);
       else build_guarded(s_nx, t_nx);
       s = s_nx;
       t = t_nx;
@@ -628,16 +709,24 @@ hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps, int TA
   p.ataps = ataps;
   p.audio = audio;
   p.audio_stride = audio_stride;
-  static int slots = 0;
+  // image loads in flight per wave: two tiles (default) or one (SDR_FE_MFMA_DEPTH=1, A/B)
+  static int depth = 0, slots = 0;
   if (slots == 0) {
+    const char* de = std::getenv("SDR_FE_MFMA_DEPTH");
+    depth = (de && std::atoi(de) == 1) ? 1 : 2;
     int dev = 0, per = 0;
     hipDeviceProp_t prop;
     int cus = 256;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_mono_kernel, 64, 0) != hipSuccess || per <= 0) per = 1;
-    slots = cus * std::min(per, 12);
+    const hipError_t oe = depth == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_mono_kernel<1>, 64, 0)
+                                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_mono_kernel<2>, 64, 0);
+    if (oe != hipSuccess || per <= 0) per = 1;
+    int cap = 12;
+    if (const char* e = std::getenv("SDR_FE_MFMA_WPC")) cap = std::max(1, std::atoi(e));   // waves per CU (A/B)
+    slots = cus * std::min(per, cap);
   }
   const int64_t grid = std::min<int64_t>(slots, p.total);
-  hipLaunchKernelGGL(fe_mfma_mono_kernel, dim3((unsigned)grid), dim3(64), 0, st, p);
+  if (depth == 1) hipLaunchKernelGGL(fe_mfma_mono_kernel<1>, dim3((unsigned)grid), dim3(64), 0, st, p);
+  else hipLaunchKernelGGL(fe_mfma_mono_kernel<2>, dim3((unsigned)grid), dim3(64), 0, st, p);
   return hipGetLastError();
 }
