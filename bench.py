@@ -581,6 +581,8 @@ def run_rx(args, ws, rank, local):
                 "p99": round(float(np.percentile(sl, 99)), 4),
                 "MS/s": round(S * B / (float(sl.mean()) * 1e-3) / 1e6, 1)}
     stage_ms = {key: round(float(np.mean([st[key] for st in stages])), 5) for key in stages[0]}
+    if stereo:
+        rx.pll_stats(reset=True)
     barrier(ws)
     ctx.synchronize()
     lat = []
@@ -602,6 +604,7 @@ def run_rx(args, ws, rank, local):
     barrier(ws)
     elapsed = max_over_ranks(ws, time.perf_counter() - t0)
     gpu_ms = tm.elapsed_ms(e0, e1) / args.steps if c5 else None
+    pll = rx.pll_stats() if stereo else None
     result = None
     if rank == 0:
         total = S * B * args.steps * ws
@@ -610,6 +613,15 @@ def run_rx(args, ws, rank, local):
         # the front end is the HBM-streaming kernel of the chain: IQ in + demod out per launch
         fe_bytes = S * (B * es + M * 4)
         fe_gbs = fe_bytes / (stage_ms["fe"] * 1e-3) / 1e9
+        if dom == "pll" and pll is not None:
+            par = pll["spec_r0"] + pll["spec_r1"] + pll["spec_r2"]
+            dom_bound = (f"PLL: {par} of {pll['recurrences']} timed recurrences solved in parallel "
+                         f"(pll_spec_kernel, one workgroup per recurrence), {pll['sequential']} by the "
+                         "sequential kernel")
+        elif dom == "fe":
+            dom_bound = "FE: IQ in, demod out (see roofline)"
+        else:
+            dom_bound = "stage FIRs: FP32 VALU multiply-adds"
         result = {
             "metric": f"IQ MSamples/s through the {'multi-stream mono+stereo+RDS receiver' if c5 else 'per-block drop-in path'}"
                       f" ({args.workload}); achieved HBM GB/s vs peak",
@@ -634,12 +646,20 @@ def run_rx(args, ws, rank, local):
                          "kernel": f"FE stage (fe_slot/ring kernel, {rf_taps} taps, + its zf and phase kernels)",
                          "algorithmic_bytes_per_launch": fe_bytes, "avg_launch_ms": stage_ms["fe"]},
             "stage_ms": stage_ms,
-            "dominant_stage": {"stage": dom, "ms": stage_ms[dom],
-                               "bound": ("serial f64 PLL recurrence: one lane per stream, ~"
-                                         f"{stage_ms[dom] * 1e6 / M:.0f} ns per sample step") if dom == "pll" else "see roofline"},
+            "dominant_stage": {"stage": dom, "ms": stage_ms[dom], "bound": dom_bound},
         }
+        if pll is not None:
+            result["pll_solver"] = pll
         if c5:
             result["gpu_ms_per_block"] = round(gpu_ms, 5)
+            # the chain is FIR work on the FP32 VALU (the FE stage's HBM figure stays beside it)
+            fps = chain_flops_per_sample()
+            tf = fps * S * B / (gpu_ms * 1e-3) / 1e12
+            result["fe_roofline"] = result["roofline"]
+            result["roofline"] = {"bound": "valu", "achieved": round(tf, 3), "peak": VALU_PEAK_TFLOPS,
+                                  "unit": "TFLOP/s", "frac": round(tf / VALU_PEAK_TFLOPS, 4), "traffic": None,
+                                  "flops_per_sample": round(fps, 2),
+                                  "note": "FIR flops of the whole chain per input sample x samples / GPU ms per block"}
         else:
             la = np.array(lat) * 1e3
             result["block_latency_ms"] = ({"mean": round(float(la.mean()), 4), "p50": round(float(np.median(la)), 4),
