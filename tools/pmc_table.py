@@ -22,6 +22,6 @@ short = lambda c: c.replace("SQ_", "").replace("INST", "I").replace("ACTIVE", "A
 print(f"{'kernel':58s}" + "".join(f"{short(c):>14s}" for c in cols))
 for k, cs in agg.items():
     waves = (sum(cs["SQ_WAVES"]) / len(cs["SQ_WAVES"])) if per_wave and "SQ_WAVES" in cs else 1.0
-    name = k.split("(")[0].replace("(anonymous namespace)::", "")[-58:]
+    name = k.replace("(anonymous namespace)::", "").removeprefix("void ").split("(")[0][-58:]
     print(f"{name:58s}" + "".join(
         f"{(sum(cs[c]) / len(cs[c]) / (waves if per_wave else 1.0)) if c in cs else float('nan'):14.4g}" for c in cols))
