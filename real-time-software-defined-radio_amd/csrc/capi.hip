@@ -447,7 +447,7 @@ int sdr_fe_mono_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t
   if (fused) {
     FeLaunch a{iq, n, xs, 0, nstreams, rts->dev_f32, &rts->h, rf_taps, rf_decim, u8, nullptr, nullptr, 0,
                nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr};
-    const hipError_t e = sdr_launch_fe_mono(a, ats->dev_f32, audio_taps, audio_decim, audio, as, c->stream);
+    const hipError_t e = sdr_launch_fe_mono(a, ats->dev_f32, ats->dev_rev, audio_taps, audio_decim, audio, as, c->stream);
     if (e == hipSuccess) return SDR_OK;
     if (e != hipErrorInvalidValue) HIP_TRY(e);
     // unsupported by the fused kernel: fall through to the two-kernel path

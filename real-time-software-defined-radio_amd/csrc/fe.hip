@@ -1293,8 +1293,8 @@ hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st) {
 // taps 101 at decim 10 (f32 or u8 IQ), audio taps 151 at decim 5 (model/fmMonoBlock.py:24-31,
 // BASELINE configs); anything else returns hipErrorInvalidValue and the C-ABI runs the
 // two-kernel path.
-hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
-                              int64_t audio_stride, hipStream_t st) {
+hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, const float* ataps_rev, int TA, int DA,
+                              float* audio, int64_t audio_stride, hipStream_t st) {
   if (a.D != 10 || TA != 151 || DA != 5 || a.T != 101) return hipErrorInvalidValue;
   constexpr int D = 10, BD = 960;                  // demod samples per audio block
   FeParams p = fe_params(a);
@@ -1305,7 +1305,7 @@ hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int
   const int64_t total = (int64_t)tps * a.nstreams;
   if (total > 0x7fffffff) return hipErrorInvalidValue;
   if (a.u8) {
-    const hipError_t em = sdr_launch_fe_mono_mfma(a, ataps, TA, DA, audio, audio_stride, st);
+    const hipError_t em = sdr_launch_fe_mono_mfma(a, ataps_rev, TA, DA, audio, audio_stride, st);
     if (em != hipErrorInvalidValue) return em;
     SlotArgs sa{};
     sa.tps = tps; sa.total = total;

@@ -39,6 +39,13 @@ namespace {
 typedef int i4v __attribute__((ext_vector_type(4)));
 
 constexpr float kPiF = 3.14159265358979323846f;
+// Ablation builds of fe_mfma_mono_kernel (tools/build_abl.sh; never the product, which is 0):
+// 1 no audio FIR, 2 no atan2, 4 no MFMAs (B reads kept), 8 no image writes, 16 no image loads
+#ifndef SDR_FE_MFMA_ABL
+#define SDR_FE_MFMA_ABL 0
+#endif
+constexpr int kAbl = SDR_FE_MFMA_ABL;
+
 constexpr float k2PiF = 6.28318530717958647692f;
 
 struct MfmaFe {
@@ -49,7 +56,7 @@ struct MfmaFe {
   int64_t total;            // audio blocks over all streams
   const float* taps;        // 101 RF taps (device)
   float qscale;             // 2^S
-  const float* ataps;       // 151 audio taps (device)
+  const float* argev;       // the 151 audio taps reversed, zero at [-1] and [151] (TapSet::dev_rev)
   float* audio;
   int64_t audio_stride;
 };
@@ -101,23 +108,18 @@ __device__ __forceinline__ void atan2_4(const float (&y)[4], const float (&x)[4]
   const f2v p23 = fast_atan2f_x2(f2v{y[2], y[3]}, f2v{x[2], x[3]});
   phi[0] = p01.x; phi[1] = p01.y; phi[2] = p23.x; phi[3] = p23.y;
 }
-// acc += tap2 * {x, x}, the tap pair in SGPRs (scalar loads of the audio taps), x = the low
-// (HI = false) or high half of x2
-template <bool HI>
-__device__ __forceinline__ void pk_fma_sx(f2v& acc, f2v tap2, const f2v& x2) {
-  if (HI)
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(tap2), "v"(x2));
-  else
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[1,0,1]" : "+v"(acc) : "s"(tap2), "v"(x2));
+// acc.xy += tap2.xy * x2.xy, the tap pair a 64-bit SGPR operand (a scalar load of two
+// consecutive reversed taps: no SALU assembles it)
+__device__ __forceinline__ void pk_fma_s(f2v& acc, f2v tap2, const f2v& x2) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(acc) : "s"(tap2), "v"(x2));
 }
+typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
 typedef const __attribute__((address_space(4))) float* cfp4;   // uniform, read-only: scalar loads
+typedef const __attribute__((address_space(4))) f2a4* cfp2;
 
-// DEPTH = tiles of image loads in flight per wave (1: the next tile's, issued at the top of a
-// tile and waited for at its end; 2: the next two -- two staging register sets, alternating,
-// so each tile's loads have two tiles' compute to land)
-template <int DEPTH>
+// The next tile's image loads are issued at the top of a tile and waited for at its end (r03
+// measured a two-tile-deep variant with alternating staging sets: no faster, 26 more VGPRs).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe_mfma_mono_kernel(MfmaFe p) {
-  static_assert(DEPTH == 1 || DEPTH == 2, "image loads in flight: one or two tiles");
   __shared__ __attribute__((aligned(16))) signed char img[2][IMG + 16];   // I, Q planes
   __shared__ __attribute__((aligned(16))) float dh[HA + AB + 8];
 
@@ -143,7 +145,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
 #pragma unroll
     for (int dg = 0; dg < 3; ++dg) afr[ks][dg] = i4v{w[dg][0], w[dg][1], w[dg][2], w[dg][3]};
   }
-  const cfp4 ga = (cfp4)p.ataps;   // audio taps: SGPR operands (scalar loads, compile-time offsets)
+  // audio taps reversed (g[j] = h[150 - j]), tap pairs as SGPR operands (scalar loads at
+  // compile-time offsets, as rx.hip's fir_tile)
+  const cfp4 gr = (cfp4)p.argev;
 
   // ---- tile images: chunk c = lane + 64 q (16 raw bytes = 8 complex u8 samples) ----
   // Interior images: hand-issued 16-B loads into a staging set, waited for by a counted
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
   // compiler merge the two through register copies taken before the data landed.  Boundary
   // images (stream head / tail: zeros, 0x80, outside [0, n)) are built at write time from
   // guarded 2-B loads.
-  f4v sa[NLD], sb[NLD];
+  f4v stg[NLD];
   const unsigned voff = 16u * lane;
   auto n_lo_of = [&](int64_t t) { return (int64_t)TO * D * t - OFF; };
   auto interior = [&](int64_t t) { return n_lo_of(t) >= 0 && n_lo_of(t) + IMG <= p.n; };
@@ -164,14 +168,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
   static_assert(D * TO / 8 == 5 * 64, "5 new chunks per lane");
   // ONE load site per staging register for both cases (the first chunk a uniform offset, the
   // last load masked by lane count): 5 full loads with the halo, 6 without
-  // (the set is a compile-time index: a runtime reference to it made the compiler shuffle both
-  // sets through copies -- 130 -> 245 VGPRs)
-  using Set0 = std::integral_constant<int, 0>;
-  using Set1 = std::integral_constant<int, 1>;
-  auto load_image = [&](auto SET, int s, int64_t t, bool halo) {
-    f4v (&stg)[NLD] = *(decltype(SET)::value == 0 ? &sa : &sb);
+  auto load_image = [&](int s, int64_t t, bool halo) {
     const int cf = halo ? HC : 0;
     const unsigned char* base = base_of(s, t) + 16 * cf;
+    if (kAbl & 16) return;
     static_for<0, NLD>([&](auto Q) {
       constexpr int q = Q;
       if (lane < NCH - cf - 64 * q) gload16_nt_v<0>(stg[q], voff, base + 1024 * q);
@@ -186,13 +186,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
     *reinterpret_cast<uint2*>(&img[0][8 * c]) = make_uint2(i_lo, i_hi);
     *reinterpret_cast<uint2*>(&img[1][8 * c]) = make_uint2(q_lo, q_hi);
   };
-  // write the staged image; `younger` = loads issued after this set's (the next set's, all
-  // 16-B loads of one tile; loads return in order, so vmcnt(5) retires this set whatever
-  // stores were issued in between -- a 6th load of the younger set only makes it wait longer)
-  auto store_image = [&](auto SET, bool halo, bool younger) {
-    f4v (&stg)[NLD] = *(decltype(SET)::value == 0 ? &sa : &sb);
-    if (younger) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // write the staged image (the audio stores wait in registers: no other VMEM is in flight)
+  auto store_image = [&](bool halo) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int cf = halo ? HC : 0;
     if (halo && lane < 2 * HC) {                 // the halo to the front (both planes), before the new chunks
       const int ch = lane / HC, k = lane - ch * HC;
@@ -205,8 +201,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
       const int c = cf + lane + 64 * q;
       if (c < NCH) {
         asm volatile("" : "+v"(stg[q]));
-        put_chunk(c, __float_as_uint(stg[q].x), __float_as_uint(stg[q].y), __float_as_uint(stg[q].z),
-                  __float_as_uint(stg[q].w));
+        if (!(kAbl & 8))
+          put_chunk(c, __float_as_uint(stg[q].x), __float_as_uint(stg[q].y), __float_as_uint(stg[q].z),
+                    __float_as_uint(stg[q].w));
       }
     }
   };
@@ -235,8 +232,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
   const int64_t U = (b1 - b0) * DA + (warm ? 1 : 0);
   for (int e = lane; e < HA; e += 64) dh[e] = 0.f;          // zero history at a stream start
   if (interior(t)) {
-    load_image(Set0{}, s, t, false);
-    store_image(Set0{}, false, false);
+    load_image(s, t, false);
+    store_image(false);
   } else {
     build_guarded(s, t);
   }
@@ -246,6 +243,39 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
   int64_t t1 = next_t(t);
   float carry = 0.f;
   float d4[4] = {0.f, 0.f, 0.f, 0.f};
+
+  // deferred audio outputs: AQ blocks of 4 outputs per lane, stored when the queue is full and
+  // at the run's end (the run's blocks complete in order: entry k is audio block qb + k)
+  constexpr int AQ = 4;
+  f4v aq[AQ];
+  int nq = 0;
+  int qs = (int)(b0 / p.bps);                                // entry 0: stream qs, block qj
+  int qj = (int)(b0 - (int64_t)qs * p.bps);
+  auto queue_flush = [&]() __attribute__((always_inline)) {
+    static_for<0, AQ>([&](auto K) {
+      constexpr int k = K;
+      if (k < nq) {
+        const int64_t j = (int64_t)TO * qj + 4 * lane;
+        float* ao = p.audio + (int64_t)qs * p.audio_stride + j;
+        if (j + 4 <= p.A && ((uintptr_t)ao & 15) == 0) {
+          *reinterpret_cast<f4v*>(ao) = aq[k];
+        } else {
+          const float rv[4] = {aq[k].x, aq[k].y, aq[k].z, aq[k].w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (j + r < p.A) ao[r] = rv[r];
+        }
+        if (++qj == p.bps) { qj = 0; ++qs; }
+      }
+    });
+    nq = 0;
+  };
+  auto queue_put = [&](const f4v& v) __attribute__((always_inline)) {
+    static_for<0, AQ>([&](auto K) {                          // compile-time slots (no scratch)
+      if ((int)K == nq) aq[K] = v;
+    });
+    if (++nq == AQ) queue_flush();
+  };
 
   // one tile from the image in LDS: MFMAs, demod, the audio block at its end
   auto tile = [&](int64_t u) __attribute__((always_inline)) {
@@ -265,13 +295,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
       for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
         for (int dg = 0; dg < 3; ++dg)
-          acc[ch][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch], acc[ch][dg], 0, 0, 0);
+          acc[ch][dg] = (kAbl & 4) ? acc[ch][dg] + bf[ch]
+                                   : __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch], acc[ch][dg], 0, 0, 0);
     }
     // combine the digits, phases, predecessor, wrap
     float yi[4], yq[4];
     combine_digits(acc, yi, yq);
     float phi[4];
-    atan2_4(yq, yi, phi);                // atan2 is scale-free: the 2^-S / 128 is never applied
+    if (kAbl & 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) phi[i] = yq[i] * 1e-9f + yi[i] * 1e-9f;
+    } else {
+      atan2_4(yq, yi, phi);              // atan2 is scale-free: the 2^-S / 128 is never applied
+    }
     const int src = gl > 0 ? lane - 16 : (pl > 0 ? lane + 47 : 63);
     const float left = __uint_as_float(bperm(src, __float_as_uint(phi[3])));
     float prev = (lane == 0) ? carry : left;
@@ -295,33 +331,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
 #pragma unroll
       for (int i = 0; i < 4; ++i) d4[i] = d[i];
     }
-    if (!(warm && u == 0) && tb == DA - 1) {
-      // audio block jb: a[j] = sum_k g[k] d[5j - k], lane -> j = 256 jb + 4 l + r
+    if (!(kAbl & 1) && !(warm && u == 0) && tb == DA - 1) {
+      // audio block jb: a[j] = sum_k g[k] d[5j - k]
       lds_order();
-      // window sample w, outputs r = 0..3: tap g[150 + 5 r - w] (0 outside [0, 151))
+      // window sample w, output r: tap h[150 + 5 r - w] = g[w - 5 r]; each output keeps its
+      // even- and odd-sample partial sums in one packed register:
+      //   acc_r.xy += (g[j], g[j+1]) * (x_w, x_{w+1}),  j = w - 5 r  (g[-1] = g[151] = 0)
       const float* aw = dh + (HA - (TA - 1)) + DA * 4 * lane;
-      f2v a01 = f2v{0.f, 0.f}, a23 = f2v{0.f, 0.f}, b01 = f2v{0.f, 0.f}, b23 = f2v{0.f, 0.f};
-      auto tap = [&](int k) { return (k >= 0 && k < TA) ? ga[k] : 0.f; };
+      f2v acc[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
       static_for<0, NW / 2>([&](auto W2) {
         constexpr int w = 2 * W2;
         const f2v x2 = *reinterpret_cast<const f2v*>(aw + w);
-        pk_fma_sx<false>(a01, f2v{tap(TA - 1 - w), tap(TA - 1 + DA - w)}, x2);
-        pk_fma_sx<false>(a23, f2v{tap(TA - 1 + 2 * DA - w), tap(TA - 1 + 3 * DA - w)}, x2);
-        pk_fma_sx<true>(b01, f2v{tap(TA - 2 - w), tap(TA - 2 + DA - w)}, x2);
-        pk_fma_sx<true>(b23, f2v{tap(TA - 2 + 2 * DA - w), tap(TA - 2 + 3 * DA - w)}, x2);
+        static_for<0, 4>([&](auto RR) {
+          constexpr int j = w - DA * (int)RR;
+          if constexpr (j >= -1 && j <= TA - 1) {
+            const f2a4 hp = *(cfp2)(gr + j);         // (g[j], g[j+1]): float-indexed pair
+            pk_fma_s(acc[RR], f2v{hp.x, hp.y}, x2);
+          }
+        });
       });
-      const f2v r01 = a01 + b01, r23 = a23 + b23;
-      const int64_t jb = t / DA;
-      const int64_t j = TO * jb + 4 * lane;
-      float* ao = p.audio + (int64_t)s * p.audio_stride + j;
-      if (j + 4 <= p.A && ((uintptr_t)ao & 15) == 0) {
-        *reinterpret_cast<f4v*>(ao) = f4v{r01.x, r01.y, r23.x, r23.y};
-      } else {
-        const float rv[4] = {r01.x, r01.y, r23.x, r23.y};
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (j + r < p.A) ao[r] = rv[r];
-      }
+      // the outputs wait in registers: stores interleaved with the read stream cost far more
+      // than their bytes (OutQ3); blocks leave in order, b0 + entry
+      queue_put(f4v{acc[0].x + acc[0].y, acc[1].x + acc[1].y, acc[2].x + acc[2].y, acc[3].x + acc[3].y});
       lds_order();
       // this block's last 150 demod samples become the next block's history
       if (o >= TO - HA) *reinterpret_cast<f4v*>(&dh[HA - TO + o]) = f4v{d4[0], d4[1], d4[2], d4[3]};
@@ -339,52 +370,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
     t1 = next_t(t);
   };
 
-  if constexpr (DEPTH == 1) {
-    for (int64_t u = 0; u < U; ++u) {
-      // the next tile's loads fly during this tile's MFMAs, epilogue and audio; they are
-      // waited for and written to LDS at the end of the iteration (an in-flight register
-      // never crosses the loop's back edge, where the compiler may copy it)
-      const bool more = u + 1 < U;
-      const bool staged = more && interior(t1);
-      const bool halo = staged && s1 == s && t1 == t + 1 && interior(t);
-      if (staged) load_image(Set1{}, s1, t1, halo);
-      tile(u);
-      if (more) {
-        lds_order();
-        if (staged) store_image(Set1{}, halo, false);
-        else build_guarded(s1, t1);
-        advance();
-      }
-    }
-  } else {
-    // tile u+1's loads (set Y) were issued during tile u-1; tile u issues tile u+2's (set X),
-    // computes, then waits for Y only.  Two steps per trip with the sets swapped keep each
-    // set's registers fixed (the set in flight across the back edge is always sb).
-    bool st1 = U > 1 && interior(t1);
-    bool h1 = st1 && s1 == s && t1 == t + 1 && interior(t);
-    if (st1) load_image(Set1{}, s1, t1, h1);
-    auto step = [&](int64_t u, auto X, auto Y) __attribute__((always_inline)) {
-      const bool more = u + 1 < U;
-      const int s2 = next_s(s1, t1);
-      const int64_t t2 = next_t(t1);
-      const bool st2 = u + 2 < U && interior(t2);
-      const bool h2 = st2 && s2 == s1 && t2 == t1 + 1 && interior(t1);
-      if (st2) load_image(X, s2, t2, h2);
-      tile(u);
-      if (more) {
-        lds_order();
-        if (st1) store_image(Y, h1, st2);
-        else build_guarded(s1, t1);
-        advance();
-        st1 = st2;
-        h1 = h2;
-      }
-    };
-    for (int64_t u = 0; u < U; u += 2) {
-      step(u, Set0{}, Set1{});
-      if (u + 1 < U) step(u + 1, Set1{}, Set0{});
+  for (int64_t u = 0; u < U; ++u) {
+    // the next tile's loads fly during this tile's MFMAs, epilogue and audio; they are
+    // waited for and written to LDS at the end of the iteration (an in-flight register
+    // never crosses the loop's back edge, where the compiler may copy it)
+    const bool more = u + 1 < U;
+    const bool staged = more && interior(t1);
+    const bool halo = staged && s1 == s && t1 == t + 1 && interior(t);
+    if (staged) load_image(s1, t1, halo);
+    tile(u);
+    if (more) {
+      lds_order();
+      if (staged) store_image(halo);
+      else build_guarded(s1, t1);
+      advance();
     }
   }
+  queue_flush();
 }
 
 // ---------------------------------------------------------------------------------
@@ -684,7 +686,7 @@ hipError_t sdr_launch_fe_mfma(const FeLaunch& a, hipStream_t st) {
 // Fused u8 FE + mono on the matrix cores.  Supported: 101 RF taps at decim 10, 151 audio
 // taps at decim 5, u8 IQ with 16-B aligned stream bases; otherwise hipErrorInvalidValue
 // (the caller runs fe_slot_kernel).
-hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps, int TA_, int DA_, float* audio,
+hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps_rev, int TA_, int DA_, float* audio,
                                    int64_t audio_stride, hipStream_t st) {
   if (!a.u8 || a.D != D || a.T != T || TA_ != TA || DA_ != DA || a.hist != 0 || a.zi_i || a.prev_phase || a.demod ||
       a.i_ds || a.last_phi || a.wraps)
@@ -706,27 +708,21 @@ hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps, int TA
   if (p.total > 0x7fffffff) return hipErrorInvalidValue;
   p.taps = a.taps_dev;
   p.qscale = std::ldexp(1.0f, S);
-  p.ataps = ataps;
+  p.argev = ataps_rev;
   p.audio = audio;
   p.audio_stride = audio_stride;
-  // image loads in flight per wave: two tiles (default) or one (SDR_FE_MFMA_DEPTH=1, A/B)
-  static int depth = 0, slots = 0;
+  static int slots = 0;
   if (slots == 0) {
-    const char* de = std::getenv("SDR_FE_MFMA_DEPTH");
-    depth = (de && std::atoi(de) == 1) ? 1 : 2;
     int dev = 0, per = 0;
     hipDeviceProp_t prop;
     int cus = 256;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
-    const hipError_t oe = depth == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_mono_kernel<1>, 64, 0)
-                                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_mono_kernel<2>, 64, 0);
-    if (oe != hipSuccess || per <= 0) per = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_mono_kernel, 64, 0) != hipSuccess || per <= 0) per = 1;
     int cap = 12;
     if (const char* e = std::getenv("SDR_FE_MFMA_WPC")) cap = std::max(1, std::atoi(e));   // waves per CU (A/B)
     slots = cus * std::min(per, cap);
   }
   const int64_t grid = std::min<int64_t>(slots, p.total);
-  if (depth == 1) hipLaunchKernelGGL(fe_mfma_mono_kernel<1>, dim3((unsigned)grid), dim3(64), 0, st, p);
-  else hipLaunchKernelGGL(fe_mfma_mono_kernel<2>, dim3((unsigned)grid), dim3(64), 0, st, p);
+  hipLaunchKernelGGL(fe_mfma_mono_kernel, dim3((unsigned)grid), dim3(64), 0, st, p);
   return hipGetLastError();
 }

@@ -28,14 +28,15 @@ struct FirLaunch {
 struct PllCfg { double freq, fs, scale, adj, kp, ki; };
 
 hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st);
-hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
-                              int64_t audio_stride, hipStream_t st);
+// ataps / ataps_rev: the audio taps forward and reversed (TapSet::dev_f32 / dev_rev)
+hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, const float* ataps_rev, int TA, int DA,
+                              float* audio, int64_t audio_stride, hipStream_t st);
 // u8 FE + mono with the RF FIR on the int8 matrix cores (fe_mfma.hip); hipErrorInvalidValue
 // when the configuration is not the one it covers
 // u8 FE (FIR + decimate + demod with carried state) on the int8 matrix cores (fe_mfma.hip):
 // 101 / 151 taps; hipErrorInvalidValue when the configuration is not one it covers
 hipError_t sdr_launch_fe_mfma(const FeLaunch& a, hipStream_t st);
-hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps, int TA, int DA, float* audio,
+hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps_rev, int TA, int DA, float* audio,
                                    int64_t audio_stride, hipStream_t st);
 hipError_t sdr_launch_iq_zf(const void* iq, int u8, int64_t n, int64_t stride, int nstreams,
                             const double* b_dev, int T, const double* zi_i, const double* zi_q,
