@@ -1496,10 +1496,22 @@ __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
   int bcur = -1;
   double sh = 0.0, vp = 0.0, vv = 0.0;
   bool lin = false;
+  // every phase of the thread is loaded before the first is used (one memory round trip, not
+  // NCO_NR), and the pseudo-block index advances by comparison (pb > 256: at most one step)
+  const int64_t k0 = (int64_t)blockIdx.x * NCO_NR * 256 + threadIdx.x;
+  double phv[NCO_NR];
+#pragma unroll
   for (int i = 0; i < NCO_NR; ++i) {
-    const int64_t k = ((int64_t)blockIdx.x * NCO_NR + i) * 256 + threadIdx.x;
+    const int64_t k = k0 + (int64_t)i * 256;
+    phv[i] = k < P.n ? ph[k] : 0.0;
+  }
+  int b = (int)(k0 / pb);
+  int64_t bnext = (int64_t)(b + 1) * pb;
+#pragma unroll
+  for (int i = 0; i < NCO_NR; ++i) {
+    const int64_t k = k0 + (int64_t)i * 256;
     if (k >= P.n) break;
-    const int b = (int)(k / pb);
+    if (k >= bnext) { ++b; bnext += pb; }
     if (b != bcur) {                         // a new pseudo-block: its shift and A^(kk+1) d
       bcur = b;
       const LongBlk* B = long_blk(P, g, b);
@@ -1521,7 +1533,7 @@ __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
       const double np = m.a * vp + m.b * vv, nv = m.c * vp + m.d * vv;
       vp = np; vv = nv;
     }
-    double p = fma(sh, kP1, fma(sh, kP2, ph[k]));
+    double p = fma(sh, kP1, fma(sh, kP2, phv[i]));
     if (lin) p = p + vp;
     const double th = w * ((off + (double)k) + 1.0) + p;
     const double a = th * cfg.scale + cfg.adj;
