@@ -689,21 +689,29 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
   // Extrapolating by integ does worse: integ swings with the loop's own oscillation.)
   {
     // sign(x_k) exp(-i w (off + k)) = exp(-i 2 pi fract(1/2 - c_k)): a hard-limited
-    // correlation, as the loop's detector
+    // correlation, as the loop's detector.  The nominal NCO's phasor exp(i w (off + k)) is
+    // rotated by exp(i w) from the chunk's first step in f32 (L <= 64 steps: a drift of ~1e-6,
+    // far below what a guess needs -- the check, not the guess, makes the solve exact)
     float zr = 0.f, zi = 0.f;
-    for (int i0 = 0; i0 < L; i0 += SB) {
-      int cd[SB];
+    {
+      const double a0 = __builtin_amdgcn_fract((w * kInv2Pi) * (off + (double)k0));
+      float ci, cr, ds, dc;
+      __sincosf((float)(k2Pi * a0), &ci, &cr);
+      __sincosf((float)w, &ds, &dc);
+      for (int i0 = 0; i0 < L; i0 += SB) {
+        int cd[SB];
 #pragma unroll
-      for (int u = 0; u < SB; ++u) cd[u] = code[(i0 + u) * CSTR + tid];
+        for (int u = 0; u < SB; ++u) cd[u] = code[(i0 + u) * CSTR + tid];
 #pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        const double c = cval(cd[u], k0 + i0 + u);
-        const float a = (float)(k2Pi * __builtin_amdgcn_fract(0.5 - c));
-        float sa, ca;
-        __sincosf(a, &sa, &ca);
-        const bool use = i0 + u < len && cd[u] != 2;   // (a 0 / NaN input is rejected below anyway)
-        zr += use ? ca : 0.f;
-        zi -= use ? sa : 0.f;
+        for (int u = 0; u < SB; ++u) {
+          // x > 0: +exp(-i a); x < 0: -exp(-i a) (the pi of sel); 0 / NaN / past the chunk: 0
+          const float sg = (i0 + u < len && cd[u] != 2) ? (cd[u] == 0 ? 1.f : -1.f) : 0.f;
+          zr = fmaf(sg, cr, zr);
+          zi = fmaf(-sg, ci, zi);
+          const float nr = cr * dc - ci * ds;
+          ci = fmaf(cr, ds, ci * dc);
+          cr = nr;
+        }
       }
     }
     yb[tid] = d2v{(double)zr, (double)zi};
