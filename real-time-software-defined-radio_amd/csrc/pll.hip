@@ -662,6 +662,8 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
   // there: only discarded steps read them, and every slot is in the array.)
   {
     constexpr int SG = 32;
+    // kk / L by a multiply-high (L <= 64, kk < 2^16: exact with m = floor(2^32 / L) + 1)
+    const unsigned mL = 0xffffffffu / (unsigned)L + 1u;
     for (int b0 = tid; b0 < N; b0 += SG * SPEC_T) {
       float xv[SG];
 #pragma unroll
@@ -670,7 +672,7 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
       for (int u = 0; u < SG; ++u) {
         const int kk = b0 + u * SPEC_T;
         if (kk < N) {
-          const int j = kk / L, i = kk - j * L;
+          const int j = (int)__umulhi((unsigned)kk, mL), i = kk - j * L;
           code[i * CSTR + j] = (int8_t)(xv[u] > 0.f ? 0 : (xv[u] < 0.f ? 1 : 2));
         }
       }
