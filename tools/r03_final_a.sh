@@ -1,7 +1,7 @@
 # round-3 closing set, part A: full GPU suite, offsets table, smoke, every bench line with CPU baselines
 set -e
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r03_final
+O=$R/gpurun_out/${R03_OUT:-r03_final}
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests > $O/pytest_gpu_full.txt 2>&1

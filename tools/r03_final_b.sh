@@ -2,7 +2,7 @@
 # streams, u8 MFMA mono) and HBM traffic passes for the headline and u8
 set -e
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r03_final
+O=$R/gpurun_out/${R03_OUT:-r03_final}
 mkdir -p $O
 export TMPDIR=/tmp
 cd /tmp

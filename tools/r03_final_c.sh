@@ -3,7 +3,7 @@
 # (fe_mfma_demod_kernel, pll_spec_kernel<512,true>) and the u8 MFMA mono kernel
 set -e
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r03_final
+O=$R/gpurun_out/${R03_OUT:-r03_final}
 mkdir -p $O
 export TMPDIR=/tmp
 cd /tmp
