@@ -82,6 +82,7 @@ int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T) 
     TapSet& t = c->taps.front();
     (void)hipFree(t.dev_f32);
     (void)hipFree(t.dev_f64);
+    (void)hipFree(t.dev_afr);
     c->taps.pop_front();
   }
   TapSet t;
@@ -99,6 +100,11 @@ int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T) 
   t.dev_rev = t.dev_f32 + cap + 2;
   HIP_TRY(hipMemcpy(t.dev_f32, fr.data(), sizeof(float) * fr.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(t.dev_f64, b, sizeof(double) * T, hipMemcpyHostToDevice));
+  std::vector<int> afr;
+  if (sdr_mfma_fragments(f.data(), T, &afr)) {        // the RF taps of the u8 MFMA front end
+    HIP_TRY(hipMalloc(&t.dev_afr, sizeof(int) * afr.size()));
+    HIP_TRY(hipMemcpy(t.dev_afr, afr.data(), sizeof(int) * afr.size(), hipMemcpyHostToDevice));
+  }
   c->taps.push_back(std::move(t));
   *out = &c->taps.back();
   return SDR_OK;
@@ -197,7 +203,7 @@ void sdr_destroy(sdr_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (int s = 0; s < S_NSLOT; ++s) if (c->slot[s]) (void)hipFree(c->slot[s]);
-  for (TapSet& t : c->taps) { (void)hipFree(t.dev_f32); (void)hipFree(t.dev_f64); }
+  for (TapSet& t : c->taps) { (void)hipFree(t.dev_f32); (void)hipFree(t.dev_f64); (void)hipFree(t.dev_afr); }
   if (c->pll_stats) (void)hipFree(c->pll_stats);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -386,7 +392,7 @@ int sdr_rf_frontend_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int
   if (fast) {
     FeLaunch a{iq, n, nstreams > 1 ? stride : ceil_div(n, G) * G, hist, nstreams,
                ts->dev_f32, &ts->h, taps, decim, u8, zi_i, zi_q, zs, prev_phase,
-               demod, nstreams > 1 ? out_stride : M, i_ds, q_ds, last_phi, wraps};
+               demod, nstreams > 1 ? out_stride : M, i_ds, q_ds, last_phi, wraps, ts->dev_afr};
     HIP_TRY(sdr_launch_fe(a, c->stream));
   } else {
     // generic tap counts: strided FIR on I and Q, then the standalone discriminator
@@ -447,6 +453,7 @@ int sdr_fe_mono_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t
   if (fused) {
     FeLaunch a{iq, n, xs, 0, nstreams, rts->dev_f32, &rts->h, rf_taps, rf_decim, u8, nullptr, nullptr, 0,
                nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr};
+    a.afr = rts->dev_afr;
     const hipError_t e = sdr_launch_fe_mono(a, ats->dev_f32, ats->dev_rev, audio_taps, audio_decim, audio, as, c->stream);
     if (e == hipSuccess) return SDR_OK;
     if (e != hipErrorInvalidValue) HIP_TRY(e);

@@ -45,6 +45,11 @@ constexpr float kPiF = 3.14159265358979323846f;
 #define SDR_FE_MFMA_ABL 0
 #endif
 constexpr int kAbl = SDR_FE_MFMA_ABL;
+// A/B builds: the A fragments built in every wave's prologue instead of loaded (-DSDR_FE_MFMA_HOST_AFR=0)
+#ifndef SDR_FE_MFMA_HOST_AFR
+#define SDR_FE_MFMA_HOST_AFR 1
+#endif
+constexpr bool kHostAfr = SDR_FE_MFMA_HOST_AFR != 0;
 
 constexpr float k2PiF = 6.28318530717958647692f;
 
@@ -57,6 +62,7 @@ struct MfmaFe {
   const float* taps;        // 101 RF taps (device)
   float qscale;             // 2^S
   const float* argev;       // the 151 audio taps reversed, zero at [-1] and [151] (TapSet::dev_rev)
+  const i4v* afr;           // nullable: the A fragments built on the host (TapSet::dev_afr)
   float* audio;
   int64_t audio_stride;
 };
@@ -129,8 +135,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
   if (b0 >= b1) return;
   const int pl = lane & 15, gl = lane >> 4;
 
-  // A fragments: lane (r = l & 15, g = l >> 4), byte j of K-step ks <-> j' = 64 ks + 16 g + j
+  // A fragments: lane (r = l & 15, g = l >> 4), byte j of K-step ks <-> j' = 64 ks + 16 g + j;
+  // from the tap set's table (one 16-B load each) or built here (~700 VALU per wave)
   i4v afr[4][3];
+  if (p.afr != nullptr) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg) afr[ks][dg] = p.afr[(ks * 3 + dg) * 64 + lane];
+  } else
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     int w[3][4] = {};
@@ -408,6 +421,7 @@ struct MfmaDemod {
   int64_t tps, total;         // tiles per stream, over all streams
   const float* taps;
   float qscale;               // 2^S
+  const i4v* afr;             // nullable: the A fragments built on the host (TapSet::dev_afr)
   const double* zi_i;         // nullable: lfilter states (T - 1 per stream, zi_stride apart)
   const double* zi_q;
   int64_t zi_stride;
@@ -446,6 +460,12 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
   const int pl = lane & 15, gl = lane >> 4;
 
   i4v afr[KS][3];
+  if (p.afr != nullptr) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int dg = 0; dg < 3; ++dg) afr[ks][dg] = p.afr[(ks * 3 + dg) * 64 + lane];
+  } else
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     int w[3][4] = {};
@@ -644,6 +664,7 @@ hipError_t launch_demod_mfma_t(const FeLaunch& a, hipStream_t st) {
   if (p.total > 0x7fffffff) return hipErrorInvalidValue;
   p.taps = a.taps_dev;
   p.qscale = std::ldexp(1.0f, S);
+  p.afr = kHostAfr ? reinterpret_cast<const i4v*>(a.afr) : nullptr;
   p.zi_i = a.zi_i;
   p.zi_q = a.zi_q;
   p.zi_stride = a.zi_stride;
@@ -670,6 +691,36 @@ hipError_t launch_demod_mfma_t(const FeLaunch& a, hipStream_t st) {
 }
 
 }  // namespace
+
+// The A fragments the kernels build from the taps (fe_mfma_*_kernel prologues), on the host:
+// the same f32 product h * 2^S, rintf, signed base-256 digits.
+bool sdr_mfma_fragments(const float* h, int T_, std::vector<int>* out) {
+  int KS, OFFT;
+  if (T_ == 101) { KS = DemodShape<101>::KS; OFFT = DemodShape<101>::OFF; }
+  else if (T_ == 151) { KS = DemodShape<151>::KS; OFFT = DemodShape<151>::OFF; }
+  else return false;
+  static_assert(DemodShape<101>::KS == 4 && DemodShape<101>::OFF == OFF, "mono and demod kernels share the T = 101 shape");
+  float hmax = 0.f;
+  for (int k = 0; k < T_; ++k) hmax = std::max(hmax, std::fabs(h[k]));
+  if (!(hmax > 0.f) || !std::isfinite(hmax)) return false;
+  const float qs = std::ldexp(1.0f, tap_scale_exp(hmax));
+  out->assign((size_t)KS * 3 * 64 * 4, 0);
+  for (int ks = 0; ks < KS; ++ks)
+    for (int lane = 0; lane < 64; ++lane) {
+      const int pl = lane & 15, gl = lane >> 4;
+      for (int j = 0; j < 16; ++j) {
+        const int k = D * pl + OFFT - (64 * ks + 16 * gl + j);
+        const float hv = (k >= 0 && k < T_) ? h[k] : 0.f;
+        int q = (int)std::rint(hv * qs);
+        for (int dg = 0; dg < 3; ++dg) {
+          const int d = ((q & 0xff) ^ 0x80) - 0x80;      // the kernels' digit(): q = d + 256 (q')
+          q = (q - d) >> 8;
+          (*out)[(((size_t)ks * 3 + dg) * 64 + lane) * 4 + (j >> 2)] |= (d & 0xff) << (8 * (j & 3));
+        }
+      }
+    }
+  return true;
+}
 
 // u8 RF front end (FIR + decimate + demod, carried state) on the matrix cores: 101 or 151
 // taps at decim 10, u8 IQ with 16-B aligned stream bases, no history prefix and no
@@ -708,6 +759,7 @@ hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps_rev, in
   if (p.total > 0x7fffffff) return hipErrorInvalidValue;
   p.taps = a.taps_dev;
   p.qscale = std::ldexp(1.0f, S);
+  p.afr = kHostAfr ? reinterpret_cast<const i4v*>(a.afr) : nullptr;
   p.argev = ataps_rev;
   p.audio = audio;
   p.audio_stride = audio_stride;

@@ -871,7 +871,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     const int64_t fstride = S > 1 ? xs : ceil_div(r->B, G) * G;
     FeLaunch a{iq, r->B, fstride, 0, S, ts[SDR_RX_F_RF]->dev_f32, &ts[SDR_RX_F_RF]->h, Trf, r->rf_decim, r->u8,
                zin(Z_FE_I), zin(Z_FE_Q), r->zlen[Z_FE_I], r->phase, o[SDR_RX_O_DEMOD], ms, nullptr, nullptr,
-               r->last_phi, r->wraps};
+               r->last_phi, r->wraps, ts[SDR_RX_F_RF]->dev_afr};
     HIP_TRY(sdr_launch_fe(a, fs));
     fst = FeState{iq, r->B, xs, ts[SDR_RX_F_RF]->dev_f64, zin(Z_FE_I), zin(Z_FE_Q), zout(Z_FE_I), zout(Z_FE_Q),
                   r->zlen[Z_FE_I], r->last_phi, r->wraps, r->phase, Trf, r->u8, 1};

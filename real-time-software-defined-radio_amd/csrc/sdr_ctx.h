@@ -26,6 +26,7 @@ struct TapSet {
   float* dev_f32 = nullptr;   // [0, cap): the taps; then, from dev_rev - 1: 0, the taps reversed, 0, 0
   float* dev_rev = nullptr;   // dev_rev[j] = h[T-1-j], dev_rev[-1] = dev_rev[T] = 0 (packed FIR tiles)
   double* dev_f64 = nullptr;
+  int* dev_afr = nullptr;     // T = 101 / 151: the u8 MFMA front end's A fragments (fe_mfma.hip)
 };
 
 // the calling thread's last error message; returns `code`

@@ -3,6 +3,7 @@
 // translation-unit boundary: each .hip file includes this header, so a field change is a
 // compile error everywhere instead of a silent ODR mismatch.
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -14,6 +15,7 @@ struct FeLaunch {
   const float* taps_dev; const TapsF32* taps; int T; int D; int u8;
   const double* zi_i; const double* zi_q; int64_t zi_stride; const double* prev_phase;
   float* demod; int64_t out_stride; float* i_ds; float* q_ds; float* last_phi; int* wraps;
+  const int* afr;   // nullable: the taps' MFMA A fragments (TapSet::dev_afr; else built in-kernel)
 };
 
 // Real-channel FIR with decimation (fir.hip); `pre` selects a fused pre-op on the input
@@ -36,6 +38,9 @@ hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, const float
 // u8 FE (FIR + decimate + demod with carried state) on the int8 matrix cores (fe_mfma.hip):
 // 101 / 151 taps; hipErrorInvalidValue when the configuration is not one it covers
 hipError_t sdr_launch_fe_mfma(const FeLaunch& a, hipStream_t st);
+// the u8 MFMA front end's A fragments of RF taps h (T = 101 or 151, decim 10), as the kernels
+// would build them: ints in [ks][digit][lane][4] order; false for other T
+bool sdr_mfma_fragments(const float* h, int T, std::vector<int>* out);
 hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps_rev, int TA, int DA, float* audio,
                                    int64_t audio_stride, hipStream_t st);
 hipError_t sdr_launch_iq_zf(const void* iq, int u8, int64_t n, int64_t stride, int nstreams,
