@@ -109,9 +109,44 @@ __device__ __forceinline__ void combine_digits(const i4v (&acc)[2][3], float (&y
     yq[i] = fmaf((float)acc[1][2][i], 65536.f, (float)(acc[1][1][i] * 256 + acc[1][0][i]));
   }
 }
+// fast_atan2f_x2 (sdr_common.h) for finite operands: the FIR sums here are integers held in
+// f32, never infinite or NaN, so the IEEE special cases (|x| or |y| infinite, NaN) drop out;
+// the same arithmetic otherwise, so the same results
+__device__ __forceinline__ f2v atan2_x2_finite(f2v y, f2v x) {
+  const float ax0 = fabsf(x.x), ay0 = fabsf(y.x), ax1 = fabsf(x.y), ay1 = fabsf(y.y);
+  const float mn0 = fminf(ax0, ay0), mx0 = fmaxf(ax0, ay0), mn1 = fminf(ax1, ay1), mx1 = fmaxf(ax1, ay1);
+  const f2v mn = f2v{mn0, mn1};
+  const f2v mxs = f2v{fmaxf(mx0, 1e-30f), fmaxf(mx1, 1e-30f)};
+  const f2v rc = f2v{__builtin_amdgcn_rcpf(mxs.x), __builtin_amdgcn_rcpf(mxs.y)};
+  f2v a = mn * rc;
+  a = __builtin_elementwise_fma(__builtin_elementwise_fma(-mxs, a, mn), rc, a);
+  const f2v s = a * a;
+  auto c = [](float v) { return f2v{v, v}; };
+  f2v r = c(0.002849547192454338f);
+  r = __builtin_elementwise_fma(r, s, c(-0.01606736145913601f));
+  r = __builtin_elementwise_fma(r, s, c(0.04268963634967804f));
+  r = __builtin_elementwise_fma(r, s, c(-0.0750415101647377f));
+  r = __builtin_elementwise_fma(r, s, c(0.1064087525010109f));
+  r = __builtin_elementwise_fma(r, s, c(-0.1420363187789917f));
+  r = __builtin_elementwise_fma(r, s, c(0.19992618262767792f));
+  r = __builtin_elementwise_fma(r, s, c(-0.3333307206630707f));
+  r = __builtin_elementwise_fma(r, s, c(1.0f));
+  r = r * a;
+  float r0 = r.x, r1 = r.y;
+  r0 = (ay0 > ax0) ? 1.57079632679489662f - r0 : r0;
+  r1 = (ay1 > ax1) ? 1.57079632679489662f - r1 : r1;
+  r0 = (x.x < 0.f) ? 3.14159265358979324f - r0 : r0;
+  r1 = (x.y < 0.f) ? 3.14159265358979324f - r1 : r1;
+  asm volatile("" : "+v"(r0), "+v"(r1));
+  r0 = (mx0 == 0.f) ? (__builtin_signbitf(x.x) ? 3.14159265358979324f : 0.f) : r0;
+  r1 = (mx1 == 0.f) ? (__builtin_signbitf(x.y) ? 3.14159265358979324f : 0.f) : r1;
+  return f2v{copysignf(r0, y.x), copysignf(r1, y.y)};
+}
+// FINITE: integer sums only (the mono kernel); the demod kernel adds the caller's lfilter zi
+template <bool FINITE>
 __device__ __forceinline__ void atan2_4(const float (&y)[4], const float (&x)[4], float (&phi)[4]) {
-  const f2v p01 = fast_atan2f_x2(f2v{y[0], y[1]}, f2v{x[0], x[1]});
-  const f2v p23 = fast_atan2f_x2(f2v{y[2], y[3]}, f2v{x[2], x[3]});
+  const f2v p01 = FINITE ? atan2_x2_finite(f2v{y[0], y[1]}, f2v{x[0], x[1]}) : fast_atan2f_x2(f2v{y[0], y[1]}, f2v{x[0], x[1]});
+  const f2v p23 = FINITE ? atan2_x2_finite(f2v{y[2], y[3]}, f2v{x[2], x[3]}) : fast_atan2f_x2(f2v{y[2], y[3]}, f2v{x[2], x[3]});
   phi[0] = p01.x; phi[1] = p01.y; phi[2] = p23.x; phi[3] = p23.y;
 }
 // acc.xy += tap2.xy * x2.xy, the tap pair a 64-bit SGPR operand (a scalar load of two
@@ -319,7 +354,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
 #pragma unroll
       for (int i = 0; i < 4; ++i) phi[i] = yq[i] * 1e-9f + yi[i] * 1e-9f;
     } else {
-      atan2_4(yq, yi, phi);              // atan2 is scale-free: the 2^-S / 128 is never applied
+      atan2_4<true>(yq, yi, phi);        // atan2 is scale-free: the 2^-S / 128 is never applied
     }
     const int src = gl > 0 ? lane - 16 : (pl > 0 ? lane + 47 : 63);
     const float left = __uint_as_float(bperm(src, __float_as_uint(phi[3])));
@@ -591,7 +626,7 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
         }
     }
     float phi[4];
-    atan2_4(yq, yi, phi);                // atan2 is scale-free: the 2^-S / 128 is never applied
+    atan2_4<false>(yq, yi, phi);         // atan2 is scale-free: the 2^-S / 128 is never applied
     const int src = gl > 0 ? lane - 16 : (pl > 0 ? lane + 47 : 63);
     const float left = __uint_as_float(bperm(src, __float_as_uint(phi[3])));
     float prev = (lane == 0) ? carry : left;

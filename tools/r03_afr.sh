@@ -1,13 +1,11 @@
-# host-built MFMA A fragments (product) vs built in every wave (libsdr_noafr), same box
+# u8 MFMA mono kernel iteration: u8 parity tests, u8 bench (twice), waves-per-CU sweep
 set -e
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r03_afr2
+O=$R/gpurun_out/r03_u8it
 mkdir -p $O
 cd $R
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests -k "u8 or mfma or mono" > $O/pytest.txt 2>&1
 A="--iq u8 --blocks 128 --no-cpu --no-extras --steps 50 --warmup 10"
-for k in 1 2; do
-timeout -k 10 120 python bench.py $A > $O/u8_afr$k.json 2> $O/u8_afr$k.err
-SDR_LIB=$R/real-time-software-defined-radio_amd/libsdr_noafr.so timeout -k 10 120 python bench.py $A > $O/u8_noafr$k.json 2> $O/u8_noafr$k.err
-done
-timeout -k 10 200 python -u bench.py --workload c5 --streams 8 --no-cpu > $O/c5_afr.json 2> $O/c5_afr.err
-SDR_LIB=$R/real-time-software-defined-radio_amd/libsdr_noafr.so timeout -k 10 200 python -u bench.py --workload c5 --streams 8 --no-cpu > $O/c5_noafr.json 2> $O/c5_noafr.err
+timeout -k 10 120 python bench.py $A > $O/u8_1.json 2> $O/u8_1.err
+timeout -k 10 120 python bench.py $A > $O/u8_2.json 2> $O/u8_2.err
+for w in 8 10; do SDR_FE_MFMA_WPC=$w timeout -k 10 120 python bench.py $A > $O/u8_w$w.json 2> $O/u8_w$w.err; done
