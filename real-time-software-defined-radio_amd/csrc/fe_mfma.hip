@@ -325,11 +325,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
     if (++nq == AQ) queue_flush();
   };
 
-  // one tile from the image in LDS: MFMAs, demod, the audio block at its end
-  auto tile = [&](int64_t u) __attribute__((always_inline)) {
-    lds_order();                                              // image of tile t written
-    // B fragments of both channels, one K-step at a time (registers: occupancy)
-    i4v acc[2][3];
+  // the MFMAs of the tile whose image is in LDS: B fragments of both channels, one K-step at a
+  // time (registers: occupancy)
+  auto mfma_tile = [&](i4v (&acc)[2][3]) __attribute__((always_inline)) {
+    lds_order();                                              // the image written
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
@@ -346,7 +345,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
           acc[ch][dg] = (kAbl & 4) ? acc[ch][dg] + bf[ch]
                                    : __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch], acc[ch][dg], 0, 0, 0);
     }
-    // combine the digits, phases, predecessor, wrap
+  };
+  // tile (s, t) from its accumulators: digits combined, demod, the audio block at its end
+  auto epilogue = [&](const i4v (&acc)[2][3], int64_t u) __attribute__((always_inline)) {
     float yi[4], yq[4];
     combine_digits(acc, yi, yq);
     float phi[4];
@@ -418,21 +419,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
     t1 = next_t(t);
   };
 
+  // Per tile: its B reads and MFMAs go out; the next tile's image (whose loads flew during
+  // the previous epilogue) is written while the MFMAs run -- a wave's LDS operations execute
+  // in order, so the stores land after this tile's B reads -- then the tile after's loads go
+  // out and fly during this tile's epilogue (an in-flight register never crosses the loop's
+  // back edge, where the compiler may copy it: the loads are issued and retired within one
+  // iteration's straight-line span of their own)
+  bool staged = U > 1 && interior(t1);
+  bool halo = staged && s1 == s && t1 == t + 1 && interior(t);
+  if (staged) load_image(s1, t1, halo);
+  i4v acc[2][3];
   for (int64_t u = 0; u < U; ++u) {
-    // the next tile's loads fly during this tile's MFMAs, epilogue and audio; they are
-    // waited for and written to LDS at the end of the iteration (an in-flight register
-    // never crosses the loop's back edge, where the compiler may copy it)
     const bool more = u + 1 < U;
-    const bool staged = more && interior(t1);
-    const bool halo = staged && s1 == s && t1 == t + 1 && interior(t);
-    if (staged) load_image(s1, t1, halo);
-    tile(u);
+    mfma_tile(acc);                                           // tile (s, t)
     if (more) {
       lds_order();
-      if (staged) store_image(halo);
+      if (staged) store_image(halo);                          // tile (s1, t1)
       else build_guarded(s1, t1);
-      advance();
+      const int s2 = next_s(s1, t1);
+      const int64_t t2 = next_t(t1);
+      staged = u + 2 < U && interior(t2);
+      halo = staged && s2 == s1 && t2 == t1 + 1 && interior(t1);
+      if (staged) load_image(s2, t2, halo);
     }
+    epilogue(acc, u);
+    if (more) advance();
   }
   queue_flush();
 }
