@@ -603,11 +603,13 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
   int wsum = 0;
   const double zscale = (double)p.qscale * 128.0;    // real-domain zi -> the integer sum's scale
 
+  // as fe_mfma_mono_kernel: the next image is written while this tile's MFMAs run, the loads
+  // of the one after fly during this tile's epilogue
+  bool staged = U > 1 && interior(t_nx);
+  bool halo = staged && s_nx == s && t_nx == t + 1 && interior(t);
+  if (staged) load_image(s_nx, t_nx, halo);
   for (int64_t u = 0; u < U; ++u) {
     const bool more = u + 1 < U;
-    const bool staged = more && interior(t_nx);
-    const bool halo = staged && s_nx == s && t_nx == t + 1 && interior(t);
-    if (staged) load_image(s_nx, t_nx, halo);
     lds_order();
     i4v acc[2][3];
 #pragma unroll
@@ -624,6 +626,17 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
 #pragma unroll
         for (int dg = 0; dg < 3; ++dg)
           acc[ch][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(afr[ks][dg], bf[ch], acc[ch][dg], 0, 0, 0);
+    }
+    if (more) {
+      lds_order();
+      if (staged) store_image(halo);                          // tile (s_nx, t_nx)
+      else build_guarded(s_nx, t_nx);
+      int s2 = s_nx;
+      int64_t t2 = t_nx + 1;
+      if (t2 == p.tps) { t2 = 0; ++s2; }
+      staged = u + 2 < U && interior(t2);
+      halo = staged && s2 == s_nx && t2 == t_nx + 1 && interior(t_nx);
+      if (staged) load_image(s2, t2, halo);
     }
     const int64_t mo = (int64_t)TO * t + 16 * pl + 4 * gl;     // first output of this lane
     float yi[4], yq[4];
@@ -682,9 +695,6 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
       wsum = 0;
     }
     if (more) {
-      lds_order();
-      if (staged) store_image(halo);
-      else build_guarded(s_nx, t_nx);
       s = s_nx;
       t = t_nx;
       t_nx = t + 1;
