@@ -480,7 +480,14 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 // literal general step (fI, fQ from the caller's state), as in the loop kernels.  A completed
 // recurrence is marked by c[0] = +inf (c[0] is the literal sample's slot: the loop kernels
 // never read it, and the prep kernel rewrites it every call).
-constexpr int SPEC_W = 256;          // warm-up samples before each chunk
+#ifndef SDR_SPEC_W
+#define SDR_SPEC_W 128
+#endif
+// warm-up samples before each chunk (A/B builds: -DSDR_SPEC_W=).  r03, per-block solves at 64
+// streams x 2 PLLs (profiles/r03/iter/specw_*): 256 -> 86 us, 128 -> 73 us, 64 -> 66 us per
+// block, every recurrence in round 0 at each, the offset sweep (tests/test_offsets.py) too;
+// 128 keeps a margin for inputs noisier than the synthetic ones
+constexpr int SPEC_W = SDR_SPEC_W;
 #ifndef SDR_SPEC_W_LONG
 #define SDR_SPEC_W_LONG 16
 #endif
