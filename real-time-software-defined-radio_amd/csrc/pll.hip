@@ -1492,7 +1492,10 @@ __global__ void nco_jobs_kernel(PllJobs P) {
 // chain accepted the pseudo-block with (kk: the step within it; zero for most blocks).
 // Workgroup: 256 x NCO_NR consecutive steps of one recurrence, thread t the steps t + 256 i
 // (coalesced), its responses 256 steps apart by A^256; A^(2^i) in LDS.
-constexpr int NCO_NR = 8;
+#ifndef SDR_NCO_NR
+#define SDR_NCO_NR 8
+#endif
+constexpr int NCO_NR = SDR_NCO_NR;     // outputs per thread of nco_long_kernel (A/B builds: -DSDR_NCO_NR=)
 __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
 #pragma clang fp contract(off)
   __shared__ Mat2 ap[15];
