@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--split-stream", action="store_true",
                     help="mono: ONE stream of --blocks blocks split over the ranks, each range with a read-only "
                          "halo (SURVEY §8e; strong scaling) instead of one stream per rank")
+    ap.add_argument("--allow-wrap", action="store_true",
+                    help="more ranks than visible GPUs: wrap them onto the devices (one-GPU rehearsals only; the "
+                         "line's n_gpus then counts distinct devices)")
     ap.add_argument("--cpu-samples", type=int, default=4_096_000, help="complex samples per CPU stream")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall time per CPU leg")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "fe_pmc_traffic.json"),
@@ -258,19 +261,51 @@ def split_range(n_total: int, ws: int, rank: int, halo: int, step: int = 50):
     return max(0, s0 - halo), s0, s1
 
 
-def device_for(local: int) -> int:
-    """GPU of this rank: LOCAL_RANK (one process per GPU); ranks beyond the visible devices
-    wrap around (a multi-process rehearsal on a one-GPU box)."""
-    import rtsdr
-    n = rtsdr.device_count()
-    return local % n if n > 0 else local
+def device_for(local: int, allow_wrap: bool = False, count: int | None = None) -> int:
+    """GPU of this rank: LOCAL_RANK (one process per GPU).  More ranks than visible devices is
+    refused (a line must not claim N GPUs that did not run) unless --allow-wrap, which wraps
+    the ranks onto the devices for a multi-process rehearsal on a one-GPU box."""
+    if count is None:
+        import rtsdr
+        count = rtsdr.device_count()
+    if count <= 0:
+        raise SystemExit("bench: no GPU visible (sdr_device_count = 0)")
+    if local >= count and not allow_wrap:
+        raise SystemExit(f"bench: LOCAL_RANK {local} but only {count} device(s) visible; refusing to wrap ranks "
+                         "onto shared devices (--allow-wrap for a one-GPU rehearsal)")
+    return local % count
+
+
+def device_map(ws: int, rank: int, mine: dict) -> list:
+    """Every rank's device (index and PCI bus id), gathered over gloo (rank order)."""
+    mine = dict(mine, rank=rank)
+    if ws == 1:
+        return [mine]
+    import torch.distributed as dist
+    out = [None] * ws
+    dist.all_gather_object(out, mine)
+    return out
+
+
+def check_devices(dmap: list, allow_wrap: bool) -> int:
+    """Distinct physical devices among the ranks (by PCI bus id); refuses a run whose ranks
+    share a device unless allow_wrap."""
+    distinct = len({d["pci_bus_id"] for d in dmap})
+    if distinct < len(dmap) and not allow_wrap:
+        raise SystemExit(f"bench: {len(dmap)} ranks ran on {distinct} distinct device(s) "
+                         f"({[d['pci_bus_id'] for d in dmap]}); refusing (--allow-wrap for a rehearsal)")
+    return distinct
 
 
 def main():
     args = parse()
     ws, rank, local = dist_setup(args)
-    local = device_for(local)
+    local = device_for(local, args.allow_wrap)
     os.environ["SDR_DEVICE"] = str(local)
+    import rtsdr
+    dmap = device_map(ws, rank, rtsdr.device_info(local))
+    args.devices = {"distinct": check_devices(dmap, args.allow_wrap), "ranks": ws,
+                    "map": [{"rank": d["rank"], "device": d["device"], "pci_bus_id": d["pci_bus_id"]} for d in dmap]}
     if args.workload == "c5" and args.span > 1:
         return run_c5_span(args, ws, rank, local)
     if args.workload != "mono":
@@ -391,7 +426,8 @@ def main():
             "metric": METRIC,
             "value": round(total / elapsed / 1e6, 1),
             "unit": "MS/s",
-            "n_gpus": ws,
+            "n_gpus": args.devices["distinct"],
+            "devices": args.devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -418,14 +454,16 @@ def main():
         }
     if rank == 0:
         # the measured ceilings beside the kernel: a copy (read + write) and a read-only stream
-        # (the FE reads 8 B per complex sample and writes 0.04 B); frac_of_copy is against the
-        # higher of the two
+        # (the FE reads 8 B per complex sample and writes 0.04 B).  frac_of_copy_kernel: against
+        # the copy (rounds 1-2's field, comparable across rounds); frac_of_stream_ceiling:
+        # against the higher of the two (the practical ceiling of a read-mostly kernel)
         cbw = copy_bandwidth(lib, h)
         rbw = copy_bandwidth(lib, h, read_only=True)
         ceil = max([v for v in (cbw, rbw) if v] or [0.0])
         result["roofline"]["copy_kernel_gbs"] = cbw
         result["roofline"]["read_stream_gbs"] = rbw
-        result["roofline"]["frac_of_copy"] = round(achieved / ceil, 4) if ceil else None
+        result["roofline"]["frac_of_copy_kernel"] = round(achieved / cbw, 4) if cbw else None
+        result["roofline"]["frac_of_stream_ceiling"] = round(achieved / ceil, 4) if ceil else None
     if ws == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, rf_b, au_b)
     elif rank == 0:
@@ -435,11 +473,17 @@ def main():
         # the other configurations, measured in the same run (same box, same clock): C5 at its
         # per-GPU shapes (8 streams and 1 stream, >= 256 blocks per stream) and the u8 FE + mono
         del d_iq, d_dm, d_au
+        cpu = ws == 1 and not args.no_cpu and rank == 0
         extras = {
-            "c5": c5_measure(ctx, 8, 256, 5, 2, rank, ws, cpu=(ws == 1 and not args.no_cpu and rank == 0),
-                             args=args),
+            "c5": c5_measure(ctx, 8, 256, 5, 2, rank, ws, cpu=cpu, args=args),
             "c5_1stream": c5_measure(ctx, 1, 256, 10, 2, rank, ws),
             "u8": u8_measure(ctx, 128, 50, 10, rank),
+            # configs[2] / [3] at fmMonoBlock.py's 51 200-sample blocks: the per-block drop-in path
+            # (host buffers, PCIe-inclusive), and configs[3] as a device-resident span
+            "c3": rx_measure(ctx, "c3", args, rank, ws, 200, 10, cpu=cpu),
+            "c4": rx_measure(ctx, "c4", args, rank, ws, 200, 10, cpu=cpu),
+            "c4_span": c5_measure(ctx, 1, 300, 10, 2, rank, ws, cpu=cpu, args=args, B=51_200, rds=False, u8=False,
+                                  rf_taps=args.taps),
         }
         cb = extras["c5"].get("cpu_baseline")
         if cb is not None:                       # the CPU leg runs one stream per host thread either way
@@ -508,16 +552,30 @@ def ref_rx_baseline(args, iq_blocks, B, u8, stereo, rds, rf_taps):
 
 
 def run_rx(args, ws, rank, local):
-    """c3 / c4 (per-block drop-in path, host buffers) and c5 (multi-stream, device-resident)."""
-    import rtsdr
+    """--workload c3 / c4 / c5 --span 1: one JSON line."""
     from importlib import import_module
     _lib = import_module("real-time-software-defined-radio_amd._lib")
     ctx = _lib.Context(local)
-    c5 = args.workload == "c5"
+    result = rx_measure(ctx, args.workload, args, rank, ws, args.steps, args.warmup,
+                        cpu=(ws == 1 and not args.no_cpu and rank == 0))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def rx_measure(ctx, workload, args, rank, ws, steps, warmup, cpu=False):
+    """c3 / c4 (per-block drop-in path, host buffers) and c5 (multi-stream, device-resident,
+    one block per call): the result dict (rank 0; None elsewhere)."""
+    import rtsdr
+    from importlib import import_module
+    _lib = import_module("real-time-software-defined-radio_amd._lib")
+    c5 = workload == "c5"
     B = 153_600 if c5 else 51_200
     S = args.streams if c5 else 1
     u8 = c5
-    stereo = args.workload in ("c4", "c5")
+    stereo = workload in ("c4", "c5")
     rds = c5
     rf_taps = 151 if c5 else args.taps
     rf_b, au_b = rtsdr.design.mono_coeffs(rf_taps, args.audio_taps)
@@ -550,7 +608,7 @@ def run_rx(args, ws, rank, local):
             if not pipe:
                 return sync_step(k)
             return rx.submit(host[k % nres], fetch=fetch)
-    for k in range(args.warmup):
+    for k in range(warmup):
         step(k)
     if not c5:
         rx.flush()
@@ -572,7 +630,7 @@ def run_rx(args, ws, rank, local):
     sync = None
     if not c5 and pipe:                      # the synchronous drop-in call, for its latency
         sl = []
-        for k in range(args.steps):
+        for k in range(steps):
             t = time.perf_counter()
             sync_step(k)
             sl.append(time.perf_counter() - t)
@@ -591,11 +649,11 @@ def run_rx(args, ws, rank, local):
         tm = _lib.Timer(ctx)
         e0, e1 = tm.event(), tm.event()
         tm.record(e0)
-        for k in range(args.steps):
+        for k in range(steps):
             step(k)
         tm.record(e1)
     else:
-        for k in range(args.steps):
+        for k in range(steps):
             t = time.perf_counter()
             step(k)
             lat.append(time.perf_counter() - t)
@@ -603,11 +661,11 @@ def run_rx(args, ws, rank, local):
     ctx.synchronize()
     barrier(ws)
     elapsed = max_over_ranks(ws, time.perf_counter() - t0)
-    gpu_ms = tm.elapsed_ms(e0, e1) / args.steps if c5 else None
+    gpu_ms = tm.elapsed_ms(e0, e1) / steps if c5 else None
     pll = rx.pll_stats() if stereo else None
     result = None
     if rank == 0:
-        total = S * B * args.steps * ws
+        total = S * B * steps * ws
         M = B // 10
         dom = max(stage_ms, key=stage_ms.get)
         # the front end is the HBM-streaming kernel of the chain: IQ in + demod out per launch
@@ -624,9 +682,10 @@ def run_rx(args, ws, rank, local):
             dom_bound = "stage FIRs: FP32 VALU multiply-adds"
         result = {
             "metric": f"IQ MSamples/s through the {'multi-stream mono+stereo+RDS receiver' if c5 else 'per-block drop-in path'}"
-                      f" ({args.workload}); achieved HBM GB/s vs peak",
-            "value": round(total / elapsed / 1e6, 1), "unit": "MS/s", "n_gpus": ws, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+                      f" ({workload}); achieved HBM GB/s vs peak",
+            "value": round(total / elapsed / 1e6, 1), "unit": "MS/s", "n_gpus": args.devices["distinct"],
+            "devices": args.devices, "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": (f"synthetic FM IQ (seed = rank*streams + stream), interleaved {'u8' if u8 else 'f32'}, "
                      + ("device-resident, 16 distinct blocks per stream cycled" if c5 else
@@ -634,7 +693,7 @@ def run_rx(args, ws, rank, local):
             "config": {"workload": {"c3": "configs[2]: FE + mono per block, fmMonoBlock.py block size",
                                     "c4": "configs[3]: FE + mono + stereo per block, fmMonoBlock.py block size",
                                     "c5": "configs[4]: independent streams, mono + stereo + RDS to the RRC output"}
-                       [args.workload],
+                       [workload],
                        "block_complex": B, "streams_per_gpu": S, "rf_taps": rf_taps, "iq": "u8" if u8 else "f32",
                        "parallelism": f"independent streams x{S * ws}",
                        "pipeline": " + ".join(
@@ -669,17 +728,13 @@ def run_rx(args, ws, rank, local):
             if sync is not None:
                 result["sync"] = sync
             result["realtime_factor"] = round((total / elapsed) / 2.4e6, 1)     # x the 2.4 MS/s input rate
-    if ws == 1 and not args.no_cpu and rank == 0:
+    if cpu and rank == 0:
         result["cpu_baseline"] = ref_rx_baseline(args, host[:, 0].reshape(-1), B, u8, stereo, rds, rf_taps)
     elif rank == 0:
         result["cpu_baseline"] = None
-    if rank == 0:
-        print(json.dumps(result), flush=True)
     rx.close()
     rx_sync.close()
-    if ws > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    return result
 
 C5_B = 153_600                 # complex samples per reference block (src/fm_radio.cpp:23)
 VALU_PEAK_TFLOPS = 157.3       # MI355X FP32 vector peak (MI355X_MICROARCH.md)
@@ -697,24 +752,29 @@ def chain_flops_per_sample(rf_taps=151, taps=151, audio_decim=5, up=19, down=80)
     return 2.0 * (2 * rf_taps + macs_demod) / 10.0
 
 
-def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, args=None):
+def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, args=None, B=None, stereo=True,
+               rds=True, u8=True, rf_taps=151):
     """configs[4] per GPU: S independent u8 streams of K reference blocks each, device-resident,
     mono + stereo + RDS to the RRC output, K blocks of every stream per receiver call (one
     span: the time-parallel receiver).  The synthetic span is K x 64 ms, over
     which every tone of the composite completes whole cycles, so repeating it is seamless
-    (the PLLs stay locked across steps); stream s is the span rotated by s/S of its length."""
+    (the PLLs stay locked across steps); stream s is the span rotated by s/S of its length.
+    Also the span form of configs[3] (c4_span: B = 51 200 f32, stereo without RDS; K chosen
+    so that the span is a whole number of every tone's cycles too)."""
     import rtsdr
     from importlib import import_module
     _lib = import_module("real-time-software-defined-radio_amd._lib")
-    rf_b, au_b = rtsdr.design.mono_coeffs(151, 151)
-    n = K * C5_B
-    base = rtsdr.synth.fm_iq(n, seed=rank * 1009, dtype=np.uint8)
+    B = C5_B if B is None else B
+    rf_b, au_b = rtsdr.design.mono_coeffs(rf_taps, 151)
+    n = K * B
+    dt = np.uint8 if u8 else np.float32
+    base = rtsdr.synth.fm_iq(n, seed=rank * 1009, dtype=dt)
     rows = np.stack([np.roll(base, 2 * ((s * n // S) // 50 * 50)) for s in range(S)])
     del base
     d_iq = _lib.DeviceBuffer.from_array(ctx, rows)
-    cpu_rows = rows[0, :16 * 2 * C5_B].copy() if cpu else None
+    cpu_rows = rows[0, :16 * 2 * B].copy() if cpu else None
     del rows
-    rx = rtsdr.Receiver(S, n, stereo=True, rds=True, iq_dtype=np.uint8, rf_coeff=rf_b, audio_coeff=au_b,
+    rx = rtsdr.Receiver(S, n, stereo=stereo, rds=rds, iq_dtype=dt, rf_coeff=rf_b, audio_coeff=au_b,
                         pipeline=pipeline, ctx=ctx)
 
     def step():
@@ -740,31 +800,43 @@ def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, arg
     barrier(ws)
     elapsed = max_over_ranks(ws, time.perf_counter() - t0)
     pll = rx.pll_stats()
+    # one call on its own (nothing else in flight): the latency of a span, next to the
+    # pipelined throughput above
+    t1 = time.perf_counter()
+    step()
+    ctx.synchronize()
+    latency = time.perf_counter() - t1
     rx.close()
     d_iq.free()
     total = S * n * steps * ws
-    fps = chain_flops_per_sample()
-    per_gpu_tflops = fps * S * n * steps / elapsed / 1e12
+    fps = chain_flops_per_sample() if rds else None
     dom = max(stage_ms, key=stage_ms.get)
     out = {
         "value": round(total / elapsed / 1e6, 1), "unit": "MS/s",
         "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps, "warmup": warmup,
-        "config": {"streams_per_gpu": S, "blocks_per_stream_per_step": K, "block_complex": C5_B,
-                   "complex_per_step": S * n, "iq": "u8", "rf_taps": 151, "pipeline": bool(pipeline),
-                   "chain": "FE + mono + stereo + RDS to the RRC output (fmMonoBlock.py:80-173, fmRDSblock.py:127-204)"},
+        "mode": (f"span: {K} blocks of every stream per receiver call, device-resident (pipelined calls); not the "
+                 f"per-block real-time loop -- one call covers {K * B / 2.4e6:.2f} s of radio"),
+        "ms_per_call": round(elapsed / steps * 1e3, 4), "call_latency_ms": round(latency * 1e3, 4),
+        "config": {"streams_per_gpu": S, "blocks_per_stream_per_step": K, "block_complex": B,
+                   "complex_per_step": S * n, "iq": "u8" if u8 else "f32", "rf_taps": rf_taps,
+                   "pipeline": bool(pipeline),
+                   "chain": ("FE + mono + stereo + RDS to the RRC output (fmMonoBlock.py:80-173, fmRDSblock.py:127-204)"
+                             if rds else "FE + mono + stereo (fmMonoBlock.py:80-173)")},
         "stage_ms": stage_ms,
         "dominant_stage": {"stage": dom, "ms": stage_ms[dom],
                            "bound": ("PLL: pseudo-blocks solved in parallel from warm-up guesses and chained "
                                      "(f64, csrc/pll.hip long calls)") if dom == "pll" else
-                           ("HBM: u8 IQ in, demod out" if dom == "fe" else "FP32 VALU: FIR multiply-adds")},
-        "roofline": {"bound": "valu", "achieved": round(per_gpu_tflops, 3), "peak": VALU_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(per_gpu_tflops / VALU_PEAK_TFLOPS, 4), "traffic": None,
-                     "flops_per_sample": round(fps, 2),
-                     "note": "FIR flops of the whole chain per input sample x samples / wall time per GPU"},
+                           ("HBM: IQ in, demod out" if dom == "fe" else "FP32 VALU: FIR multiply-adds")},
         "pll_solver": pll,
     }
+    if fps is not None:
+        per_gpu_tflops = fps * S * n * steps / elapsed / 1e12
+        out["roofline"] = {"bound": "valu", "achieved": round(per_gpu_tflops, 3), "peak": VALU_PEAK_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(per_gpu_tflops / VALU_PEAK_TFLOPS, 4), "traffic": None,
+                           "flops_per_sample": round(fps, 2),
+                           "note": "FIR flops of the whole chain per input sample x samples / wall time per GPU"}
     if cpu and args is not None:
-        out["cpu_baseline"] = ref_rx_baseline(args, cpu_rows, C5_B, True, True, True, 151)
+        out["cpu_baseline"] = ref_rx_baseline(args, cpu_rows, B, u8, stereo, rds, rf_taps)
     return out
 
 
@@ -830,7 +902,8 @@ def run_c5_span(args, ws, rank, local):
     if rank == 0:
         result = {"metric": "IQ MSamples/s through the multi-stream mono+stereo+RDS receiver (c5); "
                             "FIR TFLOP/s vs FP32 VALU peak",
-                  "value": m["value"], "unit": "MS/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+                  "value": m["value"], "unit": "MS/s", "n_gpus": args.devices["distinct"], "devices": args.devices,
+                  "steps": args.steps, "warmup": args.warmup,
                   "ms_per_step": m["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                   "dtype": "f32",
                   "data": "synthetic FM IQ (u8), device-resident, one seamless span per stream repeated",

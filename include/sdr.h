@@ -57,6 +57,9 @@ typedef struct sdr_ctx sdr_ctx;
 int sdr_abi_version(void);
 const char* sdr_last_error(void);
 int sdr_device_count(int* n);
+/* Which physical GPU `device` is (bench.py's multi-rank line proves its rank -> device map
+ * with it): its PCI bus id ("dddd:bb:dd.f", NUL-terminated into pci[len]) and compute units. */
+int sdr_device_info(int device, char* pci, int len, int* cus);
 int sdr_create(int device, sdr_ctx** out);
 void sdr_destroy(sdr_ctx* ctx);
 int sdr_synchronize(sdr_ctx* ctx);

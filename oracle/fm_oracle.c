@@ -125,3 +125,41 @@ void orc_fe_mono_streams(const float* iq, int64_t n, int64_t stride, int nstream
   for (int s = 0; s < nstreams; ++s)
     orc_fe_mono(iq + 2 * (int64_t)s * stride, n, rf_b, T, au_b, TA, NULL, audio_out + (int64_t)s * audio_stride);
 }
+
+/* fmPll (model/fmPll.py:4-46), restated operation for operation as oracle/fm_oracle.py::fm_pll
+ * (Python's float arithmetic and the same libm atan2 / cos / sin: no contraction, so the
+ * results are bit-identical -- tests/test_oracle.py::test_c_oracle_pll).  state: the 6-list
+ * [integrator, phaseEst, feedbackI, feedbackQ, ncoOut[0], trigOffset], updated in place.
+ * nco / ncoq: n + 1 values (ncoq may be NULL); ncoq[0] as fm_pll defines it. */
+__attribute__((optimize("fp-contract=off")))
+void orc_pll(const double* x, int64_t n, double freq, double fs, double scale, double adj, double bw,
+             double* state, double* nco, double* ncoq) {
+  /* called through pointers: the compiler would otherwise merge cos(a) and sin(a) into one
+   * sincos() call, whose results differ from the separate calls Python makes in the last bit */
+  double (*volatile vcos)(double) = cos;
+  double (*volatile vsin)(double) = sin;
+  double (*volatile vatan2)(double, double) = atan2;
+  const double Kp = bw * 2.666;
+  const double Ki = bw * bw * 3.555;
+  double integ = state[0], phase = state[1], fI = state[2], fQ = state[3];
+  const double off = state[5];
+  const double w = 2 * M_PI * (freq / fs);
+  nco[0] = state[4];
+  if (ncoq) ncoq[0] = off > 0 ? vsin((w * off + phase) * scale + adj) : 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    const double e = vatan2(x[k] * (-fQ), x[k] * (+fI));
+    integ = integ + Ki * e;
+    phase = phase + Kp * e + integ;
+    const double arg = w * (off + (double)k + 1) + phase;
+    fI = vcos(arg);
+    fQ = vsin(arg);
+    nco[k + 1] = vcos(arg * scale + adj);
+    if (ncoq) ncoq[k + 1] = vsin(arg * scale + adj);
+  }
+  state[0] = integ;
+  state[1] = phase;
+  state[2] = fI;
+  state[3] = fQ;
+  state[4] = nco[n];
+  state[5] = off + (double)n;
+}

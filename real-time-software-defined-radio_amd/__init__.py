@@ -16,7 +16,8 @@ RdsBlockProcessor.  See DESIGN.md and INTEGRATION.md.
 """
 from . import design, synth  # noqa: F401
 from ._lib import (SDR_IQ_F32, SDR_IQ_U8, SDR_PRE_MIX, SDR_PRE_NONE, SDR_PRE_SQUARE, Context,  # noqa: F401
-                   DeviceBuffer, SdrError, SdrUnavailable, Timer, device_count, get_context, load_library)
+                   DeviceBuffer, SdrError, SdrUnavailable, Timer, device_count, device_info, get_context,
+                   load_library)
 from .blocks import MonoBlockProcessor, RdsBlockProcessor, RdsLinkLayer, Receiver, StereoBlockProcessor  # noqa: F401
 from .design import impulseResponseRootRaisedCosine, my_filterImpulseResponse  # noqa: F401
 from .dsp import (DFT, MonoState, estimatePSD, fm_mono_range, fm_mono_streams, split_halo, fmDemodArctan, fmPll, lfilter, lfilter_decim,  # noqa: F401

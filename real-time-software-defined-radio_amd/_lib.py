@@ -49,6 +49,7 @@ SIGNATURES = {
     "sdr_abi_version": (_i32, []),
     "sdr_last_error": (_c.c_char_p, []),
     "sdr_device_count": (_i32, [_c.POINTER(_i32)]),
+    "sdr_device_info": (_i32, [_i32, _c.c_char_p, _i32, _c.POINTER(_i32)]),
     "sdr_create": (_i32, [_i32, _c.POINTER(_vp)]),
     "sdr_destroy": (None, [_vp]),
     "sdr_synchronize": (_i32, [_vp]),
@@ -163,6 +164,15 @@ def device_count() -> int:
     n = _i32(0)
     rc = lib.sdr_device_count(_c.byref(n))
     return n.value if rc == SDR_OK else 0
+
+
+def device_info(device: int) -> dict:
+    """The physical GPU behind a device index (sdr_device_info): PCI bus id and CUs."""
+    lib = load_library()
+    buf = _c.create_string_buffer(64)
+    cus = _i32(0)
+    check(lib.sdr_device_info(int(device), buf, 64, _c.byref(cus)), "sdr_device_info")
+    return {"device": int(device), "pci_bus_id": buf.value.decode(), "cus": cus.value}
 
 
 class Context:

@@ -176,6 +176,23 @@ int sdr_device_count(int* n) {
   return SDR_OK;
 }
 
+int sdr_device_info(int device, char* pci, int len, int* cus) {
+  int n = 0;
+  TRY(sdr_device_count(&n));
+  if (device < 0 || device >= n) return fail(SDR_EINVAL, "device %d not in [0, %d)", device, n);
+  if (pci != nullptr && len > 0) {
+    const hipError_t e = hipDeviceGetPCIBusId(pci, len, device);
+    if (e != hipSuccess) return fail(SDR_EHIP, "hipDeviceGetPCIBusId(%d): %s", device, hipGetErrorString(e));
+  }
+  if (cus != nullptr) {
+    hipDeviceProp_t prop;
+    const hipError_t e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return fail(SDR_EHIP, "hipGetDeviceProperties(%d): %s", device, hipGetErrorString(e));
+    *cus = prop.multiProcessorCount;
+  }
+  return SDR_OK;
+}
+
 int sdr_create(int device, sdr_ctx** out) {
   if (out == nullptr) return fail(SDR_EINVAL, "out is NULL");
   *out = nullptr;

@@ -1189,17 +1189,7 @@ void fe_slot_kernel(FeParams p, TapsF32 taps, SlotArgs a) {
 // ------------------------------------------------------------------------------
 // Host-side launchers (called by capi.hip)
 // ------------------------------------------------------------------------------
-static int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-      n = prop.multiProcessorCount;
-    if (n <= 0) n = 256;
-  }
-  return n;
-}
+static int cu_count() { return device_cus(); }
 
 // Resident workgroups per CU for a kernel (the persistent grid must be fully resident
 // for its tiles to be spread evenly; any excess would run as a second, serial round).
@@ -1281,7 +1271,12 @@ static bool fe_mfma_enabled() {
 hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st) {
   if (a.D != 10) return hipErrorInvalidValue;
   // u8 IQ: the RF FIR on the int8 matrix cores where it covers the call (fe_mfma.hip)
-  if (a.u8 && fe_mfma_enabled() && sdr_launch_fe_mfma(a, st) == hipSuccess) return hipSuccess;
+  // (hipErrorInvalidValue: a call it does not cover, which the vector kernels take; any other
+  // error is a failed launch and is returned, not retried on a different arithmetic path)
+  if (a.u8 && fe_mfma_enabled()) {
+    const hipError_t em = sdr_launch_fe_mfma(a, st);
+    if (em != hipErrorInvalidValue) return em;
+  }
   switch (a.T) {
     case 101: return launch_fe_t<101>(a, st);
     case 151: return launch_fe_t<151>(a, st);

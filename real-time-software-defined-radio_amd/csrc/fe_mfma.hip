@@ -730,14 +730,12 @@ hipError_t launch_demod_mfma_t(const FeLaunch& a, hipStream_t st) {
   p.last_phi = a.last_phi;
   p.wraps = a.wraps;
   p.vec_out = ((a.out_stride % 4) == 0 && ((uintptr_t)a.demod % 16) == 0) ? 1 : 0;
-  static int slots = 0;
-  if (slots == 0) {
-    int dev = 0, per = 0, cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+  static std::atomic<int> slot_cache[kMaxDevices];
+  const int slots = per_device(slot_cache, [] {
+    int per = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_demod_kernel<T>, 64, 0) != hipSuccess || per <= 0) per = 1;
-    slots = cus * std::min(per, 12);
-  }
+    return device_cus() * std::min(per, 12);
+  });
   // the resident waves share the tiles in runs of >= 2 (a run's warm-up tile is at most a third of
   // its work; at span sizes, 1/60)
   const int64_t run = std::max<int64_t>(2, (p.total + slots - 1) / slots);
@@ -819,17 +817,15 @@ hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps_rev, in
   p.argev = ataps_rev;
   p.audio = audio;
   p.audio_stride = audio_stride;
-  static int slots = 0;
-  if (slots == 0) {
-    int dev = 0, per = 0;
-    hipDeviceProp_t prop;
-    int cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+  static std::atomic<int> slot_cache[kMaxDevices];
+  const int slots = per_device(slot_cache, [] {
+    int per = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_mono_kernel, 64, 0) != hipSuccess || per <= 0) per = 1;
     int cap = 12;
     if (const char* e = std::getenv("SDR_FE_MFMA_WPC")) cap = std::max(1, std::atoi(e));   // waves per CU (A/B)
-    slots = cus * std::min(per, cap);
-  }
+    return device_cus() * std::min(per, cap);
+  });
+
   const int64_t grid = std::min<int64_t>(slots, p.total);
   hipLaunchKernelGGL(fe_mfma_mono_kernel, dim3((unsigned)grid), dim3(64), 0, st, p);
   return hipGetLastError();

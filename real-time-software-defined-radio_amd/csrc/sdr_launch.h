@@ -3,11 +3,38 @@
 // translation-unit boundary: each .hip file includes this header, so a field change is a
 // compile error everywhere instead of a silent ODR mismatch.
 #pragma once
+#include <atomic>
 #include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "sdr_common.h"
+
+// Launch geometry that depends on the device, cached per device (a process may hold contexts
+// on GPUs with different CU counts, from several threads): `query` runs for the current
+// device the first time, and every thread that races it there stores the same value.
+constexpr int kMaxDevices = 64;
+template <class Q>
+inline int per_device(std::atomic<int> (&cache)[kMaxDevices], Q query) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return query();
+  int v = cache[dev].load(std::memory_order_relaxed);
+  if (v == 0) {
+    v = query();
+    cache[dev].store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+// the current device's compute units (256 if the query fails)
+inline int device_cus() {
+  static std::atomic<int> cache[kMaxDevices];
+  return per_device(cache, [] {
+    int dev = 0, n = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) n = prop.multiProcessorCount;
+    return n > 0 ? n : 256;
+  });
+}
 
 // RF front end (fe.hip): interleaved IQ -> FIR + decimate -> atan2 discriminator.
 struct FeLaunch {

@@ -108,3 +108,66 @@ def test_two_rank_split_stream_ranges_gather_to_the_whole_pass():
     assert s0a == 0 and s1a == s0b and s1b == 6 * 51200 + 7 and w0b < s0b
     assert res["n"] == res["n_want"]
     assert res["maxdiff"] < 1e-12, res
+
+
+def test_device_for_refuses_to_wrap():
+    """A line must not claim N GPUs that did not run: more ranks than visible devices is
+    refused unless --allow-wrap (one-GPU rehearsals), which wraps the ranks."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import pytest
+    assert bench.device_for(1, count=2) == 1
+    with pytest.raises(SystemExit):
+        bench.device_for(3, count=2)
+    assert bench.device_for(3, allow_wrap=True, count=2) == 1
+    with pytest.raises(SystemExit):
+        bench.device_for(0, count=0)
+
+
+DEVMAP_WORKER = r"""
+import os, sys, json
+sys.path.insert(0, os.environ["ROOT"])
+import bench
+class A: pass
+ws, rank, local = bench.dist_setup(A())
+shared = os.environ["SHARED"] == "1"
+pci = "0000:05:00.0" if shared else f"0000:{5 + rank:02x}:00.0"
+dmap = bench.device_map(ws, rank, {"device": local, "pci_bus_id": pci, "cus": 256})
+res = {"rank": rank, "map": dmap}
+try:
+    res["distinct"] = bench.check_devices(dmap, allow_wrap=False)
+except SystemExit as e:
+    res["refused"] = str(e)
+res["wrapped"] = bench.check_devices(dmap, allow_wrap=True)
+import torch.distributed as dist
+print(json.dumps(res), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def _run2(worker, extra):
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, ROOT=ROOT, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **extra)
+        procs.append(subprocess.Popen([sys.executable, "-c", worker], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+    import json
+    return sorted((json.loads(o.strip().splitlines()[-1]) for o, _ in outs), key=lambda d: d["rank"])
+
+
+def test_two_rank_device_map():
+    """bench.py's rank -> device map, gathered over gloo: two ranks on two devices report 2
+    distinct; two ranks on ONE device (a misconfigured node) are refused unless wrapping was
+    asked for, in which case the line counts 1 device."""
+    res = _run2(DEVMAP_WORKER, {"SHARED": "0"})
+    for d in res:
+        assert d["distinct"] == 2 and [m["rank"] for m in d["map"]] == [0, 1]
+        assert [m["pci_bus_id"] for m in d["map"]] == ["0000:05:00.0", "0000:06:00.0"]
+    res = _run2(DEVMAP_WORKER, {"SHARED": "1"})
+    for d in res:
+        assert "refused" in d and "distinct" not in d and d["wrapped"] == 1

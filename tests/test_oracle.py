@@ -163,3 +163,29 @@ def test_c_oracle_fe_mono(liboracle, golden, oracle):
                           np.ascontiguousarray(au_b), 151, dm, au)
     assert maxabs(dm, g["demod"]) < 1e-11
     assert maxabs(au, g["audio"]) < 1e-11
+
+
+def test_c_oracle_pll(oracle, golden):
+    """orc_pll (oracle/fm_oracle.c) == fm_pll bit for bit -- the same restatement of
+    model/fmPll.py:4-46 in C, used to run the oracle over hundreds of blocks
+    (tests/test_span.py's bench-shape check) -- on the golden PLL fixture (chained calls,
+    the stereo loop) and on the RDS loop's configuration (fmRDSblock.py:167)."""
+    subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    u = golden("units.npz")
+    x = u["pll_in"]
+    for cfg in ((19e3, 240e3, 2.0, 0.0, 0.01), (114e3, 240e3, 0.5, np.pi / 3.3 - np.pi / 1.5, 0.001)):
+        st_p, st_c = [0.0, 0.0, 1.0, 0.0, 1.0, 0.0], [0.0, 0.0, 1.0, 0.0, 1.0, 0.0]
+        for a, b in ((0, 700), (700, 1701), (1701, len(x))):
+            ra = oracle.fm_pll(x[a:b], cfg[0], cfg[1], st_p, cfg[2], cfg[3], cfg[4])
+            rb = oracle.fm_pll_c(x[a:b], cfg[0], cfg[1], st_c, cfg[2], cfg[3], cfg[4])
+            assert np.array_equal(ra[0], rb[0]) and np.array_equal(ra[1], rb[1]) and ra[2] == rb[2]
+            st_p, st_c = ra[2], rb[2]
+    # and against the fixture itself (the reference's own fmPll, chained as test_pll_chained_calls)
+    st = [0.0, 0.0, 1.0, 0.0, 1.0, 0.0]
+    cuts = [0] + [len(u[f"pll{j}_nco"]) - 1 for j in range(2)]
+    a = 0
+    for j in range(2):
+        b = a + cuts[j + 1]
+        nco, ncoq, st = oracle.fm_pll_c(x[a:b], 19e3, 240e3, st, 2)
+        assert maxabs(nco, u[f"pll{j}_nco"]) < 1e-12 and maxabs(ncoq, u[f"pll{j}_ncoq"]) < 1e-12
+        a = b

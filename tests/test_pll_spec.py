@@ -120,3 +120,22 @@ def test_pll_long_call_zero_inputs(sdr, gpu_ctx, oracle):
     assert err < NCO_TOL
     s = gpu_ctx.pll_stats()
     assert s["recurrences"] == long_blocks(n) and s["sequential"] >= 2, s
+
+
+@pytest.mark.parametrize("offset,noise", [(40.0, 0.8), (7.0, 0.3)])
+def test_pll_long_call_unlocked(sdr, gpu_ctx, oracle, offset, noise):
+    """Long calls on a loop that is NOT locked (a weak, 40 Hz-off pilot in heavy noise; a
+    noisy 7 Hz offset): the pre-roll guesses are wrong, so the chain stops, hands pseudo-blocks
+    their exact (chained) starts for re-solves in later rounds, and whatever the rounds leave
+    runs sequentially from the chain's exact position.  Those hand-overs are the riskiest part
+    of the long-call solver: NCO and carried state must still equal the oracle's (model/fmPll.py
+    :4-46) over three chained calls, and the counters must show the non-trivial paths ran."""
+    n = 4 * 16384 + 5
+    x = pilot(3 * n, 19e3 + offset, seed=int(offset), noise=noise)
+    err = chained(sdr, oracle, x, [(0, n), (n, 2 * n), (2 * n, 3 * n)], 19e3, 2.0)
+    assert err < NCO_TOL
+    s = gpu_ctx.pll_stats()
+    print(f"offset {offset} noise {noise} solver counters:", s)
+    nb = long_blocks(n)
+    assert s["recurrences"] == 3 * nb, s
+    assert s["long_stops"] + s["long_tail"] + s["sequential"] + s["spec_r1"] + s["spec_r2"] > 0, s

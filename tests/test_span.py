@@ -86,3 +86,74 @@ def test_span_receiver_equals_block_loop_and_oracle(sdr, gpu_ctx, oracle):
             scale = max(float(np.max(np.abs(want))), 1e-3)
             em, er = maxabs(got[key][0], want) / scale, rms(got[key][0], want) / scale
             assert em < tmax and er < trms, (key, sp, em, er)
+
+
+def test_span_bench_shape_matches_block_loop_and_oracle(sdr, gpu_ctx, oracle):
+    """The exact shape bench.py's c5_1stream leg times: ONE u8 stream, spans of K = 256 blocks
+    (3.9 M PLL steps per recurrence: 275 pseudo-blocks chained, the RDS loop's linear
+    acceptance and the NCO's linear response over the whole span), two spans in a row.
+    Checked against (a) the per-block receiver over all 512 blocks (the reference's block
+    loop) at SPAN_REL, and (b) the oracle (model/fmMonoBlock.py:80-173,
+    model/fmRDSblock.py:127-204, run over all 512 blocks with the C restatement of fmPll,
+    bit-identical to the Python one) on the first two and last two blocks of each span; the
+    solver counters of the locked span: every pseudo-block solved in parallel in round 0, no
+    chain stop, no sequential tail."""
+    K, spans = 256, 2
+    nblk = K * spans
+    iq = sdr.synth.fm_iq(nblk * B5 + 1, seed=7, dtype=np.uint8)[None, :]
+    kw = dict(stereo=True, rds=True, iq_dtype=np.uint8)
+    span_rx = sdr.Receiver(1, K * B5, **kw)
+    nb = long_blocks(K * (B5 // 10))
+    got, stats = [], []
+    for sp in range(spans):
+        gpu_ctx.pll_stats(reset=True)
+        got.append(span_rx.process(iq[:, 2 * sp * K * B5:2 * (sp + 1) * K * B5], fetch=NAMES))
+        stats.append(span_rx.pll_stats())
+        print(f"span {sp} (K={K}) solver counters:", stats[-1])
+    for sp, st in enumerate(stats):
+        assert st["recurrences"] == 2 * nb and st["long_tail"] == 0, (sp, st)
+    st = stats[1]
+    assert st["spec_r0"] == 2 * nb and st["sequential"] == 0 and st["long_stops"] == 0, st
+    # (a) the per-block receiver over every block of both spans
+    per_rx = sdr.Receiver(1, B5, **kw)
+    M = B5 // 10
+    peak, worst = {}, {}
+    keep = {0, 1, K - 2, K - 1}
+    per_keep = {}
+    for k in range(nblk):
+        p = per_rx.process(iq[:, 2 * k * B5:2 * (k + 1) * B5], fetch=NAMES)
+        sp, kk = divmod(k, K)
+        for name in NAMES:
+            w = p[name][0]
+            n = len(w) - 1 if name in NCO_NAMES else len(w)
+            g = got[sp][name][0][kk * n:kk * n + len(w)]
+            assert g.shape == w.shape, (name, k)
+            worst[name] = max(worst.get(name, 0.0), maxabs(g, w))
+            peak[name] = max(peak.get(name, 0.0), float(np.max(np.abs(w))))
+        if kk in keep:
+            per_keep[k] = {name: p[name][0] for name in NAMES}
+    rel = {name: worst[name] / max(peak[name], 1e-3) for name in NAMES}
+    print("bench-shape span vs block loop, max error relative to peak:", {k: f"{v:.1e}" for k, v in rel.items()})
+    for name in NAMES:
+        assert rel[name] < SPAN_REL[name], (name, rel[name])
+    for a, b in zip(span_rx.state(), per_rx.state()):
+        assert maxabs(a, b) < 1e-6
+    # (b) the oracle on the first two and last two blocks of each span
+    f = (iq[0].astype(np.float64) - 128.0) / 128.0
+    mono = oracle.mono_stereo_blocks(f, B5, rf_taps=151, audio_taps=151, nblocks=nblk, pll_fn=oracle.fm_pll_c)
+    rds = oracle.rds_blocks(iq[0], 2 * B5, taps=151, nblocks=nblk, pll_fn=oracle.fm_pll_c)
+    A = len(mono[0]["audio"])
+    for k in sorted(per_keep):
+        sp, kk = divmod(k, K)
+        g = got[sp]
+        for key in ("audio", "stereo", "left", "right"):
+            gv, want = g[key][0][kk * A:(kk + 1) * A], mono[k][key]
+            assert rms(gv, want) < AUDIO_RMS and maxabs(gv, want) < AUDIO_MAX, (key, k, rms(gv, want))
+        assert maxabs(g["nco"][0][kk * M:kk * M + M + 1], mono[k]["nco"]) < 3e-7, k
+        for key, (tmax, trms) in RDS_TOL.items():
+            want = rds[k][key]
+            n = len(want) - 1 if key in NCO_NAMES else len(want)
+            gv = g[key][0][kk * n:kk * n + len(want)]
+            scale = max(float(np.max(np.abs(want))), 1e-3)
+            em, er = maxabs(gv, want) / scale, rms(gv, want) / scale
+            assert em < tmax and er < trms, (key, k, em, er)
