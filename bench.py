@@ -56,9 +56,10 @@ BLOCK = 1_024_000              # complex samples per block (SURVEY §7 hard part
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=["mono", "c3", "c4", "c5"], default="mono",
+    ap.add_argument("--workload", choices=["mono", "c3", "c4", "c5", "live"], default="mono",
                     help="mono: configs[1]+[2] batched (the headline); c3/c4: per-block drop-in path; "
-                         "c5: multi-stream mono+stereo+RDS")
+                         "c5: multi-stream mono+stereo+RDS; live: fm_radio_gpu end to end (u8 stdin -> int16 "
+                         "stdout) beside the reference's own fm_radio")
     ap.add_argument("--streams", type=int, default=8, help="c5: independent streams per GPU")
     ap.add_argument("--span", type=int, default=256,
                     help="c5: 153 600-sample blocks of every stream processed per receiver call (device-resident "
@@ -85,6 +86,8 @@ def parse():
     ap.add_argument("--split-stream", action="store_true",
                     help="mono: ONE stream of --blocks blocks split over the ranks, each range with a read-only "
                          "halo (SURVEY §8e; strong scaling) instead of one stream per rank")
+    ap.add_argument("--live-repeat", type=int, default=8,
+                    help="live: passes of the --span-block stream in the long run (the short run is one pass)")
     ap.add_argument("--allow-wrap", action="store_true",
                     help="more ranks than visible GPUs: wrap them onto the devices (one-GPU rehearsals only; the "
                          "line's n_gpus then counts distinct devices)")
@@ -306,6 +309,8 @@ def main():
     dmap = device_map(ws, rank, rtsdr.device_info(local))
     args.devices = {"distinct": check_devices(dmap, args.allow_wrap), "ranks": ws,
                     "map": [{"rank": d["rank"], "device": d["device"], "pci_bus_id": d["pci_bus_id"]} for d in dmap]}
+    if args.workload == "live":
+        return run_live(args, ws, rank, local)
     if args.workload == "c5" and args.span > 1:
         return run_c5_span(args, ws, rank, local)
     if args.workload != "mono":
@@ -917,6 +922,108 @@ def run_c5_span(args, ws, rank, local):
         import torch.distributed as dist
         dist.destroy_process_group()
 
+
+def live_run(cmd, data: bytes, repeat: int, env=None):
+    """One live-receiver process: `data` written `repeat` times to its stdin (as rtl_sdr would
+    pipe it), stdout discarded (the int16 stream is counted), stderr kept.  Returns (wall
+    seconds from process start to exit, stdout bytes, stderr text, return code)."""
+    import subprocess
+    import threading
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)
+    nout = [0]
+    err = []
+
+    def feed():
+        try:
+            for _ in range(repeat):
+                p.stdin.write(data)
+            p.stdin.close()
+        except BrokenPipeError:
+            pass
+
+    def drain_out():
+        while True:
+            b = p.stdout.read(1 << 20)
+            if not b:
+                break
+            nout[0] += len(b)
+
+    def drain_err():
+        err.append(p.stderr.read().decode(errors="replace"))
+
+    th = [threading.Thread(target=f, daemon=True) for f in (feed, drain_out, drain_err)]
+    for t in th:
+        t.start()
+    rc = p.wait()
+    for t in th:
+        t.join()
+    return time.perf_counter() - t0, nout[0], "".join(err), rc
+
+
+def run_live(args, ws, rank, local):
+    """SURVEY §8f row 2, end to end: fm_radio_gpu mode 0 (stereo + --rds) on a u8 stream fed
+    through its stdin, int16 L/R counted off its stdout, beside the reference's own fm_radio
+    (src/fm_radio.cpp, all of src/ compiled by oracle/Makefile `ref` into oracle/_ref/) on the
+    same bytes on the same host.  The stream is a seamless synthetic span (every tone completes
+    whole cycles over it, coded RDS groups) of --span blocks of 307 200 bytes, written
+    --live-repeat times; wall time from process start to exit (startup included), and the
+    marginal rate between a 1x and an Nx run (startup excluded)."""
+    import rtsdr
+    if rank != 0:
+        return
+    K = args.span
+    data = rtsdr.synth.fm_iq(K * C5_B, seed=11, dtype=np.uint8, rds_groups=True).tobytes()
+    env = dict(os.environ, SDR_DEVICE=str(local))
+    gpu_bin = os.path.join(ROOT, "real-time-software-defined-radio_amd", "fm_radio_gpu")
+    ref_bin = os.path.join(ROOT, "oracle", "_ref", "fm_radio")
+    out = {"metric": "IQ MSamples/s end to end through the live receiver (u8 stdin -> int16 L/R stdout), mode 0 "
+                     "stereo + RDS; real-time factor vs 2.4 MS/s",
+           "unit": "MS/s", "n_gpus": 1, "higher_is_better": True, "scaling": "replicas only", "vs_baseline": None,
+           "dtype": "f32", "data": f"synthetic u8 FM IQ with coded RDS groups, {K} blocks of {2 * C5_B} bytes, "
+                                   f"fed through stdin",
+           "config": {"workload": "SURVEY §8f row 2: live pipeline (src/fm_radio.cpp:31-441, 732-798)",
+                      "blocks_per_pass": K, "block_bytes": 2 * C5_B, "cmd": "fm_radio_gpu --rds"}}
+
+    def measure(cmd, reps):
+        rows = []
+        for r in reps:
+            wall, nbytes, err, rc = live_run(cmd, data, r, env=env)
+            if rc != 0:
+                raise SystemExit(f"bench live: {cmd[0]} exited {rc}: {err[-2000:]}")
+            n = r * K * C5_B
+            rows.append({"passes": r, "complex": n, "wall_s": round(wall, 4), "MS/s": round(n / wall / 1e6, 3),
+                         "realtime_factor": round(n / wall / 2.4e6, 2), "stdout_bytes": nbytes,
+                         "syndrome_lines": err.count("Syndrome")})
+        a, b = rows[0], rows[-1]
+        marg = (b["complex"] - a["complex"]) / max(b["wall_s"] - a["wall_s"], 1e-9)
+        return rows, round(marg / 1e6, 3)
+
+    reps = [1, args.live_repeat]
+    g_rows, g_marg = measure([gpu_bin, "--rds"], reps)
+    out["runs"] = g_rows
+    out["value"] = g_rows[-1]["MS/s"]
+    out["realtime_factor"] = g_rows[-1]["realtime_factor"]
+    out["marginal_MS/s"] = g_marg
+    out["marginal_realtime_factor"] = round(g_marg / 2.4, 2)
+    out["host_threads"] = 1
+    visible, model = cpu_cores()
+    if os.path.exists(ref_bin) and not args.no_cpu:
+        r_rows, r_marg = measure([ref_bin], [1, 2])
+        out["cpu_baseline"] = {"value": r_rows[-1]["MS/s"], "unit": "MS/s", "cores": 4, "kind": "reference",
+                               "cpu": model, "cores_visible": visible, "marginal_MS/s": r_marg,
+                               "realtime_factor": r_rows[-1]["realtime_factor"], "runs": r_rows,
+                               "sample": f"oracle/_ref/fm_radio (the reference's src/ compiled -O3 -pthread; its "
+                                         f"4 threads rf / mono_stereo / rds / frame), mode 0, the same bytes, "
+                                         f"1x and 2x passes; {ref_provenance()}"}
+    else:
+        out["cpu_baseline"] = {"value": None, "kind": "reference",
+                               "sample": "not run: oracle/_ref/fm_radio absent (make -C oracle ref, where "
+                                         "/root/reference exists)" if not args.no_cpu else "skipped (--no-cpu)"}
+    out["steps"] = args.live_repeat
+    out["warmup"] = 0
+    out["ms_per_step"] = round(g_rows[-1]["wall_s"] / args.live_repeat * 1e3, 3)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

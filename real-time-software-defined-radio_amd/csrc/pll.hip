@@ -563,8 +563,12 @@ __device__ __forceinline__ Mat2 mpow2(Mat2 x, int e) {
 // LONG: one workgroup per pseudo-block of a long call, from its start guess (status
 // LB_NEED_G) or its chained start (LB_NEED_X); the end state goes to the block's record and
 // the call's own state, trigOffset slot and NCO[0] are left to the long-call kernels.
-template <int SPEC_T, bool LONG>
-__global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T == 512 ? 4 : 2))) void pll_spec_kernel(PllJobs P) {
+// The body is a device function of the workgroup: pll_spec_kernel runs it once per workgroup
+// (bid = blockIdx.x); pll_long_fix_kernel re-solves single pseudo-blocks with it.  first (long
+// calls): the call's first solve -- the pseudo-block records are not initialised yet (the
+// bookkeeping is done here, for this block, instead of by a kernel of its own).
+template <int SPEC_T, bool LONG, bool first = false>
+__device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const int tid) {
 #pragma clang fp contract(off)
   // Per step k = 1 .. n-1, at slot i * CSTR + j (step i of chunk j, see the staging below):
   // the sign code of x_k (0: x > 0, 1: x < 0, 2: 0 / NaN) -- the constant c_k is a function
@@ -583,21 +587,51 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
   __shared__ double x1s[2];
   __shared__ float mg[NW + 1];                   // the waves' smallest wrap margins (+ the literal step's)
   d2v* yb = reinterpret_cast<d2v*>(tb);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
   int q, s, status = 0;
   int64_t n, base = 0;
   int pre = 0;                                   // LONG, guessed start: pre-roll steps (below)
   LongBlk* LB = nullptr;
+  bool from_call = false;                        // LONG: the start is the call's own state
   if constexpr (LONG) {
     const int nb = P.lg.nb;
-    const int r = blockIdx.x / nb;
-    const int b = blockIdx.x - r * nb;
+    const int r = bid / nb;
+    const int b = bid - r * nb;
     q = r / P.nstreams;
     s = r - q * P.nstreams;
     LB = long_blk(P, r, b);
-    status = LB->status;
-    if (status != LB_NEED_G && status != LB_NEED_X) return;
+    if constexpr (first) {
+      // every pseudo-block unsolved, no shift; the first starts from the call's state (exact),
+      // the others from the guess their pre-roll finds (below).  Block 0 also leaves the
+      // call's NCO[0] and trigOffset slot as the per-call kernels do.
+      status = LB_NEED_G;
+      from_call = b == 0;
+      if (tid == 0) {
+        const PllJob& Jq = P.j[q];
+        const double* sc = Jq.state + (int64_t)s * 6;
+        LB->shift = 0.0;
+        LB->d[0] = LB->d[1] = 0.0;
+        LB->margin = -1.0;
+        LB->status = LB_NEED_G;
+        LB->solver = -1;
+        for (int i = 0; i < 6; ++i) LB->g[i] = b == 0 ? sc[i] : __builtin_nan("");
+        if (b == 0) {
+          const double w0 = 2.0 * kPi * (Jq.cfg.freq / Jq.cfg.fs);
+          LongHdr* H = long_hdr(P, r);
+          H->sp = sc[1];
+          H->si = sc[0];
+          H->pos = 0;
+          Jq.nco_i[(int64_t)s * Jq.out_stride] = (float)sc[4];
+          if (Jq.nco_q)
+            Jq.nco_q[(int64_t)s * Jq.out_stride] =
+                (float)((sc[5] > 0.0) ? sin((w0 * sc[5] + sc[1]) * Jq.cfg.scale + Jq.cfg.adj) : 0.0);
+          Jq.theta[(int64_t)s * Jq.th_stride + P.n] = sc[5];     // the NCO kernel's trigOffset
+        }
+      }
+    } else {
+      status = LB->status;
+      if (status != LB_NEED_G && status != LB_NEED_X) return;
+    }
     base = (int64_t)b * P.lg.pb;
     n = long_len(P, b);
     // a pseudo-block after the first, not yet reached by the chain: its start is unknown, so
@@ -610,8 +644,8 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
     n += pre;
     base -= pre;
   } else {
-    q = blockIdx.x / P.nstreams;
-    s = blockIdx.x - q * P.nstreams;
+    q = bid / P.nstreams;
+    s = bid - q * P.nstreams;
     n = P.n;
   }
   const PllJob& J = P.j[q];
@@ -627,9 +661,10 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
 #else
 #define SPEC_TP() do {} while (0)
 #endif
-  double* st = LONG ? (status == LB_NEED_G ? LB->g : LB->x) : J.state + (int64_t)s * 6;
-  double* st_out = LONG ? LB->e : st;
   const double* st_call = J.state + (int64_t)s * 6;
+  double* st = LONG ? (from_call ? J.state + (int64_t)s * 6 : status == LB_NEED_G ? LB->g : LB->x)
+                    : J.state + (int64_t)s * 6;
+  double* st_out = LONG ? LB->e : st;
   const double off = sgpr_d(pre ? st_call[5] + (double)base : st[5]);   // trigOffset of local step 0
   const double w = sgpr_d(2.0 * kPi * (cfg.freq / cfg.fs));
   const double kA = sgpr_d(k2Pi * cfg.ki), kB = sgpr_d(kPi * cfg.ki);
@@ -758,8 +793,12 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
   // within a block, so it fits a byte once jb is taken off (a drifting phase estimate moves jb)
   const double jb = floor(kInv2Pi * p1);
   auto rel_of = [&](double t, double c) { return floor(t) - floor(c) + jb; };
-  // 1. guess
+  // 1. guess.  With every m_k fixed at the floor the pass itself takes, a pass over a chunk IS
+  // the loop's linear form x' = A x + u_k, so the chunk's response from zero state -- what the
+  // scan needs -- is its end state less A^L times its start: z_j = x_end - Q x_start (the
+  // solve needs no pass of its own; the check below validates whatever this rounds to)
   bool bad = false;
+  double xs_p = 0.0, xs_v = 0.0, xe_p = 0.0, xe_v = 0.0;
   {
     // the true step from a seed on the measured drift: phaseEst ~ p1 + D at the warm-up's
     // start, integ ~ the measured drift per step; 256 steps of the loop then pull the guess
@@ -789,6 +828,8 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
       }
     }
     __syncthreads();                             // yb (D_j) read before tb reuses its space
+    xs_p = p;                                    // the guess's chunk start (after the warm-up)
+    xs_v = V;
     for (int i0 = 0; i0 < L; i0 += SB) {
       int cd[SB];
 #pragma unroll
@@ -809,6 +850,8 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
         p = act ? np : p;
       }
     }
+    xe_p = p;                                    // ... and its end
+    xe_v = V;
   }
   if (__syncthreads_or(bad)) return;             // a 0 / NaN input (the general form's case)
   SPEC_TP();
@@ -834,26 +877,13 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
   };
   double* tw = tb + wv * SB * TBS;               // this wave's transpose tile
   for (int round = 0; round < SPEC_IT; ++round) {
-    // 2. solve: the chunk's response from zero state
-    double zp = 0.0, zv = 0.0;
-    for (int i0 = 0; i0 < L; i0 += SB) {
-      int cd[SB];
-      int8_t mm[SB];
-#pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        cd[u] = code[(i0 + u) * CSTR + tid];
-        mm[u] = mrel[(i0 + u) * CSTR + tid];
-      }
-#pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        const double c = cval(cd[u], k0 + i0 + u);
-        const double d = c - (floor(c) + ((double)mm[u] - jb));
-        const double np = a00 * zp + zv + kC * d;
-        const double nv = a10 * zp + zv + (kA * d - kB);
-        const bool act = i0 + u < len;
-        zp = act ? np : zp;
-        zv = act ? nv : zv;
-      }
+    // 2. solve: the chunk's response from zero state to the current integers, from the last
+    // pass over it (the guess in round 0, the previous check after): z_j = x_end - Q x_start
+    double zp, zv;
+    {
+      const Mat2 Q = qp[0];
+      zp = xe_p - (Q.a * xs_p + Q.b * xs_v);
+      zv = xe_v - (Q.c * xs_p + Q.d * xs_v);
     }
     // chunk starts y_j = Q^j x_1 + Y_{j-1}, Y_j = sum_{i<=j} Q^(j-i) z_i (Q = A^L): an inclusive
     // scan of the z_i within each wave by shuffles (offset o combines with Q^o), then across the
@@ -905,6 +935,8 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
     // (64-B runs) instead of 64 scattered doubles
     bool miss = false;
     double p = vp, V = vv;
+    xs_p = vp;                                   // this pass's start and (below) end: the next
+    xs_v = vv;                                   // round's responses to the integers it records
     float mth = 1.f;                             // smallest min(fract, 1 - fract) of the block's own steps
     for (int i0 = 0; i0 < L; i0 += SB) {
       int cd[SB / 2];                            // (half a batch of codes at a time: registers)
@@ -949,6 +981,8 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    xe_p = p;
+    xe_v = V;
     if constexpr (LONG) {
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) mth = fminf(mth, __shfl_xor(mth, o, 64));
@@ -957,8 +991,8 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
     const int nmiss = __syncthreads_count(miss);
     SPEC_TP();
 #ifdef SDR_PLL_SPEC_PROF
-    if (tid == 0 && nmiss == 0 && (blockIdx.x % 479) == 3)
-      printf("spec_prof blk %d L %d: stage %lld corr %lld guess %lld solve %lld check %lld (%d marks)\n", (int)blockIdx.x, L,
+    if (tid == 0 && nmiss == 0 && (bid % 479) == 3)
+      printf("spec_prof blk %d L %d: stage %lld corr %lld guess %lld solve %lld check %lld (%d marks)\n", bid, L,
              tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], ntp);
 #endif
 #ifdef SDR_PLL_SPEC_DEBUG   // A/B builds only (make ... CXXFLAGS+=-DSDR_PLL_SPEC_DEBUG): never in libsdr.so
@@ -1021,76 +1055,48 @@ __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T =
   }
 }
 
+template <int SPEC_T, bool LONG>
+__global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T == 512 ? 4 : 2))) void pll_spec_kernel(PllJobs P) {
+  spec_body<SPEC_T, LONG, LONG>(P, (int)blockIdx.x, (int)threadIdx.x);   // (a long call's first solve of every block)
+}
+
 // ================================================================================
 // Long calls (n > SDR_PLL_BLOCK_MAX): a device-resident span of many blocks is one recurrence
 // of n steps, cut into nb pseudo-blocks of pb <= LONG_PB (14 336) steps so that every pseudo-block
 // (with its pre-roll) is one pll_spec_kernel workgroup and the whole span fills the GPU.  A
 // pseudo-block's start state is the previous one's end state, unknown until that one is
-// solved, so:
-//   1. pll_long_init_kernel: bookkeeping; the first pseudo-block starts from the call's state.
-//   2. pll_spec_kernel<..., LONG> (+ pll_long_seq_kernel for what it cannot complete): every
-//      pseudo-block solved.  One after the first is solved together with a PRE-ROLL: the
-//      `warm` steps before it, from the phase the input measures there and the span's start
+// solved, so two launches:
+//   1. pll_spec_kernel<512, LONG> (first = 1): every pseudo-block solved (and its record
+//      initialised).  One after the first is solved together with a PRE-ROLL: the `warm`
+//      steps before it, from the phase the input measures there and the span's start
 //      integrator; the loop contracts errors by sqrt(1 - Kp) per step, and its dynamics are
 //      invariant under phaseEst -> phaseEst + 2 pi, so the pre-roll's state at the block's
 //      start -- its GUESS -- has converged to the true state up to a whole number of turns
 //      (the parallel form of a sequential warm-up over the same steps).
-//   3. pll_long_chain_kernel (one wave per recurrence, serial over the pseudo-blocks, all in
-//      f64 scalars): from the exact state at the chain's position, the 2 pi shift n between
-//      the exact start and the guess is taken out, and the remaining start error (dp, dV)
-//      bounds the phase deviation of the block's solution by err = c1 |dp| + c2 |dV| (c1, c2:
-//      the largest phase excursion the loop's linear form makes from a unit start error).
+//   2. pll_long_fix_kernel (one workgroup per recurrence): the CHAIN -- from the exact state
+//      at the chain's position, the 2 pi shift n between the exact start and each block's
+//      solved start is taken out, and the remaining start error (dp, dV) bounds the phase
+//      deviation of the block's solution by err = c1 |dp| + c2 |dV| (c1, c2: the largest phase
+//      excursion the loop's linear form makes from a unit start error):
 //        err <= 1e-9 rad: accepted -- its phases + 2 pi n are the recurrence's (to a deviation
 //                         below the reference's own rounding of its ~1e6 rad angle), and its
 //                         end state + 2 pi n is the next block's exact start;
-//        err <= 0.3 rad:  re-solve it from the exact start (step 2 again, LB_NEED_X); its end
-//                         state follows by the linear form, e + 2 pi n + Phi (dp, dV) (Phi =
-//                         the loop matrix to the block's length: the next start, provisional
-//                         until the re-solve confirms it);
-//        else:            re-solve it, and stop the chain there this round.
-//      Blocks are accepted only while the chain is exact; provisional ones are checked again.
-//   Steps 2-3 run SPEC_ROUNDS times; pll_long_tail_kernel then runs whatever is left
-//   sequentially from the chain's exact position (never on a locked signal: counted).
-//   The NCO kernel adds 2 pi n to an accepted guessed block's phases.
+//        err <= 0.3 rad and every step's wrap margin above err: accepted with the loop's
+//                         linear response to the start error (no integer m_k can move; the
+//                         NCO kernel adds the response);
+//        else:            the chain stops there.
+//      A stop is repaired in the same kernel: the block at the chain's position is re-solved
+//      from its exact start by the whole workgroup (spec_body; the sequential step if the
+//      solve cannot complete it -- a 0 / NaN input), and the chain continues; the blocks after
+//      it keep their solutions and are judged again against the new exact prefix.  After
+//      LONG_FIXES repairs the rest runs sequentially from the chain's position (never on a
+//      locked signal: counted).  On a locked signal the kernel makes one chain pass and exits:
+//      no launches for repair rounds that have nothing to do.
+//   The NCO kernel adds 2 pi n (and any linear response) to an accepted block's phases.
 constexpr double LONG_ACCEPT = 1e-9;   // rad: accepted deviation bound
 constexpr double LONG_LINEAR = 0.3;    // rad: deviation bound under which the integers m_k are kept
 constexpr double LONG_MARGIN_TOL = 1e-6;   // turns: wrap margin kept clear of rounding
-constexpr int LONG_ROUNDS = 4;
-
-// 1. Bookkeeping: every pseudo-block unsolved, no shift; the first starts from the call's
-// state (exact), the others from the guess their solve's pre-roll finds (pll_spec_kernel).
-__global__ __launch_bounds__(256) void pll_long_init_kernel(PllJobs P) {
-  const int nb = P.lg.nb;
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (int64_t)P.njobs * P.nstreams * nb) return;
-  const int r = (int)(g / nb), b = (int)(g - (int64_t)r * nb);
-  const int q = r / P.nstreams, s = r - q * P.nstreams;
-  const PllJob& J = P.j[q];
-  const PllCfg cfg = J.cfg;
-  const double* st = J.state + (int64_t)s * 6;
-  LongBlk* B = long_blk(P, r, b);
-  B->shift = 0.0;
-  B->d[0] = B->d[1] = 0.0;
-  B->margin = -1.0;
-  B->status = LB_NEED_G;
-  B->solver = -1;
-  if (b > 0) {
-    for (int i = 0; i < 6; ++i) B->g[i] = __builtin_nan("");
-    return;
-  }
-  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
-  const double off0 = st[5];
-  for (int i = 0; i < 6; ++i) B->g[i] = st[i];
-  LongHdr* H = long_hdr(P, r);
-  H->sp = st[1];
-  H->si = st[0];
-  H->pos = 0;
-  J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];       // ncoOut[0] (as the per-call kernels)
-  if (J.nco_q)
-    J.nco_q[(int64_t)s * J.out_stride] =
-        (float)((off0 > 0.0) ? sin((w * off0 + st[1]) * cfg.scale + cfg.adj) : 0.0);
-  J.theta[(int64_t)s * J.th_stride + P.n] = off0;         // the NCO kernel's trigOffset
-}
+constexpr int LONG_FIXES = 24;         // repairs (re-solves at the chain's position) before the tail
 
 // The reference's recurrence run sequentially from state st over n steps (the general form:
 // literal first step from the state's (fI, fQ); 0 / NaN inputs by atan2 on the products; the
@@ -1145,43 +1151,19 @@ __device__ void seq_run(const PllCfg& cfg, const float* in, double* th, int64_t 
   so[5] = off + (double)n;
 }
 
-// 2b. Pseudo-blocks pll_spec_kernel did not complete (a 0 / NaN input, no convergence), from
-// the same start: one lane each.
-__global__ __launch_bounds__(64) void pll_long_seq_kernel(PllJobs P) {
-  const int nb = P.lg.nb;
-  const int wpr = (nb + 63) / 64;
-  const int r = blockIdx.x / wpr;
-  const int b = (blockIdx.x - r * wpr) * 64 + threadIdx.x;
-  if (b >= nb) return;
-  const int q = r / P.nstreams, s = r - q * P.nstreams;
-  const PllJob& J = P.j[q];
-  LongBlk* B = long_blk(P, r, b);
-  const int status = B->status;
-  if (status != LB_NEED_G && status != LB_NEED_X) return;
-  if (status == LB_NEED_G && b > 0) return;      // no start yet: the chain hands it one (LB_NEED_X)
-  const int64_t base = (int64_t)b * P.lg.pb;
-  seq_run(J.cfg, J.in + (int64_t)s * J.in_stride + base, J.theta + (int64_t)s * J.th_stride + base, long_len(P, b),
-          status == LB_NEED_G ? B->g : B->x, B->e);
-  B->u[0] = (status == LB_NEED_G ? B->g : B->x)[0];
-  B->u[1] = (status == LB_NEED_G ? B->g : B->x)[1];
-  B->d[0] = B->d[1] = 0.0;
-  B->margin = -1.0;                              // (general steps: no linear acceptance)
-  B->status = status + 1;
-  B->solver = SOLVER_SEQ;
-}
-
-// 3. The chain: one workgroup per recurrence, one thread per pseudo-block of a CHAIN_T-block
-// window (the windows in order; one window up to 7 M samples).  With A_j the start block j's
-// current solution was solved from, E_j its end and S_j the chained start, the residual
-// R_j = S_j - A_j splits into n_j whole turns and rho_j = R_j - 2 pi n_j, and
+// The chain pass (CHAIN_T threads, one per pseudo-block of a CHAIN_T-block window; the
+// windows in order).  With A_j the start block j's current solution was solved from, E_j its
+// end and S_j the chained start, the residual R_j = S_j - A_j splits into n_j whole turns and
+// rho_j = R_j - 2 pi n_j, and
 //     R_{j+1} = (E_j - A_{j+1}) + 2 pi n_j + Phi_j rho_j.
 // |Phi_j| <= 1e-8 (the loop matrix over a pseudo-block), so the turns are a prefix sum of the
 // local integers rint((E_j - A_{j+1})_phase / 2 pi), and rho_{j+1} = C_j + Phi_j C_{j-1} to f64
 // rounding (C_j = E_j - A_{j+1} less its turns; the term after is Phi^2 ~ 1e-16 rho).  Then per
-// block the bound err = c1 |rho_p| + c2 |rho_v| decides, as described above; a prefix of
-// accepted blocks moves the chain's position.
+// block the bound err = c1 |rho_p| + c2 |rho_v| decides, as described above.  The accepted
+// prefix moves the chain's position; the first block after it that is not accepted gets its
+// exact start (LB_NEED_X) for a re-solve.  Returns the new position (every thread).
 constexpr int CHAIN_T = 512;
-__global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int round) {
+__device__ int chain_pass(const PllJobs& P, const int r) {
 #pragma clang fp contract(off)
   constexpr int NWV = CHAIN_T / 64;
   __shared__ double sA[2][CHAIN_T + 1];    // A_j (phase, integrator), and the next window's first
@@ -1189,13 +1171,14 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
   __shared__ double sE[3][CHAIN_T];        // E_j + 2 pi n_j (phase), E_j (integrator), and n_j
   __shared__ double sR[2][CHAIN_T];        // rho_j
   __shared__ double wtot[NWV];
-  __shared__ int wfa[NWV], wfs[NWV];
-  const int r = blockIdx.x;
+  __shared__ int wfa[NWV];
+  __shared__ int spos;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nb = P.lg.nb;
   LongHdr* H = long_hdr(P, r);
+  __syncthreads();                          // (the previous pass / re-solve: records written)
   const int pos0 = H->pos;
-  if (pos0 >= nb) return;
+  if (pos0 >= nb) return pos0;
   const int q = r / P.nstreams, s = r - q * P.nstreams;
   const PllJob& J = P.j[q];
   const PllCfg cfg = J.cfg;
@@ -1204,8 +1187,7 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
   double* st = J.state + (int64_t)s * 6;
   const double off0 = st[5];
   const int64_t pb = P.lg.pb;
-  double Cp = H->sp, Ci = H->si;     // the carried (chained) start of the window's first block
-  bool cexact = true;                // ... exact (else provisional)
+  double Cp = H->sp, Ci = H->si;     // the carried (exact) start of the window's first block
   int pos = pos0;
   double Xp = Cp, Xi = Ci;           // the exact state at `pos`
   for (int w0 = pos0; w0 < nb; w0 += CHAIN_T) {
@@ -1274,15 +1256,10 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
     // err (then no integer m_k moves: the block's phases + its linear response to the start
     // error rho are the recurrence's, up to rounding -- nco_long_kernel adds the response)
     const bool lina = err <= LONG_LINEAR && k2Pi * (margin - LONG_MARGIN_TOL) > err;
-    const bool acc = solved && (err <= LONG_ACCEPT || lina);
-    const bool lin = solved && err <= LONG_LINEAR;   // (a NaN fails both)
-    // the first block not accepted / not within the linear bound (CHAIN_T: none)
-    {
-      const uint64_t na = __ballot(!acc), nl = __ballot(!lin);   // (invalid blocks are neither)
-      if (lane == 0) {
-        wfa[wv] = na ? wv * 64 + __builtin_ctzll(na) : CHAIN_T;
-        wfs[wv] = nl ? wv * 64 + __builtin_ctzll(nl) : CHAIN_T;
-      }
+    const bool acc = solved && (err <= LONG_ACCEPT || lina);   // (a NaN fails both)
+    {                                                // the first block not accepted (CHAIN_T: none)
+      const uint64_t na = __ballot(!acc);           // (invalid blocks are not accepted)
+      if (lane == 0) wfa[wv] = na ? wv * 64 + __builtin_ctzll(na) : CHAIN_T;
     }
     const double ejp = fma(nj, kP1, fma(nj, kP2, ep));  // E_j + 2 pi n_j
     sE[0][tid] = ejp;
@@ -1291,35 +1268,39 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
     sR[0][tid] = rp;
     sR[1][tid] = rv;
     __syncthreads();
-    int fa = CHAIN_T, fs = CHAIN_T;
-    for (int i = 0; i < NWV; ++i) {
-      fa = min(fa, wfa[i]);
-      fs = min(fs, wfs[i]);
-    }
-    const int nacc = cexact ? fa : 0;
-    // this block's chained start S_j = A_j + 2 pi n_j + rho_j (exact for blocks <= nacc)
-    double sp = fma(nj, kP1, fma(nj, kP2, ap)) + rp, si = ai + rv;
-    // an unsolved block right after the exact prefix (its solve failed: no start from it): the
-    // exact start is the previous block's end + its turns (block 0: the carry)
-    if (tid == nacc && !solved) {
-      if (tid == 0) { sp = Cp; si = Ci; }
-      else { sp = sE[0][tid - 1]; si = sE[1][tid - 1]; }
-    }
-    if (valid && tid <= fs) {
+    int nacc = CHAIN_T;
+    for (int i = 0; i < NWV; ++i) nacc = min(nacc, wfa[i]);
+    if (valid && tid < nacc) {
       LongBlk* B = long_blk(P, r, j);
-      if (tid < nacc) {
-        B->status = LB_ACCEPTED;
-        B->shift = nj;
-        B->d[0] = err <= LONG_ACCEPT ? 0.0 : rp;      // the linear response the NCO kernel adds
-        B->d[1] = err <= LONG_ACCEPT ? 0.0 : rv;
-      } else if (!acc && (solved || (tid == nacc && cexact))) {   // re-solve from the chained start
+      B->status = LB_ACCEPTED;
+      B->shift = nj;
+      B->d[0] = err <= LONG_ACCEPT ? 0.0 : rp;      // the linear response the NCO kernel adds
+      B->d[1] = err <= LONG_ACCEPT ? 0.0 : rv;
+    } else if (valid && tid == nacc) {              // the chain's next block: its exact start
+      // S_j = A_j + 2 pi n_j + rho_j when it was solved; else the previous block's end + its
+      // turns + Phi rho (block `pos0`: the carry)
+      double sp, si;
+      if (solved) {
+        sp = fma(nj, kP1, fma(nj, kP2, ap)) + rp;
+        si = ai + rv;
+      } else if (tid == 0) {
+        sp = Cp;
+        si = Ci;
+      } else {
+        const double* pp = P.lg.phi[q];
+        sp = sE[0][tid - 1] + (pp[0] * sR[0][tid - 1] + pp[1] * sR[1][tid - 1]);
+        si = sE[1][tid - 1] + (pp[2] * sR[0][tid - 1] + pp[3] * sR[1][tid - 1]);
+      }
 #ifdef SDR_PLL_LONG_DEBUG
-        if (tid == fs)
-          printf("chain r%d b%d/%d status %d: err %.3e rho %.3e %.3e n %.0f\n", r, j, nb, sj, err, rp, rv, nj);
+      printf("chain r%d b%d/%d status %d: err %.3e rho %.3e %.3e n %.0f\n", r, j, nb, sj, err, rp, rv, nj);
 #endif
-        B->u[0] = ai;
-        B->u[1] = ap;
-        if (!solved) B->solver = -1;
+      LongBlk* B = long_blk(P, r, j);
+      B->u[0] = ai;
+      B->u[1] = ap;
+      B->solver = -1;
+      if (j == 0) {                                 // the call's own first step: its state as given
+        for (int i = 0; i < 6; ++i) B->x[i] = st[i];
+      } else {
         const double offp = off0 + (double)((int64_t)(j - 1) * pb);
         const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + sp;
         B->x[0] = si;
@@ -1328,9 +1309,10 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
         B->x[3] = sin(arg);
         B->x[4] = 0.0;
         B->x[5] = off0 + (double)((int64_t)j * pb);
-        B->shift = 0.0;
-        B->status = LB_NEED_X;
       }
+      B->shift = 0.0;
+      B->d[0] = B->d[1] = 0.0;
+      B->status = LB_NEED_X;
     }
     {                                                   // the counters, one atomic per wave each
       const bool a = valid && tid < nacc, ex = err <= LONG_ACCEPT;
@@ -1341,7 +1323,7 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
       stat_add_wave(P.stats, SDR_PLL_ST_LONG_CHAINED, a && !(sj == LB_DONE_G && ex));
       stat_add_wave(P.stats, SDR_PLL_ST_LONG_LINEAR, a && !ex);
       stat_max_wave(P.stats, SDR_PLL_ST_LONG_MAXGAP, a && ex, err);
-      stat_add_wave(P.stats, SDR_PLL_ST_LONG_STOPS, valid && tid == fs && !acc && (solved || (tid == nacc && cexact)));
+      stat_add_wave(P.stats, SDR_PLL_ST_LONG_STOPS, valid && tid == nacc);
     }
     // the state after the accepted prefix: E + 2 pi n + Phi rho of its last block
     if (nacc > 0) {
@@ -1349,22 +1331,13 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
       const double* phl = (w0 + l == nb - 1) ? P.lg.phi_last[q] : P.lg.phi[q];
       Xp = sE[0][l] + (phl[0] * sR[0][l] + phl[1] * sR[1][l]);
       Xi = sE[1][l] + (phl[2] * sR[0][l] + phl[3] * sR[1][l]);
-      pos = w0 + nacc;
+      pos = min(w0 + nacc, nb);
     }
-    if (fs < CHAIN_T || w0 + CHAIN_T >= nb) break;     // the chain cannot pass block fs this round
-    // carry: S_{w0+CHAIN_T} = E_last + 2 pi n_last + Phi_last rho_last
-    {
-      const int l = CHAIN_T - 1;
-      const double* pp = P.lg.phi[q];
-      Cp = sE[0][l] + (pp[0] * sR[0][l] + pp[1] * sR[1][l]);
-      Ci = sE[1][l] + (pp[2] * sR[0][l] + pp[3] * sR[1][l]);
-    }
-    cexact = cexact && fa == CHAIN_T;
+    if (nacc < CHAIN_T || w0 + CHAIN_T >= nb) break;   // stopped, or the last window
+    Cp = Xp;                                            // carry: the exact state at the next window
+    Ci = Xi;
     __syncthreads();                                    // the window's LDS read before the next writes it
   }
-#ifdef SDR_PLL_LONG_DEBUG
-  if (tid == 0) printf("chain r%d round %d: position %d -> %d of %d\n", r, round, pos0, pos, nb);
-#endif
   if (tid == 0) {
     H->pos = pos;
     H->sp = Xp;
@@ -1379,23 +1352,22 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_chain_kernel(PllJobs P, int 
       st[4] = cos(arg * cfg.scale + cfg.adj);
       st[5] = off0 + (double)P.n;
     }
+    spos = pos;
   }
-  (void)round;
+  __syncthreads();
+  return spos;
 }
 
-// 4. Whatever the rounds left: sequential from the chain's exact position to the end.
-__global__ __launch_bounds__(64) void pll_long_tail_kernel(PllJobs P) {
+// Sequential from the chain's exact position to the end (after LONG_FIXES repairs), by one thread.
+__device__ void long_tail(const PllJobs& P, const int r, const int pos) {
 #pragma clang fp contract(off)
-  const int r = blockIdx.x;
   const int nb = P.lg.nb;
   LongHdr* H = long_hdr(P, r);
-  const int pos = H->pos;
-  if (pos >= nb) return;
   const int q = r / P.nstreams, s = r - q * P.nstreams;
   const PllJob& J = P.j[q];
   const PllCfg cfg = J.cfg;
   double* st = J.state + (int64_t)s * 6;
-  for (int b = pos + threadIdx.x; b < nb; b += 64) {
+  for (int b = pos + (int)threadIdx.x; b < nb; b += blockDim.x) {
     long_blk(P, r, b)->shift = 0.0;
     long_blk(P, r, b)->d[0] = long_blk(P, r, b)->d[1] = 0.0;
   }
@@ -1421,6 +1393,43 @@ __global__ __launch_bounds__(64) void pll_long_tail_kernel(PllJobs P) {
   stat_add(P.stats, SDR_PLL_ST_RECURRENCES, (unsigned long long)(nb - pos));
   stat_add(P.stats, SDR_PLL_ST_SEQUENTIAL, (unsigned long long)(nb - pos));
   stat_add(P.stats, SDR_PLL_ST_LONG_TAIL, (unsigned long long)(nb - pos));
+}
+
+// 2. The chain with its repairs: one workgroup per recurrence (CHAIN_T == the solve's 512
+// threads, so spec_body runs in it).  Locked signal: one chain pass, done.
+static_assert(CHAIN_T == 512, "pll_long_fix_kernel runs spec_body<512, true>");
+__global__ __launch_bounds__(CHAIN_T) void pll_long_fix_kernel(PllJobs P) {
+  const int r = blockIdx.x;
+  const int nb = P.lg.nb;
+  int pos = chain_pass(P, r);
+  for (int fix = 0; pos < nb; ++fix) {
+    if (fix == LONG_FIXES) {
+      long_tail(P, r, pos);
+      return;
+    }
+    // the block at the chain's position has its exact start (LB_NEED_X): solve it in parallel.
+    // (The thread index goes in opaque: otherwise the compiler hoists the solve's per-thread
+    // LDS addresses out of this loop for its whole length, and spills.)
+    int tid = (int)threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    spec_body<512, true>(P, r * nb + pos, tid);
+    __syncthreads();
+    LongBlk* B = long_blk(P, r, pos);
+    if (threadIdx.x == 0 && B->status == LB_NEED_X) {   // not completed (0 / NaN input): the sequential step
+      const int q = r / P.nstreams, s = r - q * P.nstreams;
+      const PllJob& J = P.j[q];
+      const int64_t base = (int64_t)pos * P.lg.pb;
+      seq_run(J.cfg, J.in + (int64_t)s * J.in_stride + base, J.theta + (int64_t)s * J.th_stride + base, long_len(P, pos),
+              B->x, B->e);
+      B->u[0] = B->x[0];
+      B->u[1] = B->x[1];
+      B->d[0] = B->d[1] = 0.0;
+      B->margin = -1.0;                              // (general steps: no linear acceptance)
+      B->status = LB_DONE_X;
+      B->solver = SOLVER_SEQ;
+    }
+    pos = chain_pass(P, r);
+  }
 }
 
 // Per-sample constants of the loop (parallel): c_k = (sel_k - w (off + k)) / 2pi + 1/2 and one flag per
@@ -1711,19 +1720,13 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
   if (e != hipSuccess) return e;
   PllJobs L = P;
   if (pll_long(P)) {
-    // long call: warm-up guesses, LONG_ROUNDS x (solve, chain), the sequential tail
+    // long call: every pseudo-block solved (from warm-up guesses), then the chain with its repairs
     L.qform = 0;
     e = long_setup(L);
     if (e != hipSuccess) return e;
     const int R = L.njobs * L.nstreams;
-    const unsigned blocks = (unsigned)(R * L.lg.nb);
-    hipLaunchKernelGGL(pll_long_init_kernel, dim3((unsigned)(((int64_t)R * L.lg.nb + 255) / 256)), dim3(256), 0, st, L);
-    for (int round = 0; round < LONG_ROUNDS; ++round) {
-      hipLaunchKernelGGL((pll_spec_kernel<512, true>), dim3(blocks), dim3(512), 0, st, L);
-      hipLaunchKernelGGL(pll_long_seq_kernel, dim3((unsigned)(R * ((L.lg.nb + 63) / 64))), dim3(64), 0, st, L);
-      hipLaunchKernelGGL(pll_long_chain_kernel, dim3((unsigned)R), dim3(CHAIN_T), 0, st, L, round);
-    }
-    hipLaunchKernelGGL(pll_long_tail_kernel, dim3((unsigned)R), dim3(64), 0, st, L);
+    hipLaunchKernelGGL((pll_spec_kernel<512, true>), dim3((unsigned)(R * L.lg.nb)), dim3(512), 0, st, L);
+    hipLaunchKernelGGL(pll_long_fix_kernel, dim3((unsigned)R), dim3(CHAIN_T), 0, st, L);
     return hipGetLastError();
   }
   L.lpw = pll_lpw(P);
