@@ -116,10 +116,21 @@ __device__ __forceinline__ void sincos_red(double a, double* sv, double* cv) {
 // The loop's per-sample constant (pll_prep_kernel's, plain form): c_k = (sel_k - w (off + k)) / 2pi
 // + 1/2, offk = off + k exactly; NaN for a 0 / NaN input.  Long calls compute it where it is
 // used instead of storing a row of it.
+// (r04: one rounding, fma(-offk, w / 2pi, 1/2 + sel_k / 2pi), where r03 rounded three times
+// -- the same value to an ulp of |c_k|, the order of the reference's own rounding of its angle
+// w (off + k + 1); every kernel forms c_k this way, so all agree bit for bit)
 __device__ __forceinline__ double pll_c(float x, double w, double offk) {
-  const double cc = (x > 0.f ? 0.0 : kPi) - w * offk;
-  const double cv = fma(cc, kInv2Pi, 0.5);
+  const double cv = fma(-offk, w * kInv2Pi, x > 0.f ? 0.5 : 1.0);
   return (x > 0.f || x < 0.f) ? cv : __builtin_nan("");
+}
+
+// The low byte of floor(t) (|t| < 2^51): t - fract(t) is floor(t) exactly, and adding 1.5 2^52
+// puts that integer in the low word -- two f64 adds instead of a floor and a conversion that
+// saturates beyond 2^31.  The solve records and compares the integers m_k by this byte (a
+// guess and its check never disagree by a multiple of 256 turns).
+__device__ __forceinline__ int8_t floor_byte(double t, double f) {
+  const double u = (t - f) + 6755399441055744.0;
+  return (int8_t)(__double2loint(u) & 0xff);
 }
 
 // Steps per group: the next group's inputs are loaded (registers) while this one runs,
@@ -573,7 +584,7 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
   // Per step k = 1 .. n-1, at slot i * CSTR + j (step i of chunk j, see the staging below):
   // the sign code of x_k (0: x > 0, 1: x < 0, 2: 0 / NaN) -- the constant c_k is a function
   // of it and k alone (pll_c), recomputed where it is used, which keeps the workgroup's LDS
-  // at ~68 KB (two per CU) instead of a 128 KiB f64 image -- and m_k - floor(c_k) + jb
+  // at ~68 KB (two per CU) instead of a 128 KiB f64 image -- and the low byte of m_k
   // (jb = floor(phaseEst_1 / 2pi)).  tb: per wave, SB steps x 64 chunks of phases on their
   // way to coalesced theta stores (stride TBS = 4 mod 32 doubles: both its write and its
   // transposed read are conflict-free); the chunk scans' scratch (yb) shares its space.
@@ -586,6 +597,7 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
   __shared__ Mat2 qp[10];
   __shared__ double x1s[2];
   __shared__ float mg[NW + 1];                   // the waves' smallest wrap margins (+ the literal step's)
+  __shared__ double wsh;                         // w for the end state (no register across the solve)
   d2v* yb = reinterpret_cast<d2v*>(tb);
   const int lane = tid & 63, wv = tid >> 6;
   int q, s, status = 0;
@@ -674,12 +686,11 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
     const double i = (double)(k % PG);
     return ph + kB * ((i + 1.0) * i * 0.5);
   };
-  // c_k from the sign code: pll_c's arithmetic exactly (the prep kernel's plain form)
-  auto cval = [&](int cd, int k) {
-    const double cc = (cd == 0 ? 0.0 : kPi) - w * (off + (double)k);
-    const double cv = fma(cc, kInv2Pi, 0.5);
-    return cd == 2 ? __builtin_nan("") : cv;
-  };
+  // c_k from the sign code: pll_c's arithmetic exactly (code 2, a 0 / NaN input, is caught by
+  // the guess: the solve is abandoned to the general form, so its value here does not matter)
+  const double w2pi = sgpr_d(w * kInv2Pi);
+  if (tid == 0) wsh = w;
+  auto cval = [&](int cd, int k) { return fma(-(off + (double)k), w2pi, cd == 0 ? 0.5 : 1.0); };
   // sample 0: the literal general step (thread 0), as the loop kernels' general() (a
   // pre-roll's seed is set from the measured phase instead, below)
   if (tid == 0 && pre == 0) {
@@ -738,7 +749,7 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
     // far below what a guess needs -- the check, not the guess, makes the solve exact)
     float zr = 0.f, zi = 0.f;
     {
-      const double a0 = __builtin_amdgcn_fract((w * kInv2Pi) * (off + (double)k0));
+      const double a0 = __builtin_amdgcn_fract(w2pi * (off + (double)k0));
       float ci, cr, ds, dc;
       __sincosf((float)(k2Pi * a0), &ci, &cr);
       __sincosf((float)w, &ds, &dc);
@@ -789,10 +800,6 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
   }
   SPEC_TP();
   const double p1 = x1s[0], v1 = x1s[1];
-  // the integer part relative to floor(c_k) is floor(-phaseEst/2pi + frac(c_k)): near -jb
-  // within a block, so it fits a byte once jb is taken off (a drifting phase estimate moves jb)
-  const double jb = floor(kInv2Pi * p1);
-  auto rel_of = [&](double t, double c) { return floor(t) - floor(c) + jb; };
   // 1. guess.  With every m_k fixed at the floor the pass itself takes, a pass over a chunk IS
   // the loop's linear form x' = A x + u_k, so the chunk's response from zero state -- what the
   // scan needs -- is its end state less A^L times its start: z_j = x_end - Q x_start (the
@@ -837,13 +844,11 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
 #pragma unroll
       for (int u = 0; u < SB; ++u) {
         const int i = i0 + u;
-        const double c = cval(cd[u], k0 + i);
-        const double t = fma(-kInv2Pi, p, c);
-        const double r = rel_of(t, c);
+        const double t = fma(-kInv2Pi, p, cval(cd[u], k0 + i));
         const bool act = i < len;
-        bad |= act && !(r >= -127.0 && r <= 127.0);  // also a NaN constant (a 0 / NaN input)
-        if (act) mrel[i * CSTR + tid] = (int8_t)(bad ? 0.0 : r);
+        bad |= act && cd[u] == 2;                  // a 0 / NaN input: the general form's case
         const double f = __builtin_amdgcn_fract(t);
+        if (act) mrel[i * CSTR + tid] = floor_byte(t, f);
         const double S = p + V;
         const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
         V = act ? nV : V;
@@ -951,19 +956,17 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
           }
         }
         const int i = i0 + u;
-        const double c = cval(cd[u % (SB / 2)], k0 + i);
-        const double t = fma(-kInv2Pi, p, c);
-        const double r = rel_of(t, c);
+        const double t = fma(-kInv2Pi, p, cval(cd[u % (SB / 2)], k0 + i));
         const bool act = i < len;
-        miss |= act && r != (double)mm[u % (SB / 2)];   // (out of a byte's range: a miss, and so on)
         const double f = __builtin_amdgcn_fract(t);
+        const int8_t r = floor_byte(t, f);
+        miss |= act && r != mm[u % (SB / 2)];
         const double S = p + V;
         const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
         V = act ? nV : V;
         p = act ? np : p;
         if (act && k0 + i >= pre) mth = fminf(mth, (float)fmin(f, 1.0 - f));
-        if (act) mrel[i * CSTR + tid] = (int8_t)(r >= -127.0 && r <= 127.0 ? r : 0.0);
-        if (k0 + i == pre - 1) { x1s[0] = p; x1s[1] = V; }   // a pre-roll's state at the block start
+        if (act) mrel[i * CSTR + tid] = r;
         tw[u * TBS + lane] = thval(p, k0 + i);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -999,6 +1002,27 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
     if (tid == 0) printf("pll_spec q%d s%d n%ld T%d L%d TE%d round %d: %d chunks missed\n", q, s, (long)n, SPEC_T, L, TE, round, nmiss);
 #endif
     if (nmiss == 0) {
+      if constexpr (LONG) {
+        // a pre-roll's state at the block start (after step pre - 1): the thread whose chunk
+        // holds that step reruns its check steps up to it -- the same arithmetic, so the same
+        // state (a per-step test for it in the check loop cost the registers that spilled)
+        if (pre > 0) {
+          const int ic = (pre - 1) - k0;
+          if (ic >= 0 && ic < len) {
+            double p = xs_p, V = xs_v;
+            for (int i = 0; i <= ic; ++i) {
+              const double t = fma(-kInv2Pi, p, cval(code[i * CSTR + tid], k0 + i));
+              const double f = __builtin_amdgcn_fract(t);
+              const double S = p + V;
+              V = fma(kA, f, V - kB);
+              p = fma(kC, f, S);
+            }
+            x1s[0] = p;
+            x1s[1] = V;
+          }
+          __syncthreads();
+        }
+      }
       // done: the caller-visible results exactly as the loop kernels leave them
       if (tid == 0) {
         if (pre == 0) th[0] = thval(p1, 0);
@@ -1006,12 +1030,12 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
           J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];
           if (J.nco_q)
             J.nco_q[(int64_t)s * J.out_stride] =
-                (float)((off > 0.0) ? sin((w * off + st[1]) * cfg.scale + cfg.adj) : 0.0);
+                (float)((off > 0.0) ? sin((wsh * off + st[1]) * cfg.scale + cfg.adj) : 0.0);
         }
       }
       __syncthreads();                           // st[1], st[4] read before the last chunk writes st
       if (tid == TE - 1) {
-        const double arg = w * ((off + (double)(n - 1)) + 1.0) + p;
+        const double arg = wsh * ((off + (double)(n - 1)) + 1.0) + p;
         if constexpr (!LONG) th[n] = off;
         st_out[0] = V + kD;
         st_out[1] = p;
@@ -1025,7 +1049,7 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
           if (pre > 0) {                         // the pre-roll's state at the block start: its guess
             const double gpv = x1s[0], gvv = x1s[1];
             const double ofs = off + (double)(pre - 1);          // the previous step's trigOffset
-            const double arg = w * (ofs + 1.0) + gpv;
+            const double arg = wsh * (ofs + 1.0) + gpv;
             LB->g[0] = gvv + kD;
             LB->g[1] = gpv;
             LB->g[2] = cos(arg);
@@ -1448,10 +1472,10 @@ __global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
   if (k < P.n) {
     const float x = J.in[(int64_t)s * J.in_stride + k];
     odd = !(x > 0.f || x < 0.f);
-    const double cc = (x > 0.f ? 0.0 : kPi) - w * (off + (double)k);   // the previous step's w (off + k)
-    // a 0 / NaN input gets a NaN constant: a fast group over it ends in a NaN phase, which
-    // pll_chunk_kernel takes as its signal to redo the group in the general form
-    double cv = fma(cc, kInv2Pi, 0.5);
+    // pll_c (the previous step's w (off + k)); a 0 / NaN input gets a NaN constant: a fast
+    // group over it ends in a NaN phase, which pll_chunk_kernel takes as its signal to redo
+    // the group in the general form
+    double cv = fma(-(off + (double)k), w * kInv2Pi, x > 0.f ? 0.5 : 1.0);
     if (P.qform) {                                      // pll_chunk_kernel's Q-form
       const double i = (double)(k % PG);
       cv = cv + (kPi * J.cfg.ki) * kInv2Pi * (i * (i - 1.0) * 0.5);
@@ -1604,14 +1628,27 @@ hipError_t pll_check(const PllJobs& P, bool* vec) {
 
 namespace {
 // ---- long calls: host-side setup ---------------------------------------------------
-bool pll_long(const PllJobs& P) { return P.n > SPEC_NMAX; }
+// A per-block call is split the same way when it is long enough: pseudo-blocks of about
+// SDR_PLL_SPLIT steps (default 1 536; 0 = one workgroup per recurrence, the r03 per-block
+// solve).  A block's recurrence then runs on several workgroups (C4: 5 120 steps -> 4; C5:
+// 15 360 -> 10) instead of one, whose 256-512 threads' warm-ups were most of its time.
+int split_pb() {
+  static const int v = [] {
+    const char* e = getenv("SDR_PLL_SPLIT");
+    return e ? std::max(0, atoi(e)) : 1536;
+  }();
+  return v;
+}
+bool long_n(int64_t n) { return n > SPEC_NMAX || (split_pb() > 0 && n >= 2 * (int64_t)split_pb()); }
+bool pll_long(const PllJobs& P) { return long_n(P.n); }
 
 // pseudo-blocks of <= LONG_PB steps: with a pre-roll of <= LONG_PRE_MAX steps one solve is at
 // most SPEC_NMAX - 1 steps (its LDS image)
 constexpr int LONG_PRE_MAX = 2048;
 constexpr int LONG_PB = SPEC_NMAX - 1 - LONG_PRE_MAX;
 void long_geom(int64_t n, int64_t* pb, int* nb) {
-  const int64_t k = (n + LONG_PB - 1) / LONG_PB;
+  const int64_t per = n > SPEC_NMAX ? LONG_PB : split_pb();
+  const int64_t k = (n + per - 1) / per;
   *nb = (int)k;
   *pb = (n + k - 1) / k;
 }
@@ -1693,7 +1730,7 @@ hipError_t long_setup(PllJobs& L) {
 }  // namespace
 
 int64_t sdr_pll_work_bytes(int njobs, int nstreams, int64_t n) {
-  if (n <= SPEC_NMAX) return 0;
+  if (!long_n(n)) return 0;
   int64_t pb;
   int nb;
   long_geom(n, &pb, &nb);

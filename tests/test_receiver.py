@@ -12,7 +12,7 @@ Tolerances (f32 kernels vs the f64 oracle):
 import numpy as np
 import pytest
 
-from conftest import maxabs, rms
+from conftest import long_blocks, maxabs, rms
 
 pytestmark = pytest.mark.gpu
 
@@ -52,9 +52,10 @@ def test_receiver_c5_eight_streams_match_oracle(sdr, gpu_ctx, oracle):
             first = rx.pll_stats(reset=True)
     st = rx.pll_stats()
     print("solver counters, block 0:", first, "block 1:", st)
-    assert first["recurrences"] == 2 * S and st["recurrences"] == 2 * S
+    nb = long_blocks(B5 // 10)                       # pseudo-blocks per block and PLL
+    assert first["recurrences"] == 2 * S * nb and st["recurrences"] == 2 * S * nb
     # after the acquisition block every stereo and RDS recurrence completes in the parallel solve
-    assert st["spec_r0"] + st["spec_r1"] + st["spec_r2"] == 2 * S and st["sequential"] == 0, st
+    assert st["spec_r0"] + st["spec_r1"] + st["spec_r2"] == 2 * S * nb and st["sequential"] == 0, st
     worst = {}
     nco_worst = 0.0
     for s in range(S):

@@ -1,6 +1,3 @@
+# scratch GPU command: the full GPU suite + smoke, the default bench line, the C5 span trace
 set -e
-mkdir -p gpurun_out/r04_base
-O=gpurun_out/r04_base
-timeout -k 10 500 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
-timeout -k 10 200 python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > $O/smoke.log 2>&1
-timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err
+bash tools/gpu_round.sh gpurun_out/r04a tests bench prof:c5s8:--workload,c5,--streams,8,--span,256,--steps,5,--warmup,2,--no-cpu
