@@ -491,6 +491,36 @@ __device__ inline double unwrap_step_f64_m(double dd, int* w) {   // fe.hip unwr
   return ddmod;
 }
 
+// The phase of ONE decimated output m (10 m >= T - 1: no lfilter zi) of stream s, exactly as
+// a tile computes it: each tap digit's sum over the T samples in int32 (the matrix cores' sums
+// are exact, so the order does not matter), combined and taken through the same atan2.  A run
+// of tiles starting mid-stream needs the phase of the output before it (the demod's
+// predecessor); this replaces a whole warm-up tile (2 560 samples read and 24 MFMAs) with T
+// taps per channel over one wave.
+template <int T>
+__device__ __forceinline__ float output_phase(const unsigned char* iq_s, int64_t m, const float* taps, float qscale) {
+  const int lane = threadIdx.x;
+  int acc[2][3] = {};
+  for (int k = lane; k < T; k += 64) {
+    const int q = (int)rintf(taps[k] * qscale);
+    const unsigned short v = *reinterpret_cast<const unsigned short*>(iq_s + 2 * (D * m - k));
+    const int xi = (int)(signed char)((v & 0xff) ^ 0x80), xq = (int)(signed char)(((v >> 8) & 0xff) ^ 0x80);
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg) {
+      const int d = digit(q, dg);
+      acc[0][dg] += d * xi;
+      acc[1][dg] += d * xq;
+    }
+  }
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg) acc[ch][dg] = wave_sum_i(acc[ch][dg]);
+  const float yi = fmaf((float)acc[0][2], 65536.f, (float)(acc[0][1] * 256 + acc[0][0]));   // combine_digits
+  const float yq = fmaf((float)acc[1][2], 65536.f, (float)(acc[1][1] * 256 + acc[1][0]));
+  return fast_atan2f_x2(f2v{yq, yq}, f2v{yi, yi}).x;
+}
+
 template <int T>
 __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
   constexpr int KS = DemodShape<T>::KS, OFF = DemodShape<T>::OFF, K = 64 * KS;
@@ -587,9 +617,9 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
 
   int s = (int)(b0 / p.tps);
   int64_t t = b0 - (int64_t)s * p.tps;
-  const bool warm = t > 0;
-  if (warm) --t;
-  const int64_t U = (b1 - b0) + (warm ? 1 : 0);
+  const int64_t U = b1 - b0;
+  // the run's first tile continues the stream: the phase of the output before it
+  float carry = t > 0 ? output_phase<T>(p.iq + 2 * (int64_t)s * p.stride, TO * t - 1, p.taps, p.qscale) : 0.f;
   if (interior(t)) {
     load_image(s, t, false);
     store_image(false);
@@ -599,7 +629,6 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
   int s_nx = s;
   int64_t t_nx = t + 1;
   if (t_nx == p.tps) { t_nx = 0; ++s_nx; }
-  float carry = 0.f;
   int wsum = 0;
   const double zscale = (double)p.qscale * 128.0;    // real-domain zi -> the integer sum's scale
 
@@ -654,7 +683,7 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
     const int src = gl > 0 ? lane - 16 : (pl > 0 ? lane + 47 : 63);
     const float left = __uint_as_float(bperm(src, __float_as_uint(phi[3])));
     float prev = (lane == 0) ? carry : left;
-    const bool keep = !(warm && u == 0);
+    constexpr bool keep = true;
     float d[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -736,9 +765,9 @@ hipError_t launch_demod_mfma_t(const FeLaunch& a, hipStream_t st) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_demod_kernel<T>, 64, 0) != hipSuccess || per <= 0) per = 1;
     return device_cus() * std::min(per, 12);
   });
-  // the resident waves share the tiles in runs of >= 2 (a run's warm-up tile is at most a third of
-  // its work; at span sizes, 1/60)
-  const int64_t run = std::max<int64_t>(2, (p.total + slots - 1) / slots);
+  // the resident waves share the tiles in contiguous runs (a run's first tile takes its
+  // predecessor phase from output_phase: no warm-up tile, so a run may be one tile)
+  const int64_t run = std::max<int64_t>(1, (p.total + slots - 1) / slots);
   const int64_t grid = std::max<int64_t>(1, (p.total + run - 1) / run);
   hipLaunchKernelGGL(fe_mfma_demod_kernel<T>, dim3((unsigned)grid), dim3(64), 0, st, p);
   return hipGetLastError();
