@@ -743,6 +743,43 @@ def rx_measure(ctx, workload, args, rank, ws, steps, warmup, cpu=False):
 
 C5_B = 153_600                 # complex samples per reference block (src/fm_radio.cpp:23)
 VALU_PEAK_TFLOPS = 157.3       # MI355X FP32 vector peak (MI355X_MICROARCH.md)
+# f64 VALU issue: a wave64 f64 instruction holds its SIMD 4 cycles (half the f32 rate: 78.6
+# TFLOP/s FMA), 256 CUs x 4 SIMDs x 2.4 GHz / 4 (tools/f64_probe.hip measured a lone wave at
+# ~4.5 cycles per f64 op, dependent or not)
+F64_WAVE_INSTR_PEAK = 256 * 4 * 2.4e9 / 4
+
+
+def pll_roofline(stage_ms_pll, S, K, B, steps_per_span, path=None):
+    """The PLL stage against the f64 VALU issue rate, from committed SQ counts of its kernels
+    (tools/pmc_pll.py over rocprofv3 --pmc passes of the same configuration) and the stage time
+    measured in this run.  None when no counts for this configuration are committed."""
+    path = path or os.path.join(ROOT, "profiles", "r04", "pll_pmc.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("config", {}).get("streams") != S or t.get("config", {}).get("span") != K:
+        return None
+    f64 = valu = 0.0
+    names = []
+    for k, c in t["kernels"].items():
+        if not ("pll_spec" in k or "pll_long" in k):
+            continue
+        names.append(k)
+        f64 += sum(c.get(n, 0.0) for n in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                             "SQ_INSTS_VALU_TRANS_F64"))
+        valu += c.get("SQ_INSTS_VALU", 0.0)
+    if not names or stage_ms_pll <= 0:
+        return None
+    rate = f64 / (stage_ms_pll * 1e-3)
+    return {"bound": "f64 VALU issue", "achieved": round(rate / 1e9, 2), "peak": round(F64_WAVE_INSTR_PEAK / 1e9, 1),
+            "unit": "G f64 wave-instr/s", "frac": round(rate / F64_WAVE_INSTR_PEAK, 4),
+            "f64_wave_instr_per_span": f64, "valu_wave_instr_per_span": valu,
+            "f64_lane_ops_per_step": round(64 * f64 / steps_per_span, 2),
+            "valu_lane_ops_per_step": round(64 * valu / steps_per_span, 2),
+            "kernels": names, "stage_ms": stage_ms_pll,
+            "source": os.path.relpath(path, ROOT) + " (SQ counts per dispatch) + this run's PLL stage time"}
 
 
 def chain_flops_per_sample(rf_taps=151, taps=151, audio_decim=5, up=19, down=80):
@@ -834,6 +871,9 @@ def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, arg
                            ("HBM: IQ in, demod out" if dom == "fe" else "FP32 VALU: FIR multiply-adds")},
         "pll_solver": pll,
     }
+    pr = pll_roofline(stage_ms.get("pll", 0.0), S, K, B, (2 if rds else 1) * S * (n // 10)) if stereo else None
+    if pr is not None:
+        out["pll_roofline"] = pr
     if fps is not None:
         per_gpu_tflops = fps * S * n * steps / elapsed / 1e12
         out["roofline"] = {"bound": "valu", "achieved": round(per_gpu_tflops, 3), "peak": VALU_PEAK_TFLOPS,
