@@ -1197,6 +1197,8 @@ __device__ int chain_pass(const PllJobs& P, const int r) {
   __shared__ double wtot[NWV];
   __shared__ int wfa[NWV];
   __shared__ int spos;
+  __shared__ Mat2 fpw[10];                 // Phi^(2^i): Phi = A^pb, the loop over one pseudo-block
+  __shared__ double wY[2][NWV];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nb = P.lg.nb;
   LongHdr* H = long_hdr(P, r);
@@ -1211,6 +1213,12 @@ __device__ int chain_pass(const PllJobs& P, const int r) {
   double* st = J.state + (int64_t)s * 6;
   const double off0 = st[5];
   const int64_t pb = P.lg.pb;
+  if (tid == 0) {
+    const double* pp = P.lg.phi[q];
+    Mat2 x{pp[0], pp[1], pp[2], pp[3]};
+    for (int i = 0; i < 10; ++i, x = mmul(x, x)) fpw[i] = x;
+  }
+  __syncthreads();
   double Cp = H->sp, Ci = H->si;     // the carried (exact) start of the window's first block
   int pos = pos0;
   double Xp = Cp, Xi = Ci;           // the exact state at `pos`
@@ -1264,15 +1272,54 @@ __device__ int chain_pass(const PllJobs& P, const int r) {
     __syncthreads();
     for (int i = 0; i < wv; ++i) pre_dn += wtot[i];
     const double nj = n0 + (pre_dn - dn);
-    // rho_j: block 0 the carried one; block l: C_{l-1} + Phi_{l-1} C_{l-2} (block 1: ... rho_0)
+    // rho_l = C_{l-1} + Phi rho_{l-1} (rho_0: the carried residual), exactly: with the inclusive
+    // scan Y_l = sum_{i<=l} Phi^(l-i) C_i, rho_l = Y_{l-1} + Phi^l rho_0.  (Phi = A^pb is tiny
+    // for the long calls' 14 336-step pseudo-blocks -- there rho_l = C_{l-1} + Phi C_{l-2}
+    // already -- but not for a split per-block call's ~1 500-step ones on the RDS loop,
+    // where Phi ~ 0.1: its powers must be carried.)
     double rp, rv;
-    if (tid == 0) { rp = r0p; rv = r0v; }
-    else {
-      const double* pp = P.lg.phi[q];                // Phi_{l-1}: l - 1 < nb - 1
-      const double pcp = sC[0][tid - 1], pcv = sC[1][tid - 1];
-      const double qp = tid == 1 ? r0p : sC[0][tid - 2], qv = tid == 1 ? r0v : sC[1][tid - 2];
-      rp = pcp + (pp[0] * qp + pp[1] * qv);
-      rv = pcv + (pp[2] * qp + pp[3] * qv);
+    {
+      double yp = cp, yv = cv;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int o = 1 << i;
+        const double up = __shfl_up(yp, o, 64), uv = __shfl_up(yv, o, 64);
+        if (lane >= o) {
+          const Mat2 F = fpw[i];
+          yp = yp + (F.a * up + F.b * uv);
+          yv = yv + (F.c * up + F.d * uv);
+        }
+      }
+      if (lane == 63) { wY[0][wv] = yp; wY[1][wv] = yv; }
+      __syncthreads();
+      double cwp = 0.0, cwv = 0.0;                   // Y at the end of the previous wave
+      for (int i = 0; i < wv; ++i) {
+        const Mat2 F = fpw[6];                       // Phi^64
+        const double np = wY[0][i] + (F.a * cwp + F.b * cwv), nv = wY[1][i] + (F.c * cwp + F.d * cwv);
+        cwp = np; cwv = nv;
+      }
+      {
+        Mat2 Fl{1.0, 0.0, 0.0, 1.0};                 // Phi^(lane + 1)
+        for (int i = 0, e = lane + 1; e > 0; ++i, e >>= 1)
+          if (e & 1) Fl = mmul(Fl, fpw[i]);
+        yp = yp + (Fl.a * cwp + Fl.b * cwv);
+        yv = yv + (Fl.c * cwp + Fl.d * cwv);
+      }
+      // Y_{tid-1}: the previous lane's (lane 0: the previous wave's last, through LDS)
+      double vp = __shfl_up(yp, 1, 64), vv = __shfl_up(yv, 1, 64);
+      __syncthreads();                               // wY read before it is rewritten
+      if (lane == 63) { wY[0][wv] = yp; wY[1][wv] = yv; }
+      __syncthreads();
+      if (lane == 0) {
+        vp = wv > 0 ? wY[0][wv - 1] : 0.0;
+        vv = wv > 0 ? wY[1][wv - 1] : 0.0;
+      }
+      Mat2 Ft{1.0, 0.0, 0.0, 1.0};                   // Phi^tid
+      for (int i = 0, e = tid; e > 0; ++i, e >>= 1)
+        if (e & 1) Ft = mmul(Ft, fpw[i]);
+      rp = vp + (Ft.a * r0p + Ft.b * r0v);
+      rv = vv + (Ft.c * r0p + Ft.d * r0v);
+      if (tid == 0) { rp = r0p; rv = r0v; }
     }
     const double err = c1 * fabs(rp) + c2 * fabs(rv);
     // accepted: the solve started within LONG_ACCEPT of the chained start, or within the linear

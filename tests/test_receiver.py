@@ -52,10 +52,10 @@ def test_receiver_c5_eight_streams_match_oracle(sdr, gpu_ctx, oracle):
             first = rx.pll_stats(reset=True)
     st = rx.pll_stats()
     print("solver counters, block 0:", first, "block 1:", st)
-    nb = long_blocks(B5 // 10)                       # pseudo-blocks per block and PLL
-    assert first["recurrences"] == 2 * S * nb and st["recurrences"] == 2 * S * nb
+    npb = long_blocks(B5 // 10)                      # pseudo-blocks per block and PLL
+    assert first["recurrences"] == 2 * S * npb and st["recurrences"] == 2 * S * npb
     # after the acquisition block every stereo and RDS recurrence completes in the parallel solve
-    assert st["spec_r0"] + st["spec_r1"] + st["spec_r2"] == 2 * S * nb and st["sequential"] == 0, st
+    assert st["spec_r0"] + st["spec_r1"] + st["spec_r2"] == 2 * S * npb and st["sequential"] == 0, st
     worst = {}
     nco_worst = 0.0
     for s in range(S):
