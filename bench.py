@@ -625,7 +625,11 @@ def rx_measure(ctx, workload, args, rank, ws, steps, warmup, cpu=False):
             step(settle)
             settle += 1
         ctx.synchronize()
-    # per-stage GPU times (events between the receiver's launches), a separate pass
+    # per-stage GPU times (events between the receiver's launches), a separate pass -- on a
+    # receiver past its stream's first blocks (the PLLs' acquisition block runs sequentially)
+    if not c5 and rx_sync is not rx:
+        for k in range(4):
+            sync_step(k)
     (rx if c5 else rx_sync).set_timing(True)
     stages = []
     for k in range(8):

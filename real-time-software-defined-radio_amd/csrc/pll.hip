@@ -86,31 +86,52 @@ __device__ inline double reduce_2pi(double a) {
 // rounding): quadrant n = rint(a 2/pi) (a two-part pi/2: exact to ~1e-32 for |n| <= 2), then
 // Taylor polynomials on |y| <= pi/4 to y^13 / y^14 (truncation < 3e-14).  ~35 VALU against
 // the library sincos's general-argument path.
+// OPAQUE: each coefficient is made an SGPR at its use (a volatile asm): in kernels that call
+// this once per call (end states) the compiler otherwise keeps all 14 in VGPRs for the whole
+// kernel, which spilled the long-call fix kernel
+template <bool OPAQUE = false>
 __device__ __forceinline__ void sincos_red(double a, double* sv, double* cv) {
+  auto K = [](double c) {
+    if constexpr (OPAQUE) asm volatile("" : "+s"(c));
+    return c;
+  };
   constexpr double kPio2Hi = 1.5707963267948966, kPio2Lo = 6.123233995736766e-17, k2oPi = 0.6366197723675814;
   const double n = rint(a * k2oPi);
   double y = fma(-n, kPio2Hi, a);
   y = fma(-n, kPio2Lo, y);
   const double z = y * y;
-  double ps = 1.0 / 6227020800.0;                        // 1/13!
-  ps = fma(ps, z, -1.0 / 39916800.0);
-  ps = fma(ps, z, 1.0 / 362880.0);
-  ps = fma(ps, z, -1.0 / 5040.0);
-  ps = fma(ps, z, 1.0 / 120.0);
-  ps = fma(ps, z, -1.0 / 6.0);
+  double ps = K(1.0 / 6227020800.0);                        // 1/13!
+  ps = fma(ps, z, K(-1.0 / 39916800.0));
+  ps = fma(ps, z, K(1.0 / 362880.0));
+  ps = fma(ps, z, K(-1.0 / 5040.0));
+  ps = fma(ps, z, K(1.0 / 120.0));
+  ps = fma(ps, z, K(-1.0 / 6.0));
   const double sn = fma(ps * z, y, y);
-  double pc = 1.0 / 87178291200.0;                       // 1/14!
-  pc = fma(pc, z, -1.0 / 479001600.0);
-  pc = fma(pc, z, 1.0 / 3628800.0);
-  pc = fma(pc, z, -1.0 / 40320.0);
-  pc = fma(pc, z, 1.0 / 720.0);
-  pc = fma(pc, z, -1.0 / 24.0);
-  pc = fma(pc, z, 0.5);
+  double pc = K(1.0 / 87178291200.0);                       // 1/14!
+  pc = fma(pc, z, K(-1.0 / 479001600.0));
+  pc = fma(pc, z, K(1.0 / 3628800.0));
+  pc = fma(pc, z, K(-1.0 / 40320.0));
+  pc = fma(pc, z, K(1.0 / 720.0));
+  pc = fma(pc, z, K(-1.0 / 24.0));
+  pc = fma(pc, z, K(0.5));
   const double cs = fma(-pc, z, 1.0);
   const int q = (int)n & 3;
   const double s0 = (q & 1) ? cs : sn, c0 = (q & 1) ? sn : cs;
   *sv = (q == 2 || q == 3) ? -s0 : s0;
   *cv = (q == 1 || q == 2) ? -c0 : c0;
+}
+
+// A call's end state from its last angle arg (fmPll.py:39-44): feedbackI/Q = cos/sin(arg) and
+// ncoOut[-1] = cos(arg scale + adj), through the NCO kernels' reduction -- so the next call's
+// ncoOut[0] is this call's last NCO value bit for bit, and a growing angle never takes the
+// library's large-argument path.
+__device__ __forceinline__ void end_trig(double arg, double scale, double adj, double* st) {
+  double sv, cv;
+  sincos_red<true>(reduce_2pi(arg), &sv, &cv);
+  st[2] = cv;
+  st[3] = sv;
+  sincos_red<true>(reduce_2pi(arg * scale + adj), &sv, &cv);
+  st[4] = cv;
 }
 
 // The loop's per-sample constant (pll_prep_kernel's, plain form): c_k = (sel_k - w (off + k)) / 2pi
@@ -266,9 +287,7 @@ __global__ __launch_bounds__(64) void pll_lanes_kernel(PllJobs P) {
   if (n > 0) {
     st[0] = integ;
     st[1] = phase;
-    st[2] = cos(arg);
-    st[3] = sin(arg);
-    st[4] = cos(arg * cfg.scale + cfg.adj);
+    end_trig(arg, cfg.scale, cfg.adj, st);
     st[5] = off + (double)n;
     stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
     stat_add(P.stats, SDR_PLL_ST_SEQUENTIAL, 1);
@@ -454,9 +473,7 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
     if (n > 0) {
       st[0] = integ;
       st[1] = phase;
-      st[2] = cos(arg);
-      st[3] = sin(arg);
-      st[4] = cos(arg * cfg.scale + cfg.adj);
+      end_trig(arg, cfg.scale, cfg.adj, st);
       st[5] = off + (double)n;
       stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
       stat_add(P.stats, SDR_PLL_ST_SEQUENTIAL, 1);
@@ -492,9 +509,12 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 // recurrence is marked by c[0] = +inf (c[0] is the literal sample's slot: the loop kernels
 // never read it, and the prep kernel rewrites it every call).
 #ifndef SDR_SPEC_W
-#define SDR_SPEC_W 128
+#define SDR_SPEC_W 32
 #endif
-// warm-up samples before each chunk (A/B builds: -DSDR_SPEC_W=).  r03, per-block solves at 64
+// warm-up samples before each chunk (A/B builds: -DSDR_SPEC_W=).  r04: 32 -- the guess runs
+// the true step from the measured drift, and in the per-block solve of one recurrence (C4, a
+// 256-thread workgroup: one wave per SIMD, no other wave to hide the f64 latency behind) the
+// 128-step warm-up was 40 % of the kernel (spec_prof: 22 k of 52 k cycles).  r03, per-block solves at 64
 // streams x 2 PLLs (profiles/r03/iter/specw_*): 256 -> 86 us, 128 -> 73 us, 64 -> 66 us per
 // block, every recurrence in round 0 at each, the offset sweep (tests/test_offsets.py) too;
 // 128 keeps a margin for inputs noisier than the synthetic ones
@@ -579,7 +599,7 @@ __device__ __forceinline__ Mat2 mpow2(Mat2 x, int e) {
 // calls): the call's first solve -- the pseudo-block records are not initialised yet (the
 // bookkeeping is done here, for this block, instead of by a kernel of its own).
 template <int SPEC_T, bool LONG, bool first = false>
-__device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const int tid) {
+__device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const int tid) {
 #pragma clang fp contract(off)
   // Per step k = 1 .. n-1, at slot i * CSTR + j (step i of chunk j, see the staging below):
   // the sign code of x_k (0: x > 0, 1: x < 0, 2: 0 / NaN) -- the constant c_k is a function
@@ -642,7 +662,7 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
       }
     } else {
       status = LB->status;
-      if (status != LB_NEED_G && status != LB_NEED_X) return;
+      if (status != LB_NEED_G && status != LB_NEED_X) return true;
     }
     base = (int64_t)b * P.lg.pb;
     n = long_len(P, b);
@@ -776,7 +796,7 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
       const int j = tid + o;
       if (j >= 0 && j < TE) { sr += yb[j].x; si += yb[j].y; }
     }
-    const double ang = atan2(si, sr);
+    const double ang = (double)atan2f((float)si, (float)sr);   // (a guess: f32 is plenty)
     if (pre > 0 && tid == 0) {                   // the pre-roll's seed: measured phase, span's integrator
       x1s[0] = ang;
       x1s[1] = st_call[0] - kD;
@@ -858,7 +878,7 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
     xe_p = p;                                    // ... and its end
     xe_v = V;
   }
-  if (__syncthreads_or(bad)) return;             // a 0 / NaN input (the general form's case)
+  if (__syncthreads_or(bad)) return false;       // a 0 / NaN input (the general form's case)
   SPEC_TP();
   // Q = A^L and its squarings Q^(2^i), i < 10 (thread 0, into LDS: the scans read them as
   // broadcasts instead of holding them in registers)
@@ -994,7 +1014,7 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
     const int nmiss = __syncthreads_count(miss);
     SPEC_TP();
 #ifdef SDR_PLL_SPEC_PROF
-    if (tid == 0 && nmiss == 0 && (bid % 479) == 3)
+    if (tid == 0 && nmiss == 0 && (bid == 0 || (bid % 479) == 3))
       printf("spec_prof blk %d L %d: stage %lld corr %lld guess %lld solve %lld check %lld (%d marks)\n", bid, L,
              tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], ntp);
 #endif
@@ -1039,9 +1059,7 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
         if constexpr (!LONG) th[n] = off;
         st_out[0] = V + kD;
         st_out[1] = p;
-        st_out[2] = cos(arg);
-        st_out[3] = sin(arg);
-        st_out[4] = cos(arg * cfg.scale + cfg.adj);
+        end_trig(arg, cfg.scale, cfg.adj, st_out);
         st_out[5] = off + (double)n;
       }
       if (tid == 0) {
@@ -1052,8 +1070,10 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
             const double arg = wsh * (ofs + 1.0) + gpv;
             LB->g[0] = gvv + kD;
             LB->g[1] = gpv;
-            LB->g[2] = cos(arg);
-            LB->g[3] = sin(arg);
+            double sv, cv;
+            sincos_red<true>(reduce_2pi(arg), &sv, &cv);
+            LB->g[2] = cv;
+            LB->g[3] = sv;
             LB->g[4] = 0.0;
             LB->g[5] = off + (double)pre;
             LB->u[0] = gvv + kD;
@@ -1074,14 +1094,44 @@ __device__ __forceinline__ void spec_body(const PllJobs& P, const int bid, const
           stat_add(P.stats, SDR_PLL_ST_SPEC_R0 + round, 1);
         }
       }
-      return;
+      return true;
     }
   }
+  return false;
+}
+
+__device__ void seq_run(const PllCfg& cfg, const float* in, double* th, int64_t n, const double* st, double* so);
+
+// A per-block call's recurrence the solve does not complete (a 0 / NaN input, a loop not yet
+// locked) runs sequentially in the same workgroup (one thread, seq_run's general form) --
+// no prep / loop kernels behind the solve, so a per-block PLL call is this launch and the NCO's.
+__device__ void spec_fallback(const PllJobs& P, const int bid) {
+#pragma clang fp contract(off)
+  const int q = bid / P.nstreams, s = bid - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const PllCfg cfg = J.cfg;
+  double* st = J.state + (int64_t)s * 6;
+  double* th = J.theta + (int64_t)s * J.th_stride;
+  const double off = st[5];
+  const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
+  J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];
+  if (J.nco_q)
+    J.nco_q[(int64_t)s * J.out_stride] = (float)((off > 0.0) ? sin((w * off + st[1]) * cfg.scale + cfg.adj) : 0.0);
+  double so[6];
+  seq_run(cfg, J.in + (int64_t)s * J.in_stride, th, P.n, st, so);
+  th[P.n] = off;                                   // the NCO kernel's trigOffset
+  for (int i = 0; i < 6; ++i) st[i] = so[i];
+  stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
+  stat_add(P.stats, SDR_PLL_ST_SEQUENTIAL, 1);
 }
 
 template <int SPEC_T, bool LONG>
 __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T == 512 ? 4 : 2))) void pll_spec_kernel(PllJobs P) {
-  spec_body<SPEC_T, LONG, LONG>(P, (int)blockIdx.x, (int)threadIdx.x);   // (a long call's first solve of every block)
+  // (LONG: a long call's first solve of every block, which also initialises its record)
+  const bool done = spec_body<SPEC_T, LONG, LONG>(P, (int)blockIdx.x, (int)threadIdx.x);
+  if constexpr (!LONG) {
+    if (!done && P.lpw == 0 && threadIdx.x == 0) spec_fallback(P, (int)blockIdx.x);
+  }
 }
 
 // ================================================================================
@@ -1151,8 +1201,7 @@ __device__ void seq_run(const PllCfg& cfg, const float* in, double* th, int64_t 
         double fI = st[2], fQ = st[3];
         if (k > 0) {
           const double arg = w * ((off + (double)(k - 1)) + 1.0) + phase;
-          fI = cos(arg);
-          fQ = sin(arg);
+          sincos_red<true>(reduce_2pi(arg), &fQ, &fI);
         }
         e = atan2(xv * (-fQ), xv * fI);
       } else {
@@ -1169,9 +1218,7 @@ __device__ void seq_run(const PllCfg& cfg, const float* in, double* th, int64_t 
   const double arg = w * ((off + (double)(n - 1)) + 1.0) + phase;
   so[0] = integ;
   so[1] = phase;
-  so[2] = cos(arg);
-  so[3] = sin(arg);
-  so[4] = cos(arg * cfg.scale + cfg.adj);
+  end_trig(arg, cfg.scale, cfg.adj, so);
   so[5] = off + (double)n;
 }
 
@@ -1376,8 +1423,7 @@ __device__ int chain_pass(const PllJobs& P, const int r) {
         const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + sp;
         B->x[0] = si;
         B->x[1] = sp;
-        B->x[2] = cos(arg);
-        B->x[3] = sin(arg);
+        sincos_red<true>(reduce_2pi(arg), &B->x[3], &B->x[2]);
         B->x[4] = 0.0;
         B->x[5] = off0 + (double)((int64_t)j * pb);
       }
@@ -1418,9 +1464,7 @@ __device__ int chain_pass(const PllJobs& P, const int r) {
       const double arg = w * ((offl + (double)(long_len(P, nb - 1) - 1)) + 1.0) + Xp;
       st[0] = Xi;
       st[1] = Xp;
-      st[2] = cos(arg);
-      st[3] = sin(arg);
-      st[4] = cos(arg * cfg.scale + cfg.adj);
+      end_trig(arg, cfg.scale, cfg.adj, st);
       st[5] = off0 + (double)P.n;
     }
     spos = pos;
@@ -1453,7 +1497,8 @@ __device__ void long_tail(const PllJobs& P, const int r, const int pos) {
   } else {
     const double offp = off0 + (double)(base - pb);
     const double arg = w * ((offp + (double)(pb - 1)) + 1.0) + H->sp;
-    s0[0] = H->si; s0[1] = H->sp; s0[2] = cos(arg); s0[3] = sin(arg); s0[4] = 0.0; s0[5] = off0 + (double)base;
+    s0[0] = H->si; s0[1] = H->sp; s0[4] = 0.0; s0[5] = off0 + (double)base;
+    sincos_red<true>(reduce_2pi(arg), &s0[3], &s0[2]);
   }
   double so[6];
   seq_run(cfg, J.in + (int64_t)s * J.in_stride + base, J.theta + (int64_t)s * J.th_stride + base, P.n - base, s0,
@@ -1660,6 +1705,9 @@ bool pll_spec_enabled() {
   static const bool on = [] { const char* e = getenv("SDR_PLL_SPEC"); return !(e && e[0] == '0'); }();
   return on;
 }
+// a per-block call solved by pll_spec_kernel alone (its own sequential fallback): no prep or
+// loop kernel, plain (not Q-form) phase rows
+bool spec_only(const PllJobs& P) { return pll_spec_enabled() && P.n >= 2; }
 hipError_t pll_check(const PllJobs& P, bool* vec) {
   if (P.njobs < 1 || P.njobs > SDR_PLL_MAXJ || P.nstreams <= 0 || P.n < 0) return hipErrorInvalidValue;
   *vec = true;
@@ -1676,13 +1724,13 @@ hipError_t pll_check(const PllJobs& P, bool* vec) {
 namespace {
 // ---- long calls: host-side setup ---------------------------------------------------
 // A per-block call is split the same way when it is long enough: pseudo-blocks of about
-// SDR_PLL_SPLIT steps (default 1 536; 0 = one workgroup per recurrence, the r03 per-block
+// SDR_PLL_SPLIT steps (default 0 = off: one workgroup per recurrence, the per-block
 // solve).  A block's recurrence then runs on several workgroups (C4: 5 120 steps -> 4; C5:
 // 15 360 -> 10) instead of one, whose 256-512 threads' warm-ups were most of its time.
 int split_pb() {
   static const int v = [] {
     const char* e = getenv("SDR_PLL_SPLIT");
-    return e ? std::max(0, atoi(e)) : 1536;
+    return e ? std::max(0, atoi(e)) : 0;
   }();
   return v;
 }
@@ -1789,7 +1837,7 @@ hipError_t sdr_launch_pll_prep(const PllJobs& P, hipStream_t st) {
   bool vec;
   const hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
-  if (pll_long(P)) return hipSuccess;      // long calls compute their constants where they use them (pll_c)
+  if (pll_long(P) || spec_only(P)) return hipSuccess;   // the solve computes its constants where it uses them (pll_c)
   PllJobs L = P;
   L.qform = !pll_long(P) && vec && pll_lpw(P) == 1;
   if (P.n > 0)
@@ -1813,14 +1861,19 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     hipLaunchKernelGGL(pll_long_fix_kernel, dim3((unsigned)R), dim3(CHAIN_T), 0, st, L);
     return hipGetLastError();
   }
-  L.lpw = pll_lpw(P);
-  L.qform = vec && L.lpw == 1;
-  const dim3 grid((unsigned)(L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw)));
-  if (pll_spec_enabled() && L.n >= 2) {
+  if (spec_only(P)) {
+    // one launch: every recurrence solved in parallel, or sequentially in its own workgroup
+    // when the solve cannot complete it (lpw = 0 tells the kernel so)
+    L.lpw = 0;
+    L.qform = 0;
     const dim3 g((unsigned)(L.njobs * L.nstreams));
     if (L.n > 10240) hipLaunchKernelGGL((pll_spec_kernel<512, false>), g, dim3(512), 0, st, L);
     else hipLaunchKernelGGL((pll_spec_kernel<256, false>), g, dim3(256), 0, st, L);
+    return hipGetLastError();
   }
+  L.lpw = pll_lpw(P);
+  L.qform = vec && L.lpw == 1;
+  const dim3 grid((unsigned)(L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw)));
   if (vec && L.lpw == 1) hipLaunchKernelGGL(pll_chunk_kernel, grid, dim3(128), 0, st, L);
   else if (vec) hipLaunchKernelGGL(pll_lanes_kernel<true>, grid, dim3(64), 0, st, L);
   else hipLaunchKernelGGL(pll_lanes_kernel<false>, grid, dim3(64), 0, st, L);
@@ -1832,7 +1885,7 @@ hipError_t sdr_launch_pll_nco(const PllJobs& P, hipStream_t st) {
   hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
   PllJobs L = P;
-  L.qform = !pll_long(P) && vec && pll_lpw(P) == 1;
+  L.qform = !pll_long(P) && !spec_only(P) && vec && pll_lpw(P) == 1;
   if (pll_long(P)) {
     e = long_setup(L);
     if (e != hipSuccess) return e;

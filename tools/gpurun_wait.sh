@@ -8,7 +8,7 @@ log=$1; to=$2; cmd=$3; tries=${4:-12}
 for i in $(seq 1 "$tries"); do
   timeout $((to + 1500)) /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
   rc=$?
-  if grep -q "no free box right now\|backing off\|stopped responding while being prepared" "$log" && \
+  if grep -q "no free box right now\|backing off\|stopped responding while being prepared\|slot(s) on this pod are busy\|nothing was charged" "$log" && \
      ! grep -q "status=\(ok\|fail\|error\|timeout\)" "$log"; then
     wait_s=$(grep -o "retry in [0-9]*s" "$log" | grep -o "[0-9]*" | tail -1)
     echo "try $i: no box; waiting ${wait_s:-240}s" >> "$log.tries"
