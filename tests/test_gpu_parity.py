@@ -382,6 +382,20 @@ def test_fm_mono_streams_u8_mfma(sdr, gpu_ctx, oracle, n):
                                                                                  maxabs(got[s], ref))
 
 
+def test_fm_mono_streams_u8_mfma_long_runs(sdr, gpu_ctx, oracle):
+    """48 streams (19 440 tiles: runs of 6-7 tiles per wave on 256 CUs, so runs hold whole
+    audio blocks queued between the two blocks their ends cut, and cross stream ends) == the
+    f64 oracle on three of them."""
+    rf_b, au_b = sdr.design.mono_coeffs(101, 151)
+    S, n = 48, 1_024_000 + 16
+    iq = np.stack([sdr.synth.fm_iq(n, seed=200 + s, dtype=np.uint8) for s in range(S)])
+    got = sdr.fm_mono_streams(iq, rf_b, au_b)
+    for s in (0, 17, S - 1):
+        ref, _ = oracle.mono_basic_coeffs((iq[s].astype(np.float64) - 128.0) / 128.0, rf_b, au_b)
+        assert got[s].shape == ref.shape
+        assert rms(got[s], ref) < AUDIO_RMS and maxabs(got[s], ref) < AUDIO_MAX, (s, rms(got[s], ref))
+
+
 @pytest.mark.parametrize("gain", [37.0, 1e-3])
 def test_fm_mono_streams_u8_mfma_tap_scale(sdr, gpu_ctx, oracle, gain):
     """The int8-MFMA front end quantises the taps against their largest magnitude (2^S), so a
