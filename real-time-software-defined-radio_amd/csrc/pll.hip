@@ -1606,7 +1606,7 @@ __global__ void nco_jobs_kernel(PllJobs P) {
   // 3-part Cody-Waite step (exact multiples of 2 pi for |n| < 2^26), sincos then takes its
   // small-argument path instead of the large-argument reduction
   double sv, cv;
-  sincos_red(reduce_2pi(a), &sv, &cv);
+  sincos_red<true>(reduce_2pi(a), &sv, &cv);
   J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
   if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
 }
@@ -1615,12 +1615,14 @@ __global__ void nco_jobs_kernel(PllJobs P) {
 // The NCO of a long call: phaseEst_k = the stored phase + 2 pi (the chain's turns for its
 // pseudo-block) + (A^(kk+1) d)_phase, the loop's linear response to the start error d the
 // chain accepted the pseudo-block with (kk: the step within it; zero for most blocks).
-// Workgroup: 256 x NCO_NR consecutive steps of one recurrence, thread t the steps t + 256 i
-// (coalesced), its responses 256 steps apart by A^256; A^(2^i) in LDS.
+// Workgroup: 256 x NCO_NR consecutive steps of ONE pseudo-block (grid.x = pseudo-blocks x
+// tiles per block), thread t the steps t + 256 i (coalesced): the shift and d are uniform and
+// the response branch with them; its responses 256 steps apart by A^256, A^(2^i) in LDS.
 #ifndef SDR_NCO_NR
 #define SDR_NCO_NR 8
 #endif
 constexpr int NCO_NR = SDR_NCO_NR;     // outputs per thread of nco_long_kernel (A/B builds: -DSDR_NCO_NR=)
+__host__ __device__ inline int nco_tiles_per_block(int64_t pb) { return (int)((pb + 256 * NCO_NR - 1) / (256 * NCO_NR)); }
 __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
 #pragma clang fp contract(off)
   __shared__ Mat2 ap[15];
@@ -1629,63 +1631,62 @@ __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
   const int s = g - q * P.nstreams;
   const PllJob& J = P.j[q];
   const PllCfg cfg = J.cfg;
-  if (threadIdx.x == 0) {
-    Mat2 x{1.0 - (k2Pi * (cfg.kp + cfg.ki)) * kInv2Pi, 1.0, -(k2Pi * cfg.ki) * kInv2Pi, 1.0};
-    for (int i = 0; i < 15; ++i, x = mmul(x, x)) ap[i] = x;
+  const int64_t pb = P.lg.pb;
+  const int tpb = nco_tiles_per_block(pb);
+  const int b = (int)blockIdx.x / tpb;
+  const int64_t kb = (int64_t)b * pb;                          // the pseudo-block's first step
+  const int64_t kk0 = (int64_t)((int)blockIdx.x - b * tpb) * (256 * NCO_NR);
+  const int64_t len = min(pb, P.n - kb);
+  if (kk0 >= len) return;                                      // uniform
+  const LongBlk* B = long_blk(P, g, b);
+  const double sh = B->shift;
+  double vp = B->d[0], vv = B->d[1];
+  const bool lin = vp != 0.0 || vv != 0.0;                     // uniform
+  if (lin) {
+    if (threadIdx.x == 0) {
+      Mat2 x{1.0 - (k2Pi * (cfg.kp + cfg.ki)) * kInv2Pi, 1.0, -(k2Pi * cfg.ki) * kInv2Pi, 1.0};
+      for (int i = 0; i < 15; ++i, x = mmul(x, x)) ap[i] = x;
+    }
+    __syncthreads();
+    int e = (int)kk0 + (int)threadIdx.x + 1;                   // A^(kk+1) d, kk < pb < 2^15
+    for (int j = 0; e > 0; ++j, e >>= 1)
+      if (e & 1) {
+        const Mat2 m = ap[j];
+        const double np = m.a * vp + m.b * vv, nv = m.c * vp + m.d * vv;
+        vp = np; vv = nv;
+      }
   }
-  __syncthreads();
   const double* ph = J.theta + (int64_t)s * J.th_stride;
   const double off = ph[P.n];
   const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
-  const int64_t pb = P.lg.pb;
-  int bcur = -1;
-  double sh = 0.0, vp = 0.0, vv = 0.0;
-  bool lin = false;
-  // every phase of the thread is loaded before the first is used (one memory round trip, not
-  // NCO_NR), and the pseudo-block index advances by comparison (pb > 256: at most one step)
-  const int64_t k0 = (int64_t)blockIdx.x * NCO_NR * 256 + threadIdx.x;
+  // every phase of the thread is loaded before the first is used (one memory round trip)
+  const int64_t k0 = kb + kk0 + threadIdx.x;
+  const int64_t kend = kb + len;
   double phv[NCO_NR];
 #pragma unroll
   for (int i = 0; i < NCO_NR; ++i) {
     const int64_t k = k0 + (int64_t)i * 256;
-    phv[i] = k < P.n ? ph[k] : 0.0;
+    phv[i] = k < kend ? ph[k] : 0.0;
   }
-  int b = (int)(k0 / pb);
-  int64_t bnext = (int64_t)(b + 1) * pb;
+  float* oi = J.nco_i + (int64_t)s * J.out_stride + 1;
+  float* oq = J.nco_q ? J.nco_q + (int64_t)s * J.out_stride + 1 : nullptr;
 #pragma unroll
   for (int i = 0; i < NCO_NR; ++i) {
     const int64_t k = k0 + (int64_t)i * 256;
-    if (k >= P.n) break;
-    if (k >= bnext) { ++b; bnext += pb; }
-    if (b != bcur) {                         // a new pseudo-block: its shift and A^(kk+1) d
-      bcur = b;
-      const LongBlk* B = long_blk(P, g, b);
-      sh = B->shift;
-      vp = B->d[0];
-      vv = B->d[1];
-      lin = vp != 0.0 || vv != 0.0;
-      if (lin) {
-        int e = (int)(k - (int64_t)b * pb) + 1;
-        for (int j = 0; e > 0; ++j, e >>= 1)
-          if (e & 1) {
-            const Mat2 m = ap[j];
-            const double np = m.a * vp + m.b * vv, nv = m.c * vp + m.d * vv;
-            vp = np; vv = nv;
-          }
-      }
-    } else if (lin) {                        // 256 steps on: A^256
-      const Mat2 m = ap[8];
+    if (k >= kend) break;
+    double p = fma(sh, kP1, fma(sh, kP2, phv[i]));
+    if (lin) {
+      p = p + vp;
+      const Mat2 m = ap[8];                                    // 256 steps on: A^256
       const double np = m.a * vp + m.b * vv, nv = m.c * vp + m.d * vv;
       vp = np; vv = nv;
     }
-    double p = fma(sh, kP1, fma(sh, kP2, phv[i]));
-    if (lin) p = p + vp;
     const double th = w * ((off + (double)k) + 1.0) + p;
     const double a = th * cfg.scale + cfg.adj;
     double sv, cv;
-    sincos_red(reduce_2pi(a), &sv, &cv);
-    J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
-    if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
+    sincos_red<true>(reduce_2pi(a), &sv, &cv);
+    oi[k] = (float)cv;
+    if (oq) oq[k] = (float)sv;
   }
 }
 
@@ -1891,7 +1892,7 @@ hipError_t sdr_launch_pll_nco(const PllJobs& P, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   if (pll_long(P))
-    hipLaunchKernelGGL(nco_long_kernel, dim3((unsigned)((P.n + 256 * NCO_NR - 1) / (256 * NCO_NR)), (unsigned)(P.njobs * P.nstreams)),
+    hipLaunchKernelGGL(nco_long_kernel, dim3((unsigned)(L.lg.nb * nco_tiles_per_block(L.lg.pb)), (unsigned)(P.njobs * P.nstreams)),
                        dim3(256), 0, st, L);
   else if (P.n > 0)
     hipLaunchKernelGGL(nco_jobs_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
