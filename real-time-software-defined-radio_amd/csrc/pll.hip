@@ -1125,12 +1125,68 @@ __device__ void spec_fallback(const PllJobs& P, const int bid) {
   stat_add(P.stats, SDR_PLL_ST_SEQUENTIAL, 1);
 }
 
+// nco[k+1] from phaseEst_k for step k of recurrence g = (job, stream): th_k by the reference's
+// formula (fmPll.py:33), the Q-form row converted back when the loop kernels left one.
+__device__ __forceinline__ void nco_out(const PllJobs& P, const PllJob& J, int s, double off, int64_t k, double p) {
+#pragma clang fp contract(off)
+  const double w = 2.0 * kPi * (J.cfg.freq / J.cfg.fs);
+  if (P.qform) {                                        // Q_{i+1} -> phase_{i+1}
+    const double i = (double)(k % PG);
+    p = p - (kPi * J.cfg.ki) * ((i + 1.0) * i * 0.5);
+  }
+  const double th = w * ((off + (double)k) + 1.0) + p;
+  const double a = th * J.cfg.scale + J.cfg.adj;
+  // the reference's angle grows with the stream (~1e7 rad after a minute): reduced here by the
+  // 3-part Cody-Waite step (exact multiples of 2 pi for |n| < 2^26), sincos then takes its
+  // small-argument path instead of the large-argument reduction
+  double sv, cv;
+  sincos_red<true>(reduce_2pi(a), &sv, &cv);
+  J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
+  if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
+}
+__device__ __forceinline__ void nco_step(const PllJobs& P, int g, int64_t k) {
+  const int q = g / P.nstreams;
+  const int s = g - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const double* ph = J.theta + (int64_t)s * J.th_stride;
+  nco_out(P, J, s, ph[P.n], k, ph[k]);
+}
+// a recurrence's whole NCO row by one workgroup of NT threads: NB outputs per thread at a time,
+// their phases loaded first and their sincos chains independent (one wave per SIMD: the
+// chains' latency, not their issue, is what a single pass would wait on)
+template <int NT>
+__device__ __forceinline__ void nco_row(const PllJobs& P, int g, int tid) {
+  constexpr int NB = 4;
+  const int q = g / P.nstreams;
+  const int s = g - q * P.nstreams;
+  const PllJob& J = P.j[q];
+  const double* ph = J.theta + (int64_t)s * J.th_stride;
+  const double off = ph[P.n];
+  for (int64_t k0 = tid; k0 < P.n; k0 += NB * NT) {
+    double pv[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) pv[b] = k0 + b * NT < P.n ? ph[k0 + b * NT] : 0.0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (k0 + b * NT < P.n) nco_out(P, J, s, off, k0 + b * NT, pv[b]);
+  }
+}
+
 template <int SPEC_T, bool LONG>
 __global__ __launch_bounds__(SPEC_T) __attribute__((amdgpu_waves_per_eu(SPEC_T == 512 ? 4 : 2))) void pll_spec_kernel(PllJobs P) {
   // (LONG: a long call's first solve of every block, which also initialises its record)
   const bool done = spec_body<SPEC_T, LONG, LONG>(P, (int)blockIdx.x, (int)threadIdx.x);
   if constexpr (!LONG) {
-    if (!done && P.lpw == 0 && threadIdx.x == 0) spec_fallback(P, (int)blockIdx.x);
+    if (P.lpw == 0) {
+      // a per-block call (spec-only): the sequential fallback when the solve could not complete
+      // the recurrence, then its NCO row here -- the theta row is this workgroup's own (visible
+      // after the barrier), and the NCO needs no launch of its own
+      if (!done && threadIdx.x == 0) spec_fallback(P, (int)blockIdx.x);
+      if (P.nco_fused) {
+        __syncthreads();
+        nco_row<SPEC_T>(P, (int)blockIdx.x, (int)threadIdx.x);
+      }
+    }
   }
 }
 
@@ -1227,10 +1283,11 @@ __device__ void seq_run(const PllCfg& cfg, const float* in, double* th, int64_t 
 // end and S_j the chained start, the residual R_j = S_j - A_j splits into n_j whole turns and
 // rho_j = R_j - 2 pi n_j, and
 //     R_{j+1} = (E_j - A_{j+1}) + 2 pi n_j + Phi_j rho_j.
-// |Phi_j| <= 1e-8 (the loop matrix over a pseudo-block), so the turns are a prefix sum of the
-// local integers rint((E_j - A_{j+1})_phase / 2 pi), and rho_{j+1} = C_j + Phi_j C_{j-1} to f64
-// rounding (C_j = E_j - A_{j+1} less its turns; the term after is Phi^2 ~ 1e-16 rho).  Then per
-// block the bound err = c1 |rho_p| + c2 |rho_v| decides, as described above.  The accepted
+// The turns are a prefix sum of the local integers rint((E_j - A_{j+1})_phase / 2 pi), and with
+// C_j = E_j - A_{j+1} less its turns, rho_{j+1} = C_j + Phi rho_j (Phi = A^pb, the loop matrix
+// over a pseudo-block): an exact scan below (Phi is ~1e-8 over a long call's pseudo-block but
+// ~0.1 over a split per-block call's on the RDS loop).  Then per block the bound
+// err = c1 |rho_p| + c2 |rho_v| decides, as described above.  The accepted
 // prefix moves the chain's position; the first block after it that is not accepted gets its
 // exact start (LB_NEED_X) for a re-solve.  Returns the new position (every thread).
 constexpr int CHAIN_T = 512;
@@ -1585,30 +1642,8 @@ __global__ __launch_bounds__(256) void pll_prep_kernel(PllJobs P) {
 // nco[k+1] from phaseEst_k for every (job, stream) of the table (th_k by the reference's
 // formula, fmPll.py:33); nco[0] is the loop kernel's.
 __global__ void nco_jobs_kernel(PllJobs P) {
-#pragma clang fp contract(off)
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= P.n) return;
-  const int g = blockIdx.y;                 // uniform: (job, stream)
-  const int q = g / P.nstreams;
-  const int s = g - q * P.nstreams;
-  const PllJob& J = P.j[q];
-  const double* ph = J.theta + (int64_t)s * J.th_stride;
-  const double off = ph[P.n];
-  const double w = 2.0 * kPi * (J.cfg.freq / J.cfg.fs);
-  double p = ph[k];
-  if (P.qform) {                                        // Q_{i+1} -> phase_{i+1}
-    const double i = (double)(k % PG);
-    p = p - (kPi * J.cfg.ki) * ((i + 1.0) * i * 0.5);
-  }
-  const double th = w * ((off + (double)k) + 1.0) + p;
-  const double a = th * J.cfg.scale + J.cfg.adj;
-  // the reference's angle grows with the stream (~1e7 rad after a minute): reduced here by the
-  // 3-part Cody-Waite step (exact multiples of 2 pi for |n| < 2^26), sincos then takes its
-  // small-argument path instead of the large-argument reduction
-  double sv, cv;
-  sincos_red<true>(reduce_2pi(a), &sv, &cv);
-  J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
-  if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
+  if (k < P.n) nco_step(P, (int)blockIdx.y, k);
 }
 
 
@@ -1709,6 +1744,11 @@ bool pll_spec_enabled() {
 // a per-block call solved by pll_spec_kernel alone (its own sequential fallback): no prep or
 // loop kernel, plain (not Q-form) phase rows
 bool spec_only(const PllJobs& P) { return pll_spec_enabled() && P.n >= 2; }
+// a spec-only call's NCO rows by the solve's own launch unless SDR_PLL_NCO_FUSE=0 (A/B runs)
+bool nco_fused(const PllJobs& P) {
+  static const bool on = [] { const char* e = getenv("SDR_PLL_NCO_FUSE"); return !(e && e[0] == '0'); }();
+  return on && spec_only(P);
+}
 hipError_t pll_check(const PllJobs& P, bool* vec) {
   if (P.njobs < 1 || P.njobs > SDR_PLL_MAXJ || P.nstreams <= 0 || P.n < 0) return hipErrorInvalidValue;
   *vec = true;
@@ -1867,6 +1907,7 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     // when the solve cannot complete it (lpw = 0 tells the kernel so)
     L.lpw = 0;
     L.qform = 0;
+    L.nco_fused = nco_fused(P) ? 1 : 0;
     const dim3 g((unsigned)(L.njobs * L.nstreams));
     if (L.n > 10240) hipLaunchKernelGGL((pll_spec_kernel<512, false>), g, dim3(512), 0, st, L);
     else hipLaunchKernelGGL((pll_spec_kernel<256, false>), g, dim3(256), 0, st, L);
@@ -1894,7 +1935,7 @@ hipError_t sdr_launch_pll_nco(const PllJobs& P, hipStream_t st) {
   if (pll_long(P))
     hipLaunchKernelGGL(nco_long_kernel, dim3((unsigned)(L.lg.nb * nco_tiles_per_block(L.lg.pb)), (unsigned)(P.njobs * P.nstreams)),
                        dim3(256), 0, st, L);
-  else if (P.n > 0)
+  else if (P.n > 0 && !nco_fused(P))                  // (fused: the solve's launch wrote the rows)
     hipLaunchKernelGGL(nco_jobs_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
                        dim3(256), 0, st, L);
   return hipGetLastError();

@@ -919,7 +919,16 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   // and constant rows alternate with the row set; set q is free once block k-2's back half
   // (which waited for its recurrence) is done.
   const bool plls = stx || rd;
-  hipStream_t ps = r->pipe ? r->mid : st;
+  // The recurrences get a stream of their own (block k's beside block k-1's NCO and stages
+  // C-E) when they are the long part of the back half: many recurrences, or a span's long
+  // call.  A few per-block recurrences (c4: one, ~20 us) run on the back stream instead -- each
+  // cross-stream hop costs ~10 us of queue hand-off, more than the overlap returns (c4
+  // pipelined 790-840 -> 950 MS/s; 64-stream C5 blocks 98 -> 92 k MS/s the other way).
+  // SDR_RX_PLL_STREAM=0 / 1 forces either (A/B).
+  static const int pll_stream = [] { const char* e = getenv("SDR_RX_PLL_STREAM"); return e ? (e[0] == '0' ? 0 : 1) : -1; }();
+  const int njobs = (stx ? 1 : 0) + (rd ? 1 : 0);
+  const bool mid = r->pipe && (pll_stream >= 0 ? pll_stream == 1 : (S * njobs >= 8 || M > SDR_PLL_BLOCK_MAX));
+  hipStream_t ps = mid ? r->mid : st;
   PllJobs P{};
   if (plls) {
     P.nstreams = S;
@@ -942,7 +951,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   }
   if (r->pipe) {
     HIP_TRY(hipEventRecord(r->ev_front[q], fs));
-    if (plls) {
+    if (plls && mid) {
       HIP_TRY(hipStreamWaitEvent(ps, r->ev_front[q], 0));
       if (r->blocks >= 2) HIP_TRY(hipStreamWaitEvent(ps, r->ev_back[q], 0));
     } else {
@@ -951,7 +960,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   }
   if (plls) HIP_TRY(sdr_launch_pll_loop(P, ps));
   HIP_TRY(mark(1 + SDR_RX_ST_PLL, ps));
-  if (r->pipe && plls) {
+  if (mid && plls) {
     HIP_TRY(hipEventRecord(r->ev_mid[q], ps));
     HIP_TRY(hipStreamWaitEvent(st, r->ev_mid[q], 0));
   }

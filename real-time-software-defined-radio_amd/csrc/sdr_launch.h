@@ -114,6 +114,7 @@ struct PllLong {
 struct PllJobs {
   PllJob j[SDR_PLL_MAXJ]; int njobs; int nstreams; int64_t n;
   int lpw; int qform;                  // set by the launchers
+  int nco_fused;                       // per-block spec-only calls: the solve's launch writes the NCO rows
   unsigned long long* stats;           // device counters (SDR_PLL_NSTATS, include/sdr.h), nullable
   void* work;                          // long calls: sdr_pll_work_bytes() of device scratch
   PllLong lg;                          // long calls: set by the launcher

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Derived per-kernel metrics from the closing set's SQ / TCC passes (tools/r03_final_c.sh).
+"""Derived per-kernel metrics from a closing set's SQ / TCC passes (tools/gpu_round.sh pmc steps).
 
 usage: python3 tools/pmc_derived.py DIR TAG [TAG ...] > profiles/rNN/pmc_derived.md
 Reads DIR/pmc_<tag>_{a,b,c,fetch,write}/pmc_counter_collection.csv and prints, per kernel

@@ -2,9 +2,10 @@
 """HBM traffic per launch of the bench's dominant kernel from rocprofv3 --pmc CSVs.
 
 usage: python3 tools/pmc_traffic.py <tag> [--blocks 64 --taps 101] [--dir D]
-Reads gpurun_out/pmc_<tag>_<path>_{fetch,write}/pmc_counter_collection.csv (written by
-tools/prof_round.sh, one counter per rocprofv3 pass), or with --dir D the closing set's
-D/pmc_<path>_{fetch,write}/ (tools/r03_final_b.sh: paths fused, u8), and writes
+Reads gpurun_out/pmc_<tag>_<path>_{fetch,write}/pmc_counter_collection.csv, or with --dir D
+(relative to the repo) the closing set's D/pmc_<path>_{fetch,write}/ -- one counter per
+rocprofv3 pass, tools/gpu_round.sh pmc:<path>_fetch:FETCH_SIZE:<bench args> and
+pmc:<path>_write:WRITE_SIZE:<bench args>, paths fused / u8 / split -- and writes
 profiles/fe_pmc_traffic.json.
 
 Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 counts half
