@@ -464,15 +464,8 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
 #pragma unroll
   for (int j = 0; j < TP; ++j) asm volatile("" : "+v"(tp[j]));
 
-  // this lane's taps for a run's cooperative predecessor output, loaded (and waited for)
-  // before any LDS-DMA is in flight: the first tile then needs no VMEM of its own
   constexpr int NK = (T + 63) / 64;
   float hk[NK];
-#pragma unroll
-  for (int q = 0; q < NK; ++q) hk[q] = (lane + 64 * q < T) ? p.taps_dev[lane + 64 * q] : 0.f;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int q = 0; q < NK; ++q) asm volatile("" : "+v"(hk[q]));
 
   const unsigned voff = 16u * lane;
   const float* iqf = reinterpret_cast<const float*>(p.iq);
@@ -522,17 +515,11 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
   int i = (int)(g0 - (int64_t)s * a.tps);
   int U = (int)(g1 - g0);
   bool mid = false;
+  // a run starting mid-stream first runs the warm-up tile i-1 (history / predecessor);
+  // a run may start and end mid audio block (audio_store keeps to the outputs it owns)
   if constexpr (FUSED) {
-    // a run starting mid-stream first runs the warm-up tile i-1 (history / predecessor);
-    // a run may start and end mid audio block (audio_store keeps to the outputs it owns)
     mid = i > 0;
     if (mid) { --i; ++U; }
-    for (int e = lane; e < HA + BD + 4; e += 64) dh[e] = 0.f;   // finite everywhere (0 * x)
-    for (int w = lane; w < NW + 1; w += 64) {               // entry NW: zero (pairs over-read)
-      const int k0 = (TA - 1) - w, k1 = k0 + DA, k2 = k0 + 2 * DA;
-      ptab[w] = f4v{(k0 >= 0 && k0 < TA) ? a.ataps[k0] : 0.f, (k1 >= 0 && k1 < TA) ? a.ataps[k1] : 0.f,
-                    (k2 >= 0 && k2 < TA) ? a.ataps[k2] : 0.f, 0.f};
-    }
   }
   // image kinds: 1 guarded build, 2 DMA (whole image), 3 DMA (new chunks; halo by LDS copy)
   enum { K_NONE = 0, K_BUILD = 1, K_FULL = 2, K_HALO = 3 };
@@ -540,13 +527,33 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
   int b = 0;
   int issued = 0, mark = 0;                        // VMEM instructions issued / per-tile mark
   int kind = dma_full(nl) ? K_FULL : K_BUILD;
-  if (kind == K_FULL) { issued += issue(s, nl, 0, true); mark = issued; }
+  // r04b: the first image's DMA goes out before the prologue's own loads (this lane's taps for a
+  // run's cooperative predecessor output; FUSED: the audio tap table), and one wait covers all:
+  // the launch pays one memory round trip before its first tile instead of three
+  if (kind == K_FULL) issue(s, nl, 0, true);
+#pragma unroll
+  for (int q = 0; q < NK; ++q) hk[q] = (lane + 64 * q < T) ? p.taps_dev[lane + 64 * q] : 0.f;
+  if constexpr (FUSED) {
+    for (int e = lane; e < HA + BD + 4; e += 64) dh[e] = 0.f;   // finite everywhere (0 * x)
+    for (int w = lane; w < NW + 1; w += 64) {               // entry NW: zero (pairs over-read)
+      const int k0 = (TA - 1) - w, k1 = k0 + DA, k2 = k0 + 2 * DA;
+      ptab[w] = f4v{(k0 >= 0 && k0 < TA) ? a.ataps[k0] : 0.f, (k1 >= 0 && k1 < TA) ? a.ataps[k1] : 0.f,
+                    (k2 >= 0 && k2 < TA) ? a.ataps[k2] : 0.f, 0.f};
+    }
+  }
+  // the first image landed too (nothing in flight: issued = mark = 0)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int q = 0; q < NK; ++q) asm volatile("" : "+v"(hk[q]));
   float carry = 0.f;                               // phase of the previous tile's last output
   bool have = false;                               // carry valid (previous tile, same stream)
   int wacc = 0;                                    // per-lane 2*pi correction count
 
   // ---- deferred outputs (OutQ3): FE demod tiles / FUSED audio blocks ----
-  constexpr int QN = FUSED ? 12 : 36;
+#ifndef SDR_RING_QN
+#define SDR_RING_QN 12
+#endif
+  constexpr int QN = FUSED ? SDR_RING_QN : 36;
   OutQ3<QN> oq;
   int qn = 0, qs = 0;
   int64_t q0 = 0;                                  // FE: first tile; FUSED: first audio block
@@ -1215,7 +1222,8 @@ template <int T, bool FUSED>
 static hipError_t launch_ring_t(FeParams p, const TapsF32& taps, RingArgs ra, hipStream_t st) {
   if (ra.total <= 0) return hipSuccess;
   if (ra.total > 0x7fffffff) return hipErrorInvalidValue;
-  static const int wpc = resident_per_cu(fe_ring_kernel<T, FUSED>, 64);
+  static std::atomic<int> wpc_cache[kMaxDevices];     // per device (a process may drive several)
+  const int wpc = per_device(wpc_cache, [] { return resident_per_cu(fe_ring_kernel<T, FUSED>, 64); });
   const int64_t slots = (int64_t)cu_count() * std::max(1, std::min(wpc, 4));
   const int64_t grid = std::min<int64_t>(slots, ra.total);
   p.tiles_per_stream = ra.tps;
@@ -1228,7 +1236,8 @@ template <int T, bool FUSED>
 static hipError_t launch_slot_t(FeParams p, const TapsF32& taps, SlotArgs sa, hipStream_t st) {
   if (sa.total <= 0) return hipSuccess;
   if (sa.total > 0x7fffffff) return hipErrorInvalidValue;
-  static const int wpc = resident_per_cu(fe_slot_kernel<T, FUSED, true>, 64);
+  static std::atomic<int> wpc_cache[kMaxDevices];     // per device (a process may drive several)
+  const int wpc = per_device(wpc_cache, [] { return resident_per_cu(fe_slot_kernel<T, FUSED, true>, 64); });
   const int64_t slots = (int64_t)cu_count() * std::max(1, std::min(wpc, 8));
   const int64_t grid = std::min<int64_t>(slots, sa.total);
   p.tiles_per_stream = sa.tps;

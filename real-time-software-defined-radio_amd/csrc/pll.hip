@@ -529,6 +529,7 @@ constexpr int SPEC_W_LONG = SDR_SPEC_W_LONG;
 constexpr int SPEC_IT = 3;           // solve / check rounds before the sequential kernel takes over
 constexpr int SPEC_NMAX = SDR_PLL_BLOCK_MAX; // samples per call (the sign codes of steps 1.. in LDS: 16 KiB)
 static_assert(SPEC_NMAX == 16384 + 1, "LDS sizing");
+constexpr int SPEC_N256 = 10240;             // longest call the 256-thread solve takes (512 above)
 constexpr int SPEC_LDS = 32 * 513;           // padded transposed bytes: 512 chunks of <= 32 steps (or 256 of <= 40)
 constexpr int SB = 8;                        // steps per batch of LDS reads in the step loops
 
@@ -618,6 +619,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   __shared__ double x1s[2];
   __shared__ float mg[NW + 1];                   // the waves' smallest wrap margins (+ the literal step's)
   __shared__ double wsh;                         // w for the end state (no register across the solve)
+  __shared__ double kds;                         // kD for the cold paths after the staging (registers)
   d2v* yb = reinterpret_cast<d2v*>(tb);
   const int lane = tid & 63, wv = tid >> 6;
   int q, s, status = 0;
@@ -701,16 +703,18 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   const double w = sgpr_d(2.0 * kPi * (cfg.freq / cfg.fs));
   const double kA = sgpr_d(k2Pi * cfg.ki), kB = sgpr_d(kPi * cfg.ki);
   const double kC = sgpr_d(k2Pi * (cfg.kp + cfg.ki)), kD = sgpr_d(kPi * (cfg.kp + cfg.ki));
-  auto thval = [&](double ph, int64_t k) {       // what the theta row holds for step k
-    if (!P.qform) return ph;
-    const double i = (double)(k % PG);
-    return ph + kB * ((i + 1.0) * i * 0.5);
-  };
+  // what the theta row holds for step k: the phase itself (every launch of the solve -- per-block,
+  // long call, fix kernel -- runs with qform = 0, sdr_launch_pll_loop; the Q-form rows are the
+  // sequential chunk kernel's alone)
+  auto thval = [&](double ph, int64_t) { return ph; };
   // c_k from the sign code: pll_c's arithmetic exactly (code 2, a 0 / NaN input, is caught by
   // the guess: the solve is abandoned to the general form, so its value here does not matter)
   const double w2pi = sgpr_d(w * kInv2Pi);
-  if (tid == 0) wsh = w;
+  if (tid == 0) { wsh = w; kds = kD; }
   auto cval = [&](int cd, int k) { return fma(-(off + (double)k), w2pi, cd == 0 ? 0.5 : 1.0); };
+  // ... from offk = off + k itself: the step loops carry offk as an f64 counter (+1.0 a step, exact
+  // for the integer-valued trigOffset) instead of converting k every step (cval's value exactly)
+  auto cvk = [&](int cd, double offk) { return fma(-offk, w2pi, cd == 0 ? 0.5 : 1.0); };
   // sample 0: the literal general step (thread 0), as the loop kernels' general() (a
   // pre-roll's seed is set from the measured phase instead, below)
   if (tid == 0 && pre == 0) {
@@ -734,20 +738,30 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // out SG at a time before the first is used.  (Slots of steps past N hold whatever was
   // there: only discarded steps read them, and every slot is in the array.)
   {
-    constexpr int SG = 32;
-    // kk / L by a multiply-high (L <= 64, kk < 2^16: exact with m = floor(2^32 / L) + 1)
-    const unsigned mL = 0xffffffffu / (unsigned)L + 1u;
-    for (int b0 = tid; b0 < N; b0 += SG * SPEC_T) {
-      float xv[SG];
+    // r04b: no per-element guard (its branches were ~13 SALU a step): every thread loads and
+    // writes all SG of its elements, a load past N clamped into the array and its code written
+    // to the unused slot of step kk (i = kk mod L, j = kk / L is one-to-one and stays inside
+    // code[] for every L the launchers produce: (L-1) CSTR + (SG SPEC_T - 1) / L < SPEC_LDS)
+    constexpr int SG = SPEC_T == 512 ? 32 : 40;
+    static_assert(SG * SPEC_T >= (SPEC_T == 512 ? SPEC_NMAX : SPEC_N256) - 1, "one pass of SG loads covers a call");
+    float xv[SG];
 #pragma unroll
-      for (int u = 0; u < SG; ++u) xv[u] = b0 + u * SPEC_T < N ? in[b0 + u * SPEC_T + 1] : 0.f;
+    for (int u = 0; u < SG; ++u) xv[u] = in[min(tid + u * SPEC_T, N - 1) + 1];
+    auto cod = [](float x) { return (int8_t)(x > 0.f ? 0 : (x < 0.f ? 1 : 2)); };
+    if (SPEC_T % L == 0) {
+      // element kk = tid + u SPEC_T: i = tid mod L for every u, j = tid / L + u SPEC_T / L
+      int8_t* cb = code + (tid % L) * CSTR + tid / L;
+      const int js = SPEC_T / L;
+#pragma unroll
+      for (int u = 0; u < SG; ++u) cb[u * js] = cod(xv[u]);
+    } else {
+      // kk / L by a multiply-high (L <= 64, kk < 2^16: exact with m = floor(2^32 / L) + 1)
+      const unsigned mL = 0xffffffffu / (unsigned)L + 1u;
 #pragma unroll
       for (int u = 0; u < SG; ++u) {
-        const int kk = b0 + u * SPEC_T;
-        if (kk < N) {
-          const int j = (int)__umulhi((unsigned)kk, mL), i = kk - j * L;
-          code[i * CSTR + j] = (int8_t)(xv[u] > 0.f ? 0 : (xv[u] < 0.f ? 1 : 2));
-        }
+        const int kk = tid + u * SPEC_T;
+        const int j = (int)__umulhi((unsigned)kk, mL), i = kk - j * L;
+        code[i * CSTR + j] = cod(xv[u]);
       }
     }
   }
@@ -799,7 +813,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     const double ang = (double)atan2f((float)si, (float)sr);   // (a guess: f32 is plenty)
     if (pre > 0 && tid == 0) {                   // the pre-roll's seed: measured phase, span's integrator
       x1s[0] = ang;
-      x1s[1] = st_call[0] - kD;
+      x1s[1] = st_call[0] - kds;
     }
     __syncthreads();
     yb[tid].x = ang;
@@ -826,55 +840,98 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // solve needs no pass of its own; the check below validates whatever this rounds to)
   bool bad = false;
   double xs_p = 0.0, xs_v = 0.0, xe_p = 0.0, xe_v = 0.0;
+  // r04b: a wave whose chunks are all full runs the step loops without a per-step "inside the
+  // chunk" predicate (its selects and compares were a fifth of the check loop's VALU); the wave
+  // holding the last, partial chunk (and the unused ones) keeps them.  wfast: also every chunk
+  // after a long call's pre-roll, so every step's wrap margin counts and every phase is stored.
+  const bool wfull = __all(len == L);
+  const bool wfast = wfull && __all(k0 >= pre);
   {
     // the true step from a seed on the measured drift: phaseEst ~ p1 + D at the warm-up's
     // start, integ ~ the measured drift per step; 256 steps of the loop then pull the guess
     // onto the trajectory
-    const int kw = max(1, k0 - (LONG ? SPEC_W_LONG : SPEC_W));
+    constexpr int SW = LONG ? SPEC_W_LONG : SPEC_W;
+    const int kw = max(1, k0 - SW);
     const int jw = (kw - 1) / L;
     double p = p1 + yb[jw].x, V = v1;
-    if (k0 - kw >= 64 && tid < TE) V = (yb[tid].x - yb[jw].x) / (double)(k0 - kw) - kD;
+    if (k0 - kw >= 64 && tid < TE) V = (yb[tid].x - yb[jw].x) / (double)(k0 - kw) - kds;
     const int W = tid < TE ? k0 - kw : 0;        // warm-up steps (over the chunks before this one)
-    int jc = jw, ic = (kw - 1) - jw * L;         // (chunk, step) of step kw
-    for (int i0 = 0; i0 < W; i0 += SB) {
-      int cd[SB];
+    if (wfull && SW <= L) {
+      // every warm-up is the last SW steps of the previous chunk (thread 0 has none: it runs SW
+      // discarded steps over chunk 0 and takes its seed back)
+      const double p0 = p, v0 = V;
+      const int jc = max(tid - 1, 0);
+      double kd = off + (double)(k0 - SW);
+#pragma unroll 1
+      for (int i0 = 0; i0 < SW; i0 += SB) {
+        int cd[SB];
 #pragma unroll
-      for (int u = 0; u < SB; ++u) {             // (past the warm-up: slots of this chunk, unused)
-        cd[u] = code[ic * CSTR + jc];
-        if (++ic == L) { ic = 0; ++jc; }
+        for (int u = 0; u < SB; ++u) cd[u] = code[(L - SW + i0 + u) * CSTR + jc];
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+          const double t = fma(-kInv2Pi, p, cvk(cd[u], kd));
+          kd += 1.0;
+          const double f = __builtin_amdgcn_fract(t);
+          const double S = p + V;
+          V = fma(kA, f, V - kB);
+          p = fma(kC, f, S);
+        }
       }
+      if (W == 0) { p = p0; V = v0; }
+    } else {
+      int jc = jw, ic = (kw - 1) - jw * L;       // (chunk, step) of step kw
+      for (int i0 = 0; i0 < W; i0 += SB) {
+        int cd[SB];
 #pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        const double t = fma(-kInv2Pi, p, cval(cd[u], kw + i0 + u));
-        const double f = __builtin_amdgcn_fract(t);
-        const double S = p + V;
-        const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
-        const bool act = i0 + u < W;
-        V = act ? nV : V;
-        p = act ? np : p;
+        for (int u = 0; u < SB; ++u) {           // (past the warm-up: slots of this chunk, unused)
+          cd[u] = code[ic * CSTR + jc];
+          if (++ic == L) { ic = 0; ++jc; }
+        }
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+          const double t = fma(-kInv2Pi, p, cval(cd[u], kw + i0 + u));
+          const double f = __builtin_amdgcn_fract(t);
+          const double S = p + V;
+          const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
+          const bool act = i0 + u < W;
+          V = act ? nV : V;
+          p = act ? np : p;
+        }
       }
     }
     __syncthreads();                             // yb (D_j) read before tb reuses its space
     xs_p = p;                                    // the guess's chunk start (after the warm-up)
     xs_v = V;
-    for (int i0 = 0; i0 < L; i0 += SB) {
-      int cd[SB];
+    auto guess = [&](auto FC) __attribute__((always_inline)) {
+      constexpr bool F = decltype(FC)::value;
+      double kd = off + (double)k0;
+      for (int i0 = 0; i0 < L; i0 += SB) {
+        int cd[SB];
 #pragma unroll
-      for (int u = 0; u < SB; ++u) cd[u] = code[(i0 + u) * CSTR + tid];
+        for (int u = 0; u < SB; ++u) cd[u] = code[(i0 + u) * CSTR + tid];
 #pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        const int i = i0 + u;
-        const double t = fma(-kInv2Pi, p, cval(cd[u], k0 + i));
-        const bool act = i < len;
-        bad |= act && cd[u] == 2;                  // a 0 / NaN input: the general form's case
-        const double f = __builtin_amdgcn_fract(t);
-        if (act) mrel[i * CSTR + tid] = floor_byte(t, f);
-        const double S = p + V;
-        const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
-        V = act ? nV : V;
-        p = act ? np : p;
+        for (int u = 0; u < SB; ++u) {
+          const int i = i0 + u;
+          const double t = fma(-kInv2Pi, p, cvk(cd[u], kd));
+          kd += 1.0;
+          const bool act = F || i < len;
+          bad |= act && cd[u] == 2;                // a 0 / NaN input: the general form's case
+          const double f = __builtin_amdgcn_fract(t);
+          if (act) mrel[i * CSTR + tid] = floor_byte(t, f);
+          const double S = p + V;
+          const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
+          if constexpr (F) {
+            V = nV;
+            p = np;
+          } else {
+            V = act ? nV : V;
+            p = act ? np : p;
+          }
+        }
       }
-    }
+    };
+    if (wfull) guess(std::true_type{});
+    else guess(std::false_type{});
     xe_p = p;                                    // ... and its end
     xe_v = V;
   }
@@ -962,48 +1019,68 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     double p = vp, V = vv;
     xs_p = vp;                                   // this pass's start and (below) end: the next
     xs_v = vv;                                   // round's responses to the integers it records
-    float mth = 1.f;                             // smallest min(fract, 1 - fract) of the block's own steps
-    for (int i0 = 0; i0 < L; i0 += SB) {
-      int cd[SB / 2];                            // (half a batch of codes at a time: registers)
-      int8_t mm[SB / 2];
+    // smallest / largest fract(t) of the block's own steps, as f32 bit patterns (non-negative:
+    // integer min / max order them; the margin is min(lo, 1 - hi))
+    unsigned mlo = 0x3f800000u, mhi = 0u;
+    auto check = [&](auto FC) __attribute__((always_inline)) {
+      constexpr bool F = decltype(FC)::value;
+      double kd = off + (double)k0;
+      for (int i0 = 0; i0 < L; i0 += SB) {
+        int cd[SB / 2];                          // (half a batch of codes at a time: registers)
+        int8_t mm[SB / 2];
 #pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        if (u % (SB / 2) == 0) {
+        for (int u = 0; u < SB; ++u) {
+          if (u % (SB / 2) == 0) {
 #pragma unroll
-          for (int v = 0; v < SB / 2; ++v) {
-            cd[v] = code[(i0 + u + v) * CSTR + tid];
-            mm[v] = mrel[(i0 + u + v) * CSTR + tid];
+            for (int v = 0; v < SB / 2; ++v) {
+              cd[v] = code[(i0 + u + v) * CSTR + tid];
+              mm[v] = mrel[(i0 + u + v) * CSTR + tid];
+            }
           }
+          const int i = i0 + u;
+          const double t = fma(-kInv2Pi, p, cvk(cd[u % (SB / 2)], kd));
+          kd += 1.0;
+          const bool act = F || i < len;
+          const double f = __builtin_amdgcn_fract(t);
+          const int8_t r = floor_byte(t, f);
+          miss |= act && r != mm[u % (SB / 2)];
+          const double S = p + V;
+          const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
+          const unsigned fb = __float_as_uint((float)f);
+          if constexpr (F) {
+            V = nV;
+            p = np;
+            mlo = min(mlo, fb);
+            mhi = max(mhi, fb);
+          } else {
+            V = act ? nV : V;
+            p = act ? np : p;
+            const bool own = act && k0 + i >= pre;
+            mlo = min(mlo, own ? fb : 0x3f800000u);
+            mhi = max(mhi, own ? fb : 0u);
+          }
+          if (act) mrel[i * CSTR + tid] = r;
+          tw[u * TBS + lane] = thval(p, k0 + i);
         }
-        const int i = i0 + u;
-        const double t = fma(-kInv2Pi, p, cval(cd[u % (SB / 2)], k0 + i));
-        const bool act = i < len;
-        const double f = __builtin_amdgcn_fract(t);
-        const int8_t r = floor_byte(t, f);
-        miss |= act && r != mm[u % (SB / 2)];
-        const double S = p + V;
-        const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
-        V = act ? nV : V;
-        p = act ? np : p;
-        if (act && k0 + i >= pre) mth = fminf(mth, (float)fmin(f, 1.0 - f));
-        if (act) mrel[i * CSTR + tid] = r;
-        tw[u * TBS + lane] = thval(p, k0 + i);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int u = lane & (SB - 1), cw = lane / SB;   // this lane stores step i0 + u of chunk 8 r + cw
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int u = lane & (SB - 1), cw = lane / SB;   // this lane stores step i0 + u of chunk 8 r + cw
 #pragma unroll
-      for (int r8 = 0; r8 < 64 / SB; ++r8) {
-        const int ch = r8 * SB + cw;                   // chunk within the wave
-        const int k = 1 + (wv * 64 + ch) * L + i0 + u;
-        const double v = tw[u * TBS + ch];
-        if (k >= pre && k < (int)n) th[k] = v;
+        for (int r8 = 0; r8 < 64 / SB; ++r8) {
+          const int ch = r8 * SB + cw;                   // chunk within the wave
+          const int k = 1 + (wv * 64 + ch) * L + i0 + u;
+          const double v = tw[u * TBS + ch];
+          if (F || (k >= pre && k < (int)n)) th[k] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+    };
+    if (wfast) check(std::true_type{});
+    else check(std::false_type{});
+    float mth = fminf(__uint_as_float(mlo), 1.f - __uint_as_float(mhi));
     xe_p = p;
     xe_v = V;
     if constexpr (LONG) {
@@ -1057,7 +1134,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       if (tid == TE - 1) {
         const double arg = wsh * ((off + (double)(n - 1)) + 1.0) + p;
         if constexpr (!LONG) th[n] = off;
-        st_out[0] = V + kD;
+        st_out[0] = V + kds;
         st_out[1] = p;
         end_trig(arg, cfg.scale, cfg.adj, st_out);
         st_out[5] = off + (double)n;
@@ -1068,7 +1145,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
             const double gpv = x1s[0], gvv = x1s[1];
             const double ofs = off + (double)(pre - 1);          // the previous step's trigOffset
             const double arg = wsh * (ofs + 1.0) + gpv;
-            LB->g[0] = gvv + kD;
+            LB->g[0] = gvv + kds;
             LB->g[1] = gpv;
             double sv, cv;
             sincos_red<true>(reduce_2pi(arg), &sv, &cv);
@@ -1076,7 +1153,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
             LB->g[3] = sv;
             LB->g[4] = 0.0;
             LB->g[5] = off + (double)pre;
-            LB->u[0] = gvv + kD;
+            LB->u[0] = gvv + kds;
             LB->u[1] = gpv;
           } else {
             LB->u[0] = st[0];
@@ -1909,7 +1986,7 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     L.qform = 0;
     L.nco_fused = nco_fused(P) ? 1 : 0;
     const dim3 g((unsigned)(L.njobs * L.nstreams));
-    if (L.n > 10240) hipLaunchKernelGGL((pll_spec_kernel<512, false>), g, dim3(512), 0, st, L);
+    if (L.n > SPEC_N256) hipLaunchKernelGGL((pll_spec_kernel<512, false>), g, dim3(512), 0, st, L);
     else hipLaunchKernelGGL((pll_spec_kernel<256, false>), g, dim3(256), 0, st, L);
     return hipGetLastError();
   }
