@@ -473,12 +473,14 @@ int sdr_fe_mono_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t
     FeLaunch a{iq, n, xs, 0, nstreams, rts->dev_f32, &rts->h, rf_taps, rf_decim, u8, nullptr, nullptr, 0,
                nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr};
     a.afr = rts->dev_afr;
-    if (u8 && c->xwave == nullptr && !(getenv("SDR_XWAVE") && getenv("SDR_XWAVE")[0] == '0')) {
-      // the u8 kernel's hand-off records: allocated and zeroed once per context (stream-ordered)
+    const bool xw_on = !(getenv("SDR_XWAVE") && getenv("SDR_XWAVE")[0] == '0');   // (0: warm-up tiles, A/B)
+    if (xw_on && c->xwave == nullptr) {
+      // the fused kernels' run-boundary hand-off records: allocated and zeroed once per context
+      // (stream-ordered before the first kernel that counts on the zeroed arrival counters)
       HIP_TRY(hipMalloc(&c->xwave, SDR_XWAVE_BYTES));
       HIP_TRY(hipMemsetAsync(c->xwave, 0, SDR_XWAVE_BYTES, c->stream));
     }
-    a.xwave = c->xwave;
+    a.xwave = xw_on ? c->xwave : nullptr;
     const hipError_t e = sdr_launch_fe_mono(a, ats->dev_f32, ats->dev_rev, audio_taps, audio_decim, audio, as, c->stream);
     if (e == hipSuccess) return SDR_OK;
     if (e != hipErrorInvalidValue) HIP_TRY(e);

@@ -603,7 +603,7 @@ template <int SPEC_T, bool LONG, bool first = false>
 __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const int tid) {
 #pragma clang fp contract(off)
   // Per step k = 1 .. n-1, at slot i * CSTR + j (step i of chunk j, see the staging below):
-  // the sign code of x_k (0: x > 0, 1: x < 0, 2: 0 / NaN) -- the constant c_k is a function
+  // the sign code of x_k (+1: x > 0, -1: x < 0, 0: 0 / NaN; r04b: the sign itself, as the correlation uses it) -- the constant c_k is a function
   // of it and k alone (pll_c), recomputed where it is used, which keeps the workgroup's LDS
   // at ~68 KB (two per CU) instead of a 128 KiB f64 image -- and the low byte of m_k
   // (jb = floor(phaseEst_1 / 2pi)).  tb: per wave, SB steps x 64 chunks of phases on their
@@ -707,14 +707,14 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // long call, fix kernel -- runs with qform = 0, sdr_launch_pll_loop; the Q-form rows are the
   // sequential chunk kernel's alone)
   auto thval = [&](double ph, int64_t) { return ph; };
-  // c_k from the sign code: pll_c's arithmetic exactly (code 2, a 0 / NaN input, is caught by
+  // c_k from the sign code: pll_c's arithmetic exactly (code 0, a 0 / NaN input, is caught by
   // the guess: the solve is abandoned to the general form, so its value here does not matter)
   const double w2pi = sgpr_d(w * kInv2Pi);
   if (tid == 0) { wsh = w; kds = kD; }
-  auto cval = [&](int cd, int k) { return fma(-(off + (double)k), w2pi, cd == 0 ? 0.5 : 1.0); };
+  auto cval = [&](int cd, int k) { return fma(-(off + (double)k), w2pi, cd > 0 ? 0.5 : 1.0); };
   // ... from offk = off + k itself: the step loops carry offk as an f64 counter (+1.0 a step, exact
   // for the integer-valued trigOffset) instead of converting k every step (cval's value exactly)
-  auto cvk = [&](int cd, double offk) { return fma(-offk, w2pi, cd == 0 ? 0.5 : 1.0); };
+  auto cvk = [&](int cd, double offk) { return fma(-offk, w2pi, cd > 0 ? 0.5 : 1.0); };
   // sample 0: the literal general step (thread 0), as the loop kernels' general() (a
   // pre-roll's seed is set from the measured phase instead, below)
   if (tid == 0 && pre == 0) {
@@ -747,7 +747,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     float xv[SG];
 #pragma unroll
     for (int u = 0; u < SG; ++u) xv[u] = in[min(tid + u * SPEC_T, N - 1) + 1];
-    auto cod = [](float x) { return (int8_t)(x > 0.f ? 0 : (x < 0.f ? 1 : 2)); };
+    auto cod = [](float x) { return (int8_t)(x > 0.f ? 1 : (x < 0.f ? -1 : 0)); };
     if (SPEC_T % L == 0) {
       // element kk = tid + u SPEC_T: i = tid mod L for every u, j = tid / L + u SPEC_T / L
       int8_t* cb = code + (tid % L) * CSTR + tid / L;
@@ -767,6 +767,12 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   }
   __syncthreads();
   SPEC_TP();
+  // r04b: a wave whose chunks are all full runs the step loops without a per-step "inside the
+  // chunk" predicate (its selects and compares were a fifth of the check loop's VALU); the wave
+  // holding the last, partial chunk (and the unused ones) keeps them.  wfast: also every chunk
+  // after a long call's pre-roll, so every step's wrap margin counts and every phase is stored.
+  const bool wfull = __all(len == L);
+  const bool wfast = wfull && __all(k0 >= pre);
   // 0. where the locked phase estimate goes within the block, measured from the input: a
   // locked loop keeps its angle th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's
   // phase, so z_j = sum over chunk j of x_k exp(-i w (off + k)) ~ (A/2) exp(i phaseEst) (+ an
@@ -781,29 +787,40 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     // correlation, as the loop's detector.  The nominal NCO's phasor exp(i w (off + k)) is
     // rotated by exp(i w) from the chunk's first step in f32 (L <= 64 steps: a drift of ~1e-6,
     // far below what a guess needs -- the check, not the guess, makes the solve exact)
-    float zr = 0.f, zi = 0.f;
+    // r04b: packed f32 -- the phasor (cr, ci) and the sums in register pairs: per step one
+    // v_pk_fma_f32 accumulates sg (cr, ci) (zi = -its second half) and a v_pk_mul + v_pk_fma
+    // rotate the phasor: (cr, ci) <- (cr dc - ci ds, ci dc + cr ds) (the swapped operand by
+    // op_sel); the sign code IS sg.  (A guess: the check, not this, makes the solve exact.)
+    f2v z = f2v{0.f, 0.f};
     {
       const double a0 = __builtin_amdgcn_fract(w2pi * (off + (double)k0));
       float ci, cr, ds, dc;
       __sincosf((float)(k2Pi * a0), &ci, &cr);
       __sincosf((float)w, &ds, &dc);
-      for (int i0 = 0; i0 < L; i0 += SB) {
-        int cd[SB];
+      f2v c = f2v{cr, ci};
+      f2v dcv = f2v{dc, dc}, dsv = f2v{-ds, ds};
+      auto corr = [&](auto FC) __attribute__((always_inline)) {
+        constexpr bool F = decltype(FC)::value;
+        f2v rs = dsv;
+        for (int i0 = 0; i0 < L; i0 += SB) {
+          int cd[SB];
 #pragma unroll
-        for (int u = 0; u < SB; ++u) cd[u] = code[(i0 + u) * CSTR + tid];
+          for (int u = 0; u < SB; ++u) cd[u] = code[(i0 + u) * CSTR + tid];
 #pragma unroll
-        for (int u = 0; u < SB; ++u) {
-          // x > 0: +exp(-i a); x < 0: -exp(-i a) (the pi of sel); 0 / NaN / past the chunk: 0
-          const float sg = (i0 + u < len && cd[u] != 2) ? (cd[u] == 0 ? 1.f : -1.f) : 0.f;
-          zr = fmaf(sg, cr, zr);
-          zi = fmaf(-sg, ci, zi);
-          const float nr = cr * dc - ci * ds;
-          ci = fmaf(cr, ds, ci * dc);
-          cr = nr;
+          for (int u = 0; u < SB; ++u) {
+            // x > 0: +exp(-i a); x < 0: -exp(-i a) (the pi of sel); 0 / NaN / past the chunk: 0
+            const float sg = (F || i0 + u < len) ? (float)cd[u] : 0.f;
+            const f2v sgv = f2v{sg, sg};
+            asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(z) : "v"(sgv), "v"(c));
+            const f2v t = c * dcv;
+            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1]" : "=v"(c) : "v"(c), "v"(rs), "v"(t));
+          }
         }
-      }
+      };
+      if (wfull) corr(std::true_type{});
+      else corr(std::false_type{});
     }
-    yb[tid] = d2v{(double)zr, (double)zi};
+    yb[tid] = d2v{(double)z.x, -(double)z.y};
     __syncthreads();
     double sr = 0.0, si = 0.0;
     for (int o = -2; o <= 2; ++o) {
@@ -840,12 +857,6 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // solve needs no pass of its own; the check below validates whatever this rounds to)
   bool bad = false;
   double xs_p = 0.0, xs_v = 0.0, xe_p = 0.0, xe_v = 0.0;
-  // r04b: a wave whose chunks are all full runs the step loops without a per-step "inside the
-  // chunk" predicate (its selects and compares were a fifth of the check loop's VALU); the wave
-  // holding the last, partial chunk (and the unused ones) keeps them.  wfast: also every chunk
-  // after a long call's pre-roll, so every step's wrap margin counts and every phase is stored.
-  const bool wfull = __all(len == L);
-  const bool wfast = wfull && __all(k0 >= pre);
   {
     // the true step from a seed on the measured drift: phaseEst ~ p1 + D at the warm-up's
     // start, integ ~ the measured drift per step; 256 steps of the loop then pull the guess
@@ -856,27 +867,36 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     double p = p1 + yb[jw].x, V = v1;
     if (k0 - kw >= 64 && tid < TE) V = (yb[tid].x - yb[jw].x) / (double)(k0 - kw) - kds;
     const int W = tid < TE ? k0 - kw : 0;        // warm-up steps (over the chunks before this one)
-    if (wfull && SW <= L) {
-      // every warm-up is the last SW steps of the previous chunk (thread 0 has none: it runs SW
-      // discarded steps over chunk 0 and takes its seed back)
+    if (wfull && SW <= 2 * L) {
+      // every warm-up is the last SW steps before the chunk: the last SW - L of chunk j-2 when
+      // SW > L (the per-block C4 solve: L = 24, SW = 32), then the last min(SW, L) of chunk j-1.
+      // Threads with a shorter warm-up (j = 0: none; j = 1 when SW > L: L steps) run the same
+      // passes over chunk 0 and take their seed back before the part that is theirs.
       const double p0 = p, v0 = V;
-      const int jc = max(tid - 1, 0);
       double kd = off + (double)(k0 - SW);
+      auto pass = [&](int jc, int ib, int ns) __attribute__((always_inline)) {
 #pragma unroll 1
-      for (int i0 = 0; i0 < SW; i0 += SB) {
-        int cd[SB];
+        for (int i0 = 0; i0 < ns; i0 += SB) {
+          int cd[SB];
 #pragma unroll
-        for (int u = 0; u < SB; ++u) cd[u] = code[(L - SW + i0 + u) * CSTR + jc];
+          for (int u = 0; u < SB; ++u) cd[u] = code[(ib + i0 + u) * CSTR + jc];
 #pragma unroll
-        for (int u = 0; u < SB; ++u) {
-          const double t = fma(-kInv2Pi, p, cvk(cd[u], kd));
-          kd += 1.0;
-          const double f = __builtin_amdgcn_fract(t);
-          const double S = p + V;
-          V = fma(kA, f, V - kB);
-          p = fma(kC, f, S);
+          for (int u = 0; u < SB; ++u) {
+            const double t = fma(-kInv2Pi, p, cvk(cd[u], kd));
+            kd += 1.0;
+            const double f = __builtin_amdgcn_fract(t);
+            const double S = p + V;
+            V = fma(kA, f, V - kB);
+            p = fma(kC, f, S);
+          }
         }
+      };
+      if (SW > L) {
+        pass(max(tid - 2, 0), 2 * L - SW, SW - L);
+        if (W < SW) { p = p0; V = v0; }
       }
+      const int s2 = SW > L ? L : SW;
+      pass(max(tid - 1, 0), L - s2, s2);
       if (W == 0) { p = p0; V = v0; }
     } else {
       int jc = jw, ic = (kw - 1) - jw * L;       // (chunk, step) of step kw
@@ -915,7 +935,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
           const double t = fma(-kInv2Pi, p, cvk(cd[u], kd));
           kd += 1.0;
           const bool act = F || i < len;
-          bad |= act && cd[u] == 2;                // a 0 / NaN input: the general form's case
+          bad |= act && cd[u] == 0;                // a 0 / NaN input: the general form's case
           const double f = __builtin_amdgcn_fract(t);
           if (act) mrel[i * CSTR + tid] = floor_byte(t, f);
           const double S = p + V;
