@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--path", choices=["fused", "split"], default="fused",
                     help="fused: one fe_mono_kernel (demod stays on chip); split: FE kernel + FIR kernel")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--depth", type=int, default=2,
+                    help="c3 / c4: sdr_rx_submit depth (blocks in flight; sdr_rx_set_depth)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="c3/c4/c5: one block at a time (c3/c4: sdr_rx_run; c5: one stream of launches)")
     ap.add_argument("--split-stream", action="store_true",
@@ -588,9 +590,10 @@ def rx_measure(ctx, workload, args, rank, ws, steps, warmup, cpu=False):
     # the second stream only pays where there is a back half (PLLs, stereo / RDS stages) to
     # overlap; c3's two launches gain nothing from it but the cross-stream event hops
     two_streams = pipe and (stereo or rds)
-    mk = lambda two: rtsdr.Receiver(S, B, stereo=stereo, rds=rds, iq_dtype=np.uint8 if u8 else np.float32,
-                                    rf_coeff=rf_b, audio_coeff=au_b, pipeline=two, ctx=ctx)
-    rx = mk(two_streams)
+    depth = 1 if c5 else max(1, args.depth)
+    mk = lambda two, d=1: rtsdr.Receiver(S, B, stereo=stereo, rds=rds, iq_dtype=np.uint8 if u8 else np.float32,
+                                         rf_coeff=rf_b, audio_coeff=au_b, pipeline=two, depth=d, ctx=ctx)
+    rx = mk(two_streams, depth if pipe else 1)
     rx_sync = mk(False) if (pipe and not c5) else rx     # the one-block-at-a-time call
     nres = 16                                           # distinct blocks per stream, cycled
     dt = np.uint8 if u8 else np.float32
@@ -609,7 +612,7 @@ def rx_measure(ctx, workload, args, rank, ws, steps, warmup, cpu=False):
         def sync_step(k):
             return rx_sync.process(host[k % nres], fetch=fetch)
 
-        def step(k):                         # block k launched, block k-1 delivered
+        def step(k):                         # block k launched, block k-depth delivered
             if not pipe:
                 return sync_step(k)
             return rx.submit(host[k % nres], fetch=fetch)
@@ -706,7 +709,8 @@ def rx_measure(ctx, workload, args, rank, ws, steps, warmup, cpu=False):
                        "block_complex": B, "streams_per_gpu": S, "rf_taps": rf_taps, "iq": "u8" if u8 else "f32",
                        "parallelism": f"independent streams x{S * ws}",
                        "pipeline": " + ".join(
-                           (["sdr_rx_submit: block k launched while block k-1 is delivered"] if not c5 else [])
+                           ([f"sdr_rx_submit: block k launched while block k-{depth} is delivered "
+                             f"({depth} block{'s' if depth > 1 else ''} in flight)"] if (not c5 and pipe) else [])
                            + (["front half (FE, stage A) of block k beside the back half of k-1 (two streams)"]
                               if two_streams else [])) or None},
             "roofline": {"bound": "hbm", "achieved": round(fe_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -283,6 +283,13 @@ enum { SDR_RX_MAXOUT = 32 };
 int sdr_rx_submit(sdr_rx* rx, const void* iq, int64_t iq_stride, int nout, const int* which,
                   float* const* out, const int64_t* out_stride);
 int sdr_rx_flush(sdr_rx* rx);
+/* Submission depth (set before the first block; 1..3, default 1): sdr_rx_submit of block k
+ * delivers block k-depth (not k-1), so `depth` blocks stay in flight while the host prepares
+ * the next one -- the reference's RF thread running ahead of its audio thread through its
+ * queue (src/fm_radio.cpp:783-792).  sdr_rx_flush delivers every block still in flight,
+ * oldest first.  With depth >= 2 a pipelined receiver keeps three output row sets (block k's
+ * rows stay valid until block k+3 is processed). */
+int sdr_rx_set_depth(sdr_rx* rx, int depth);
 /* Pipelined receiver (set before the first block): block k's front half (FE and the
  * filters of the demod) runs on a second stream, its PLLs on a third once block k-1's PLLs
  * are done, and its stereo / RDS stages on the context stream -- so block k's PLLs start

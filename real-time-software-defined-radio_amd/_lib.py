@@ -102,6 +102,7 @@ SIGNATURES = {
     "sdr_rx_submit": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp]),
     "sdr_rx_flush": (_i32, [_vp]),
     "sdr_rx_set_pipeline": (_i32, [_vp, _i32]),
+    "sdr_rx_set_depth": (_i32, [_vp, _i32]),
     "sdr_rx_output": (_i32, [_vp, _i32, _c.POINTER(_vp), _c.POINTER(_i64), _c.POINTER(_i64)]),
     "sdr_rx_fetch": (_i32, [_vp, _i32, _fp, _i64]),
     "sdr_rx_state": (_i32, [_vp, _dp, _dp, _dp]),

@@ -16,6 +16,7 @@ reference loops:
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 
 import numpy as np
@@ -42,7 +43,7 @@ class Receiver:
     def __init__(self, nstreams: int, block_complex: int, *, mono: bool = True, stereo: bool = False,
                  rds: bool = False, iq_dtype=np.uint8, rf_coeff=None, audio_coeff=None, stereo_taps: int = 151,
                  rds_taps: int = 151, rf_decim: int = 10, audio_decim: int = 5, pipeline: bool = False,
-                 ctx=None):
+                 depth: int = 1, ctx=None):
         self.ctx = ctx if ctx is not None else _lib.get_context()
         self.lib = self.ctx.lib
         self.S, self.B = int(nstreams), int(block_complex)
@@ -51,13 +52,16 @@ class Receiver:
         self.flags = flags
         self._lengths = {}
         self._plans = {}
-        self._pending = None                  # submit(): the block in flight's output arrays
+        self._pending = collections.deque()   # submit(): the blocks in flight's output arrays
+        self.depth = int(depth)
         h = ctypes.c_void_p()
         check(self.lib.sdr_rx_create(self.ctx.handle, self.S, self.B, SDR_IQ_U8 if self.u8 else SDR_IQ_F32,
                                      flags, ctypes.byref(h)), "sdr_rx_create")
         self.handle = h
         if pipeline:                          # front half of block k+1 beside the back half of k
             check(self.lib.sdr_rx_set_pipeline(self.handle, 1), "sdr_rx_set_pipeline")
+        if self.depth != 1:                   # submit(): `depth` blocks in flight
+            check(self.lib.sdr_rx_set_depth(self.handle, self.depth), "sdr_rx_set_depth")
         if rf_coeff is None or audio_coeff is None:
             rc, ac = design.mono_coeffs()
             rf_coeff = rc if rf_coeff is None else rf_coeff
@@ -116,23 +120,27 @@ class Receiver:
         """One block of every stream; returns {name: (nstreams, n) float32} for `fetch`
         (default: the configuration's final outputs).  One C call: IQ up, the chain, the
         outputs down, one wait (sdr_rx_run)."""
-        if self._pending is not None:         # a submitted block is delivered (and dropped) first
+        if self._pending:                     # submitted blocks are delivered (and dropped) first
             self.flush()
         return self._call("sdr_rx_run", iq, fetch)
 
     def submit(self, iq, fetch=None):
         """process() without waiting (sdr_rx_submit): launches this block and returns the
-        PREVIOUS submitted block's outputs (None for the first), so the host prepares the
-        next block while this one runs.  flush() returns the last block's."""
-        outs = self._call("sdr_rx_submit", iq, fetch)
-        prev, self._pending = self._pending, outs
-        return prev
+        outputs of the block submitted `depth` calls earlier (None while the pipeline fills:
+        depth 1 = the PREVIOUS block), so the host prepares the next block while these run.
+        flush() returns the rest."""
+        self._pending.append(self._call("sdr_rx_submit", iq, fetch))
+        return self._pending.popleft() if len(self._pending) > self.depth else None
 
     def flush(self):
-        """Wait for the last submitted block; its outputs (or None)."""
+        """Wait for every submitted block: depth 1, the last block's outputs (or None); deeper,
+        the list of the blocks' outputs not yet returned, oldest first."""
         check(self.lib.sdr_rx_flush(self.handle), "sdr_rx_flush")
-        prev, self._pending = self._pending, None
-        return prev
+        rest = list(self._pending)
+        self._pending.clear()
+        if self.depth == 1:
+            return rest[-1] if rest else None
+        return rest
 
     def _length(self, name):
         if name not in self._lengths:
@@ -173,7 +181,7 @@ class Receiver:
 
     def reset(self):
         check(self.lib.sdr_rx_reset(self.handle), "sdr_rx_reset")
-        self._pending = None
+        self._pending.clear()
 
     def set_timing(self, on: bool = True):
         """Record HIP events between the receiver's launches (stage_ms)."""

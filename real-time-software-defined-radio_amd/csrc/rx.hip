@@ -541,7 +541,7 @@ struct sdr_rx {
   bool ready = false;
   int64_t M = 0, A = 0, R = 0;
   float* out[SDR_RX_NOUTPUTS] = {};    // the rows of the latest block (one of outs[])
-  float* outs[2][SDR_RX_NOUTPUTS] = {}; // row sets; the second only when pipelined
+  float* outs[3][SDR_RX_NOUTPUTS] = {}; // row sets: nq when pipelined, else one
   int64_t out_n[SDR_RX_NOUTPUTS] = {}, out_stride[SDR_RX_NOUTPUTS] = {};
   void* mem = nullptr;                 // one allocation for outputs, states and phases
   double* bank[2] = {};
@@ -566,22 +566,25 @@ struct sdr_rx {
   int parity = 0;
   int64_t blocks = 0;
   // sdr_rx_set_pipeline: block k's front half (FE, stage A) runs on `front` while block
-  // k-1's back half (B, PLLs, C, D, E) runs on the context stream; row set k % 2
+  // k-1's back half (B, PLLs, C, D, E) runs on the context stream; row set k % nq
   int pipe = 0;
+  int nq = 2;                           // row sets when pipelined (3 with sdr_rx_set_depth >= 2)
   hipStream_t front = nullptr;          // FE, stages A and B
   hipStream_t mid = nullptr;            // the PLLs (prep, lanes, NCO)
-  hipEvent_t ev_front[2] = {}, ev_mid[2] = {}, ev_back[2] = {}, ev_done[2] = {};
-  // sdr_rx_submit: pinned slots (input and outputs per block parity) and the block in flight
+  hipEvent_t ev_front[3] = {}, ev_mid[3] = {}, ev_back[3] = {}, ev_done[4] = {};
+  // sdr_rx_submit: depth blocks in flight before a submit waits (sdr_rx_set_depth); pinned
+  // slots (input and outputs) per block, depth + 1 of them; the blocks in flight, oldest first
+  int depth = 1;
   size_t in_slot = 0, out_slot = 0;
   int64_t subs = 0;
   struct Pending {
-    bool on = false;
     int slot = 0, nout = 0;
     int which[SDR_RX_MAXOUT] = {};
     float* out[SDR_RX_MAXOUT] = {};
     int64_t os[SDR_RX_MAXOUT] = {};
     size_t region[SDR_RX_NOUTPUTS] = {};
-  } pend;
+  } pq[3];
+  int pq_head = 0, pq_n = 0;
   bool timing = false;                 // events between the stages of each block
   hipEvent_t ev[SDR_RX_NSTAGES + 1] = {};
 };
@@ -660,7 +663,7 @@ int rx_finalize(sdr_rx* r) {
     r->out_n[o] = n;
     r->out_stride[o] = st;
   }
-  for (int q = 0; q < (r->pipe ? 2 : 1); ++q)
+  for (int q = 0; q < (r->pipe ? r->nq : 1); ++q)
     for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) {
       if (!need_out(r, o)) continue;
       r->outs[q][o] = reinterpret_cast<float*>((intptr_t)floats);   // offset for now
@@ -678,7 +681,7 @@ int rx_finalize(sdr_rx* r) {
   r->ths = round_up(M, 2) + 2;
   r->cst = round_up(M + M / 32, 2) + 2;
   const int64_t S2 = round_up(S, 2);                 // keeps the phase rows 16-B aligned
-  const int nsets = r->pipe ? 2 : 1;
+  const int nsets = r->pipe ? r->nq : 1;
   const int64_t doubles = 2 * zl + 3 * S2 + 2 * 6 * S2 + nsets * (2 * S * r->ths + 2 * S * r->cst);
   r->pllw_bytes = round_up(sdr_pll_work_bytes(2, r->S, M), 256);
   const size_t bytes = (size_t)floats * 4 + 64 + (size_t)doubles * 8 + 256 + (size_t)(nsets * r->pllw_bytes);
@@ -686,7 +689,7 @@ int rx_finalize(sdr_rx* r) {
   hipError_t e = hipMalloc(&r->mem, bytes);
   if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx: hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
   char* base = static_cast<char*>(r->mem);
-  for (int q = 0; q < (r->pipe ? 2 : 1); ++q)
+  for (int q = 0; q < (r->pipe ? r->nq : 1); ++q)
     for (int o = 0; o < SDR_RX_NOUTPUTS; ++o)
       if (need_out(r, o)) r->outs[q][o] = reinterpret_cast<float*>(base) + (intptr_t)r->outs[q][o];
   std::memcpy(r->out, r->outs[0], sizeof r->out);
@@ -743,9 +746,11 @@ void sdr_rx_destroy(sdr_rx* r) {
   if (r->pin_out) (void)hipHostFree(r->pin_out);
   for (hipEvent_t e : r->ev)
     if (e) (void)hipEventDestroy(e);
-  for (int q = 0; q < 2; ++q)
-    for (hipEvent_t e : {r->ev_front[q], r->ev_mid[q], r->ev_back[q], r->ev_done[q]})
+  for (int q = 0; q < 3; ++q)
+    for (hipEvent_t e : {r->ev_front[q], r->ev_mid[q], r->ev_back[q]})
       if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : r->ev_done)
+    if (e) (void)hipEventDestroy(e);
   if (r->front) (void)hipStreamDestroy(r->front);
   if (r->mid) (void)hipStreamDestroy(r->mid);
   delete r;
@@ -788,7 +793,7 @@ int sdr_rx_reset(sdr_rx* r) {
   hipStream_t st = r->c->stream;
   if (r->front) HIP_TRY(hipStreamSynchronize(r->front));
   if (r->mid) HIP_TRY(hipStreamSynchronize(r->mid));
-  r->pend.on = false;                            // a submitted block's outputs are dropped
+  r->pq_n = 0;                                   // submitted blocks' outputs are dropped
   // state banks, phases and wrap counters (contiguous)
   HIP_TRY(hipMemsetAsync(r->bank[0], 0, sizeof(double) * (size_t)(2 * r->bank_len + 2 * round_up(r->S, 2)), st));
   std::vector<double> ps(6 * (size_t)r->S);
@@ -812,7 +817,7 @@ int sdr_rx_set_pipeline(sdr_rx* r, int on) {
     TRY(set_dev(r->c));
     HIP_TRY(hipStreamCreateWithFlags(&r->front, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&r->mid, hipStreamNonBlocking));
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < 3; ++q) {
       HIP_TRY(hipEventCreateWithFlags(&r->ev_front[q], hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&r->ev_mid[q], hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&r->ev_back[q], hipEventDisableTiming));
@@ -834,7 +839,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   const int64_t M = r->M;
   double* zi = r->bank[r->parity];
   double* zf = r->bank[r->parity ^ 1];
-  const int q = r->pipe ? (int)(r->blocks & 1) : 0;
+  const int q = r->pipe ? (int)(r->blocks % r->nq) : 0;
   // FE: RF FIR + decimate + demod (fe.hip).  The tiled kernels take the reference's RF
   // configurations; their carried state (I/Q zf, demod phase) is finished by workgroups of
   // the stage-A launch.  Other configurations run sdr_rf_frontend_dev's generic path (on the
@@ -846,8 +851,8 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
                     ((uintptr_t)iq % (r->u8 ? 4 : 16)) == 0;
   hipStream_t fs = (r->pipe && fast) ? r->front : st;
   if (r->pipe) {
-    if (r->blocks >= 1) HIP_TRY(hipStreamWaitEvent(fs, r->ev_front[q ^ 1], 0));   // states of block k-1
-    if (r->blocks >= 2) HIP_TRY(hipStreamWaitEvent(fs, r->ev_back[q], 0));        // set q read by k-2
+    if (r->blocks >= 1) HIP_TRY(hipStreamWaitEvent(fs, r->ev_front[(q + r->nq - 1) % r->nq], 0));   // states of block k-1
+    if (r->blocks >= r->nq) HIP_TRY(hipStreamWaitEvent(fs, r->ev_back[q], 0));    // set q read by k-nq
   }
   auto mark = [&](int k, hipStream_t s) { return r->timing ? hipEventRecord(r->ev[k], s) : hipSuccess; };
   HIP_TRY(mark(0, fs));
@@ -953,7 +958,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     HIP_TRY(hipEventRecord(r->ev_front[q], fs));
     if (plls && mid) {
       HIP_TRY(hipStreamWaitEvent(ps, r->ev_front[q], 0));
-      if (r->blocks >= 2) HIP_TRY(hipStreamWaitEvent(ps, r->ev_back[q], 0));
+      if (r->blocks >= r->nq) HIP_TRY(hipStreamWaitEvent(ps, r->ev_back[q], 0));
     } else {
       HIP_TRY(hipStreamWaitEvent(st, r->ev_front[q], 0));
     }
@@ -1038,10 +1043,12 @@ bool stage_output(int o) {
 }
 
 // Deliver the block in flight: wait for it, copy its rows out of pinned memory.
+// the oldest block in flight: wait for it, copy its outputs out of its pinned slot
 int deliver(sdr_rx* r) {
-  sdr_rx::Pending& P = r->pend;
-  if (!P.on) return SDR_OK;
-  P.on = false;
+  if (r->pq_n == 0) return SDR_OK;
+  const sdr_rx::Pending& P = r->pq[r->pq_head];
+  r->pq_head = (r->pq_head + 1) % 3;
+  --r->pq_n;
   HIP_TRY(hipEventSynchronize(r->ev_done[P.slot]));
   const float* base = r->pin_out + (size_t)P.slot * r->out_slot / sizeof(float);
   for (int i = 0; i < P.nout; ++i) {
@@ -1065,8 +1072,8 @@ int sdr_rx_process(sdr_rx* r, const void* iq_host, int64_t iq_stride) {
 // IQ is copied into a pinned slot and the FE kernel reads it from there over PCIe; each
 // requested output is stored into the slot's pinned output region by the stage kernel that
 // produces it (the demod and NCO rows, which no stage kernel stores, come back by copy).
-// Two slots by block parity: while block k runs, the host delivers block k-1's outputs
-// (into the buffers given with k-1) and returns; sdr_rx_flush delivers the last one.
+// depth + 1 slots (sdr_rx_set_depth, default 1): while block k runs, the host delivers block
+// k-depth's outputs (into the buffers given with it) and returns; sdr_rx_flush delivers the rest.
 int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, const int* which, float* const* out,
                   const int64_t* out_stride) {
   if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
@@ -1102,17 +1109,18 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
     obytes += sizeof(float) * (size_t)(r->out_n[o] * r->S);
   }
   const size_t in_slot = (bytes + 255) / 256 * 256, out_slot = (std::max<size_t>(obytes, 16) + 255) / 256 * 256;
-  if (in_slot > r->in_slot || out_slot > r->out_slot) {   // grow (the block in flight is delivered first)
-    TRY(deliver(r));
-    TRY(grow_pinned(r, &r->pin_in, &r->pin_in_cap, 2 * in_slot));
-    TRY(grow_pinned(r, reinterpret_cast<void**>(&r->pin_out), &r->pin_out_cap, 2 * out_slot));
+  const int nslot = r->depth + 1;
+  if (in_slot > r->in_slot || out_slot > r->out_slot) {   // grow (the blocks in flight are delivered first)
+    while (r->pq_n > 0) TRY(deliver(r));
     r->in_slot = std::max(r->in_slot, in_slot);
     r->out_slot = std::max(r->out_slot, out_slot);
-    for (int q = 0; q < 2; ++q)
+    TRY(grow_pinned(r, &r->pin_in, &r->pin_in_cap, nslot * r->in_slot));
+    TRY(grow_pinned(r, reinterpret_cast<void**>(&r->pin_out), &r->pin_out_cap, nslot * r->out_slot));
+    for (int q = 0; q < nslot; ++q)
       if (!r->ev_done[q]) HIP_TRY(hipEventCreateWithFlags(&r->ev_done[q], hipEventDisableTiming));
   }
-  const int slot = (int)(r->subs & 1);
-  // slot `slot` was last used by block k-2, delivered (waited for) by the previous call
+  const int slot = (int)(r->subs % nslot);
+  // slot `slot` was last used by block k-depth-1, delivered (waited for) by the previous call
   char* pin = static_cast<char*>(r->pin_in) + (size_t)slot * r->in_slot;
   float* pout = r->pin_out + (size_t)slot * r->out_slot / sizeof(float);
   std::memcpy(pin, iq_host, bytes);
@@ -1129,19 +1137,29 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
   }
   HIP_TRY(hipEventRecord(r->ev_done[slot], st));
   ++r->subs;
-  TRY(deliver(r));                                       // block k-1
-  P.on = true;
   P.slot = slot;
   P.nout = nout;
-  r->pend = P;
+  r->pq[(r->pq_head + r->pq_n) % 3] = P;
+  ++r->pq_n;
+  while (r->pq_n > r->depth) TRY(deliver(r));            // block k-depth
   return SDR_OK;
 }
 
 int sdr_rx_flush(sdr_rx* r) {
   if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
-  if (!r->pend.on) return SDR_OK;
+  if (r->pq_n == 0) return SDR_OK;
   TRY(set_dev(r->c));
-  return deliver(r);
+  while (r->pq_n > 0) TRY(deliver(r));
+  return SDR_OK;
+}
+
+int sdr_rx_set_depth(sdr_rx* r, int depth) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  if (r->ready) return fail(SDR_EINVAL, "sdr_rx_set_depth: the receiver has processed a block");
+  if (depth < 1 || depth > 3) return fail(SDR_EINVAL, "sdr_rx_set_depth: depth %d outside [1, 3]", depth);
+  r->depth = depth;
+  r->nq = depth >= 2 ? 3 : 2;
+  return SDR_OK;
 }
 
 // One block from host memory, waited for: the per-block drop-in call of fmMonoBlock.py's loop.

@@ -154,26 +154,29 @@ def test_receiver_argument_errors(sdr, gpu_ctx):
         _lib.check(gpu_ctx.lib.sdr_rx_create(gpu_ctx.handle, 1, 100, 0, 8, ctypes.byref(h)), "bad flags")
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
-def test_receiver_submit_equals_process(sdr, gpu_ctx, pipeline):
-    """sdr_rx_submit / sdr_rx_flush (block k launched, block k-1 delivered) == sdr_rx_run
-    block by block, bit for bit, for every output -- the stage-stored ones (pinned host
-    stores) and the copied ones (demod, NCOs) -- with and without the two-stream pipeline."""
-    B, S, nb = 51_200, 2, 4
+@pytest.mark.parametrize("pipeline,depth", [(False, 1), (True, 1), (False, 2), (True, 2), (True, 3)])
+def test_receiver_submit_equals_process(sdr, gpu_ctx, pipeline, depth):
+    """sdr_rx_submit / sdr_rx_flush (block k launched, block k-depth delivered; r04b: depth 2
+    and 3 keep that many blocks in flight, a pipelined receiver then three row sets) ==
+    sdr_rx_run block by block, bit for bit, for every output -- the stage-stored ones (pinned
+    host stores) and the copied ones (demod, NCOs) -- with and without the two-stream pipeline."""
+    B, S, nb = 51_200, 2, 6
     iq = np.stack([sdr.synth.fm_iq(nb * B, seed=60 + s) for s in range(S)])
     kw = dict(stereo=True, rds=True, iq_dtype=np.float32)
     ref_rx = sdr.Receiver(S, B, **kw)
-    rx = sdr.Receiver(S, B, pipeline=pipeline, **kw)
+    rx = sdr.Receiver(S, B, pipeline=pipeline, depth=depth, **kw)
     names = ref_rx.outputs
     want = [ref_rx.process(iq[:, 2 * k * B:2 * (k + 1) * B], fetch=names) for k in range(nb)]
     got = []
     for k in range(nb):
         prev = rx.submit(iq[:, 2 * k * B:2 * (k + 1) * B], fetch=names)
-        assert (prev is None) == (k == 0)
+        assert (prev is None) == (k < depth)
         if prev is not None:
             got.append(prev)
-    got.append(rx.flush())
-    assert rx.flush() is None
+    rest = rx.flush()
+    got.extend([rest] if depth == 1 else rest)
+    assert len(got) == nb
+    assert rx.flush() == (None if depth == 1 else [])
     for k in range(nb):
         for name in names:
             assert np.array_equal(got[k][name], want[k][name]), (name, k)

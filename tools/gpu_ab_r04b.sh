@@ -13,8 +13,11 @@ tail -3 "$O/pytest_gpu.txt"
 [ $rc -le 1 ] || { echo "pytest rc $rc: stopping"; exit $rc; }
 set -e
 bash tools/ab_bench.sh gpurun_out/r04b/ab_u8 3 "--iq,u8,--no-extras,--no-cpu" prod SDR_XWAVE=0
-bash tools/ab_bench.sh gpurun_out/r04b/ab_ring 3 "--no-extras,--no-cpu" base prod SDR_XWAVE=0 q16
+bash tools/ab_bench.sh gpurun_out/r04b/ab_ring 3 "--no-extras,--no-cpu" base prod SDR_XWAVE=0
 bash tools/ab_bench.sh gpurun_out/r04b/ab_c5 2 "--workload,c5,--steps,5,--no-cpu" base prod
 bash tools/ab_bench.sh gpurun_out/r04b/ab_c4 2 "--workload,c4,--no-cpu" base prod
+bash tools/ab_bench.sh gpurun_out/r04b/ab_c4d1 2 "--workload,c4,--no-cpu,--depth,1" prod
+bash tools/ab_bench.sh gpurun_out/r04b/ab_c3 2 "--workload,c3,--no-cpu" prod
+bash tools/ab_bench.sh gpurun_out/r04b/ab_c3d1 2 "--workload,c3,--no-cpu,--depth,1" prod
 bash tools/ab_bench.sh gpurun_out/r04b/ab_c5b64 2 "--workload,c5,--streams,64,--span,1,--steps,20,--warmup,5,--no-cpu" base prod
 bash tools/gpu_round.sh gpurun_out/r04b pmc:fused_fetch:FETCH_SIZE:--no-extras,--steps,10 pmc:u8_fetch:FETCH_SIZE:--iq,u8,--no-extras,--steps,10
