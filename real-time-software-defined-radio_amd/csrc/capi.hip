@@ -17,7 +17,6 @@
 #include <cmath>
 #include <new>
 #include <cstdarg>
-#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -223,7 +222,6 @@ void sdr_destroy(sdr_ctx* c) {
   for (int s = 0; s < S_NSLOT; ++s) if (c->slot[s]) (void)hipFree(c->slot[s]);
   for (TapSet& t : c->taps) { (void)hipFree(t.dev_f32); (void)hipFree(t.dev_f64); (void)hipFree(t.dev_afr); }
   if (c->pll_stats) (void)hipFree(c->pll_stats);
-  if (c->xwave) (void)hipFree(c->xwave);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -473,14 +471,6 @@ int sdr_fe_mono_dev(sdr_ctx* c, const void* iq, int iq_dtype, int64_t n, int64_t
     FeLaunch a{iq, n, xs, 0, nstreams, rts->dev_f32, &rts->h, rf_taps, rf_decim, u8, nullptr, nullptr, 0,
                nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr};
     a.afr = rts->dev_afr;
-    const bool xw_on = !(getenv("SDR_XWAVE") && getenv("SDR_XWAVE")[0] == '0');   // (0: warm-up tiles, A/B)
-    if (xw_on && c->xwave == nullptr) {
-      // the fused kernels' run-boundary hand-off records: allocated and zeroed once per context
-      // (stream-ordered before the first kernel that counts on the zeroed arrival counters)
-      HIP_TRY(hipMalloc(&c->xwave, SDR_XWAVE_BYTES));
-      HIP_TRY(hipMemsetAsync(c->xwave, 0, SDR_XWAVE_BYTES, c->stream));
-    }
-    a.xwave = xw_on ? c->xwave : nullptr;
     const hipError_t e = sdr_launch_fe_mono(a, ats->dev_f32, ats->dev_rev, audio_taps, audio_decim, audio, as, c->stream);
     if (e == hipSuccess) return SDR_OK;
     if (e != hipErrorInvalidValue) HIP_TRY(e);

@@ -422,8 +422,6 @@ struct RingArgs {
   float* audio;        // FUSED: per stream ceil(M/5) audio samples, audio_stride apart
   int64_t audio_stride;
   const float* ataps;  // FUSED: 151 audio taps (device)
-  float* xw;           // FUSED, nullable: run-boundary hand-off records (SDR_XWAVE_REC floats each)
-  int* xc;             // ... and their arrival counters (as fe_mfma_mono_kernel's)
 };
 
 template <int T, bool FUSED>
@@ -516,20 +514,12 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
   int s = (int)(g0 / a.tps);
   int i = (int)(g0 - (int64_t)s * a.tps);
   int U = (int)(g1 - g0);
-  bool mid = false, wu = false;
-  // a run starting mid-stream needs the audio history before its first tile.  With hand-off
-  // records (a.xw, r04b) the outputs whose windows reach across the run boundary (30 of them)
-  // are computed by the boundary's second arrival at its run end (below); without them, the
-  // run first runs the warm-up tile i-1 (wu).  A run may start and end mid audio block
-  // (audio_store keeps to the outputs it owns).
-  const bool xh = FUSED && a.xw != nullptr;
-  constexpr int XJ = 30;                           // (TA - 1) / DA outputs straddle a boundary
-  constexpr int XH = 150, XT = 155;                // record: demod [B - 150, B + 155) of boundary B
-  static_assert(XH + XT <= SDR_XWAVE_REC && XT <= TO && XH <= TO, "one tile each side fills the record");
+  bool mid = false;
+  // a run starting mid-stream first runs the warm-up tile i-1 (history / predecessor);
+  // a run may start and end mid audio block (audio_store keeps to the outputs it owns)
   if constexpr (FUSED) {
     mid = i > 0;
-    wu = mid && !xh;
-    if (wu) { --i; ++U; }
+    if (mid) { --i; ++U; }
   }
   // image kinds: 1 guarded build, 2 DMA (whole image), 3 DMA (new chunks; halo by LDS copy)
   enum { K_NONE = 0, K_BUILD = 1, K_FULL = 2, K_HALO = 3 };
@@ -571,7 +561,7 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
   // its tile range): every output is stored by exactly one wave
   auto own_lo = [&](int ss) {
     const int64_t lo = max<int64_t>(g0 - (int64_t)ss * a.tps, 0);
-    return (TO * lo + DA - 1) / DA + ((xh && lo > 0) ? XJ : 0);   // (hand-off: the boundary's XJ)
+    return (TO * lo + DA - 1) / DA;
   };
   auto own_hi = [&](int ss) {
     const int64_t hi = min<int64_t>(g1 - (int64_t)ss * a.tps, a.tps);
@@ -793,26 +783,9 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
 
     // ---- FUSED: demod -> history; after a block's last tile, its audio ----
     if constexpr (FUSED) {
-      const bool warm = wu && u == 0 && (i + 1) % TPB == 0;    // warm-up = previous block's last tile
+      const bool warm = mid && u == 0 && (i + 1) % TPB == 0;   // warm-up = previous block's last tile
       dh_write(i, warm, d);
-      if (xh) {
-        // the hand-off records from this tile's demod: the run's first tile gives its
-        // boundary's samples [B, B + 155), its last tile the next boundary's [B' - 150, B')
-        const int o = R * lane;
-        if (mid && u == 0) {
-          float* rec = a.xw + (int64_t)blockIdx.x * SDR_XWAVE_REC + XH;
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (o + r < XT) rec[o + r] = d[r];
-        }
-        if (u + 1 == U && g1 < a.total && (g1 % a.tps) != 0) {
-          float* rec = a.xw + ((int64_t)blockIdx.x + 1) * SDR_XWAVE_REC - (TO - XH);
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (o + r >= TO - XH) rec[o + r] = d[r];
-        }
-      }
-      const bool last = (u + 1 == U) && !(wu && u == 0);
+      const bool last = (u + 1 == U) && !(mid && u == 0);
       if (!warm && (i % TPB == TPB - 1 || last)) {
         if (i % TPB == TPB - 1 && u + 1 < U && s1 == s) {
           pend = true;                             // computed during the next tile's FIR
@@ -841,51 +814,6 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
     b ^= 1;
   }
   q_flush();
-  if constexpr (FUSED) {
-    // ---- run-boundary hand-off (r04b; as fe_mfma_mono_kernel's) ----
-    // Boundary r (wave r's first tile, mid-stream, at demod sample B) has one record, the demod
-    // samples [B - 150, B + 155): wave r-1's last tile wrote the first 150, wave r's first tile
-    // the rest.  After both arrivals are counted (+2 per boundary per launch: the parity says
-    // which one this is), the second rebuilds the audio window of each block holding the
-    // boundary's 30 straddling outputs -- zeros elsewhere, as the kernel's own zeroed history
-    // -- and runs the same audio_block3: the bits a run holding both sides would store.
-    if (!xh) return;
-    const bool tailb = g1 < a.total && (g1 % a.tps) != 0;
-    if (!tailb && !mid) return;
-    __threadfence();                                 // the records before the arrivals
-    int second = 0;
-    if (lane == 0) {
-      if (mid && (atomicAdd(a.xc + blockIdx.x, 1) & 1)) second |= 1;
-      if (tailb && (atomicAdd(a.xc + blockIdx.x + 1, 1) & 1)) second |= 2;
-    }
-    second = __builtin_amdgcn_readfirstlane(second);
-    for (int h = 0; h < 2; ++h) {
-      if (!(second & (1 << h))) continue;
-      const int64_t r = (int64_t)blockIdx.x + h;
-      const int64_t rg = r * a.total / gridDim.x;      // wave r's first tile
-      const int rs = (int)(rg / a.tps);
-      const int64_t B = (int64_t)TO * (rg - (int64_t)rs * a.tps);
-      const int64_t jlo = (B + DA - 1) / DA, jhi = min<int64_t>(jlo + XJ, (M + DA - 1) / DA);
-      const float* rec = a.xw + r * SDR_XWAVE_REC;     // rec[x - (B - 150)] = demod x
-      __threadfence();                               // the other side's record after its arrival
-      for (int64_t qq = jlo / BO; qq * BO < jhi; ++qq) {
-        asm volatile("" ::: "memory");
-        const int64_t x0 = (int64_t)BD * qq - HA;      // dh[e] = demod x0 + e
-        for (int e = lane; e < HA + BD + 4; e += 64) {
-          const int64_t x = x0 + e;
-          dh[e] = (x >= B - XH && x < B + XT) ? rec[x - (B - XH)] : 0.f;
-        }
-        float o0, o1, o2;
-        audio_block3(aw_lane, ptab, o0, o1, o2);
-        const int64_t jb = (int64_t)BO * qq + RA * lane;
-        float* ao = a.audio + (int64_t)rs * a.audio_stride + jb;
-        if (jb >= jlo && jb < jhi) ao[0] = o0;
-        if (jb + 1 >= jlo && jb + 1 < jhi) ao[1] = o1;
-        if (jb + 2 >= jlo && jb + 2 < jhi) ao[2] = o2;
-        asm volatile("" ::: "memory");
-      }
-    }
-  }
 }
 
 // lfilter final state zf for the I and Q channels of an interleaved IQ block
@@ -1298,7 +1226,6 @@ static hipError_t launch_ring_t(FeParams p, const TapsF32& taps, RingArgs ra, hi
   const int wpc = per_device(wpc_cache, [] { return resident_per_cu(fe_ring_kernel<T, FUSED>, 64); });
   const int64_t slots = (int64_t)cu_count() * std::max(1, std::min(wpc, 4));
   const int64_t grid = std::min<int64_t>(slots, ra.total);
-  if (grid > SDR_XWAVE_MAX) { ra.xw = nullptr; ra.xc = nullptr; }   // (warm-up tiles instead)
   p.tiles_per_stream = ra.tps;
   hipLaunchKernelGGL((fe_ring_kernel<T, FUSED>), dim3((unsigned)grid), dim3(64), 0, st, p, taps, ra);
   return hipGetLastError();
@@ -1392,10 +1319,6 @@ hipError_t sdr_launch_fe_mono(const FeLaunch& a, const float* ataps, const float
   RingArgs ra{};
   ra.tps = tps; ra.total = total;
   ra.audio = audio; ra.audio_stride = audio_stride; ra.ataps = ataps;
-  if (a.xwave != nullptr) {                        // run-boundary hand-off (launch_ring_t checks the grid)
-    ra.xw = static_cast<float*>(a.xwave);
-    ra.xc = reinterpret_cast<int*>(static_cast<char*>(a.xwave) + (size_t)SDR_XWAVE_MAX * SDR_XWAVE_REC * 4);
-  }
   return launch_ring_t<101, true>(p, *a.taps, ra, st);
 }
 

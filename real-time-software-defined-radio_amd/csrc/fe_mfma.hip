@@ -65,8 +65,6 @@ struct MfmaFe {
   const i4v* afr;           // nullable: the A fragments built on the host (TapSet::dev_afr)
   float* audio;
   int64_t audio_stride;
-  float* xw;                // nullable: hand-off records (SDR_XWAVE_REC floats per run boundary)
-  int* xc;                  // ... and their arrival counters (zeroed once, +2 per boundary per launch)
 };
 
 constexpr int D = 10, T = 101, TO = 256, OFF = 104;
@@ -160,44 +158,11 @@ typedef float f2a4 __attribute__((ext_vector_type(2), aligned(4)));
 typedef const __attribute__((address_space(4))) float* cfp4;   // uniform, read-only: scalar loads
 typedef const __attribute__((address_space(4))) f2a4* cfp2;
 
-// The phase of ONE decimated output m (10 m >= T - 1: no lfilter zi) of stream s, exactly as
-// a tile computes it: each tap digit's sum over the T samples in int32 (the matrix cores' sums
-// are exact, so the order does not matter), combined and taken through the same atan2.  A run
-// of tiles starting mid-stream needs the phase of the output before it (the demod's
-// predecessor); this replaces a whole warm-up tile (2 560 samples read and 24 MFMAs) with T
-// taps per channel over one wave.
-template <int T>
-__device__ __forceinline__ float output_phase(const unsigned char* iq_s, int64_t m, const float* taps, float qscale) {
-  const int lane = threadIdx.x;
-  int acc[2][3] = {};
-  for (int k = lane; k < T; k += 64) {
-    const int q = (int)rintf(taps[k] * qscale);
-    const unsigned short v = *reinterpret_cast<const unsigned short*>(iq_s + 2 * (D * m - k));
-    const int xi = (int)(signed char)((v & 0xff) ^ 0x80), xq = (int)(signed char)(((v >> 8) & 0xff) ^ 0x80);
-#pragma unroll
-    for (int dg = 0; dg < 3; ++dg) {
-      const int d = digit(q, dg);
-      acc[0][dg] += d * xi;
-      acc[1][dg] += d * xq;
-    }
-  }
-#pragma unroll
-  for (int ch = 0; ch < 2; ++ch)
-#pragma unroll
-    for (int dg = 0; dg < 3; ++dg) acc[ch][dg] = wave_sum_i(acc[ch][dg]);
-  const float yi = fmaf((float)acc[0][2], 65536.f, (float)(acc[0][1] * 256 + acc[0][0]));   // combine_digits
-  const float yq = fmaf((float)acc[1][2], 65536.f, (float)(acc[1][1] * 256 + acc[1][0]));
-  return fast_atan2f_x2(f2v{yq, yq}, f2v{yi, yi}).x;
-}
-
 // The next tile's image loads are issued at the top of a tile and waited for at its end (r03
 // measured a two-tile-deep variant with alternating staging sets: no faster, 26 more VGPRs).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe_mfma_mono_kernel(MfmaFe p) {
   __shared__ __attribute__((aligned(16))) signed char img[2][IMG + 16];   // I, Q planes
   __shared__ __attribute__((aligned(16))) float dh[HA + AB + 8];
-  // the run's first block's head (hand-off, below), kept until the run ends: LDS per wave 11.1 ->
-  // 11.7 KB, within the 13.3 KB that 12 waves per CU (the VGPR bound) leave
-  __shared__ __attribute__((aligned(16))) float hd[SDR_XWAVE_REC - HA];
 
   const int lane = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * p.total / gridDim.x;
@@ -306,23 +271,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
     }
   };
 
-  // ---- run: audio blocks [b0, b1) ----
-  // A run starting mid-stream needs the 150 demod samples before its first block (the audio
-  // FIR's history) and the phase of the output before its first tile.  r04b, with hand-off
-  // records (p.xw): the phase is that ONE output computed exactly (output_phase), and the first
-  // block's outputs that reach into the history (j < 30) are left to the run boundary's
-  // hand-off (below); without them, the previous block's last tile runs first as a warm-up.
+  // ---- run: audio blocks [b0, b1), warm-up tile first when starting mid-stream ----
   int s = (int)(b0 / p.bps);
   int64_t t = (b0 - (int64_t)s * p.bps) * DA;
   const int64_t tps = (int64_t)p.bps * DA;
-  const bool xh = p.xw != nullptr;
-  const bool mid = t > 0;                                    // the run starts mid-stream
-  const bool warm = mid && !xh;
+  const bool warm = t > 0;
   if (warm) --t;
   const int64_t U = (b1 - b0) * DA + (warm ? 1 : 0);
-  constexpr int XJ = (TA - 1) / DA;                          // 30 outputs of a block reach into its history
-  constexpr int HH = SDR_XWAVE_REC - HA;                     // 160 head samples: lanes 0..7's windows
-  static_assert(HH >= DA * 4 * ((XJ + 3) / 4 - 1) + NW - (TA - 1) && HH % 4 == 0, "head record covers the windows");
   for (int e = lane; e < HA; e += 64) dh[e] = 0.f;          // zero history at a stream start
   if (interior(t)) {
     load_image(s, t, false);
@@ -334,7 +289,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
   auto next_t = [&](int64_t t_) { return t_ + 1 == tps ? (int64_t)0 : t_ + 1; };
   int s1 = next_s(s, t);
   int64_t t1 = next_t(t);
-  float carry = (mid && xh) ? output_phase<T>(p.iq + 2 * (int64_t)s * p.stride, TO * t - 1, p.taps, p.qscale) : 0.f;
+  float carry = 0.f;
   float d4[4] = {0.f, 0.f, 0.f, 0.f};
 
   // deferred audio outputs: AQ blocks of 4 outputs per lane, stored when the queue is full and
@@ -344,55 +299,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
   int nq = 0;
   int qs = (int)(b0 / p.bps);                                // entry 0: stream qs, block qj
   int qj = (int)(b0 - (int64_t)qs * p.bps);
-  int qskip = (mid && xh) ? XJ : 0;                          // the first block's outputs [0, XJ): the hand-off's
   auto queue_flush = [&]() __attribute__((always_inline)) {
     static_for<0, AQ>([&](auto K) {
       constexpr int k = K;
       if (k < nq) {
-        const int sk = k == 0 ? qskip : 0;
         const int64_t j = (int64_t)TO * qj + 4 * lane;
         float* ao = p.audio + (int64_t)qs * p.audio_stride + j;
-        if (j + 4 <= p.A && ((uintptr_t)ao & 15) == 0 && 4 * lane >= sk) {
+        if (j + 4 <= p.A && ((uintptr_t)ao & 15) == 0) {
           *reinterpret_cast<f4v*>(ao) = aq[k];
         } else {
           const float rv[4] = {aq[k].x, aq[k].y, aq[k].z, aq[k].w};
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (j + r < p.A && 4 * lane + r >= sk) ao[r] = rv[r];
+            if (j + r < p.A) ao[r] = rv[r];
         }
         if (++qj == p.bps) { qj = 0; ++qs; }
       }
     });
     nq = 0;
-    qskip = 0;
   };
   auto queue_put = [&](const f4v& v) __attribute__((always_inline)) {
     static_for<0, AQ>([&](auto K) {                          // compile-time slots (no scratch)
       if ((int)K == nq) aq[K] = v;
     });
     if (++nq == AQ) queue_flush();
-  };
-
-  // audio block from the LDS window (history + block): a[j] = sum_k g[k] d[5j - k]; lane l ->
-  // outputs 4 l .. 4 l + 3.  Window sample w, output r: tap h[150 + 5 r - w] = g[w - 5 r]; each
-  // output keeps its even- and odd-sample partial sums in one packed register:
-  //   acc_r.xy += (g[j], g[j+1]) * (x_w, x_{w+1}),  j = w - 5 r  (g[-1] = g[151] = 0)
-  auto audio_fir = [&]() __attribute__((always_inline)) {
-    lds_order();
-    const float* aw = dh + (HA - (TA - 1)) + DA * 4 * lane;
-    f2v acc[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
-    static_for<0, NW / 2>([&](auto W2) {
-      constexpr int w = 2 * W2;
-      const f2v x2 = *reinterpret_cast<const f2v*>(aw + w);
-      static_for<0, 4>([&](auto RR) {
-        constexpr int j = w - DA * (int)RR;
-        if constexpr (j >= -1 && j <= TA - 1) {
-          const f2a4 hp = *(cfp2)(gr + j);           // (g[j], g[j+1]): float-indexed pair
-          pk_fma_s(acc[RR], f2v{hp.x, hp.y}, x2);
-        }
-      });
-    });
-    return f4v{acc[0].x + acc[0].y, acc[1].x + acc[1].y, acc[2].x + acc[2].y, acc[3].x + acc[3].y};
   };
 
   // the MFMAs of the tile whose image is in LDS: B fragments of both channels, one K-step at a
@@ -451,14 +381,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
       for (int i = 0; i < 4; ++i) d4[i] = d[i];
     }
     if (!(kAbl & 1) && !(warm && u == 0) && tb == DA - 1) {
-      // the run's first block (mid-stream, hand-off): its head, for the boundary's record
-      if (xh && mid && u == DA - 1) {
-        lds_order();
-        if (lane < HH / 4) *reinterpret_cast<f4v*>(&hd[4 * lane]) = *reinterpret_cast<const f4v*>(&dh[HA + 4 * lane]);
-      }
+      // audio block jb: a[j] = sum_k g[k] d[5j - k]
+      lds_order();
+      // window sample w, output r: tap h[150 + 5 r - w] = g[w - 5 r]; each output keeps its
+      // even- and odd-sample partial sums in one packed register:
+      //   acc_r.xy += (g[j], g[j+1]) * (x_w, x_{w+1}),  j = w - 5 r  (g[-1] = g[151] = 0)
+      const float* aw = dh + (HA - (TA - 1)) + DA * 4 * lane;
+      f2v acc[4] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+      static_for<0, NW / 2>([&](auto W2) {
+        constexpr int w = 2 * W2;
+        const f2v x2 = *reinterpret_cast<const f2v*>(aw + w);
+        static_for<0, 4>([&](auto RR) {
+          constexpr int j = w - DA * (int)RR;
+          if constexpr (j >= -1 && j <= TA - 1) {
+            const f2a4 hp = *(cfp2)(gr + j);         // (g[j], g[j+1]): float-indexed pair
+            pk_fma_s(acc[RR], f2v{hp.x, hp.y}, x2);
+          }
+        });
+      });
       // the outputs wait in registers: stores interleaved with the read stream cost far more
       // than their bytes (OutQ3); blocks leave in order, b0 + entry
-      queue_put(audio_fir());
+      queue_put(f4v{acc[0].x + acc[0].y, acc[1].x + acc[1].y, acc[2].x + acc[2].y, acc[3].x + acc[3].y});
       lds_order();
       // this block's last 150 demod samples become the next block's history
       if (o >= TO - HA) *reinterpret_cast<f4v*>(&dh[HA - TO + o]) = f4v{d4[0], d4[1], d4[2], d4[3]};
@@ -503,48 +446,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void fe
     if (more) advance();
   }
   queue_flush();
-  if (!xh) return;
-
-  // ---- run-boundary hand-off (r04b) ----
-  // Boundary r (between wave r-1's last block and wave r's first, mid-stream) has one record:
-  // the history wave r-1 leaves in dh (its last block's last 152 demod samples) and the head
-  // of wave r's first block.  Each side writes its half, then counts its arrival; the second
-  // to arrive -- nobody waits -- loads the record into its window and computes the block's
-  // outputs [0, 30), the FIR of the same samples in the same order as a run holding both
-  // blocks would: the same bits.  The counter is +2 per boundary per launch, so its parity
-  // says which arrival this is without a reset.
-  const bool tail = b1 < p.total && (b1 % p.bps) != 0;       // boundary blockIdx + 1 is mid-stream
-  lds_order();
-  if (tail && lane < HA / 4)
-    *reinterpret_cast<f4v*>(p.xw + ((int64_t)blockIdx.x + 1) * SDR_XWAVE_REC + 4 * lane) = *reinterpret_cast<const f4v*>(&dh[4 * lane]);
-  if (mid && lane < HH / 4)
-    *reinterpret_cast<f4v*>(p.xw + (int64_t)blockIdx.x * SDR_XWAVE_REC + HA + 4 * lane) = *reinterpret_cast<const f4v*>(&hd[4 * lane]);
-  if (!tail && !mid) return;
-  __threadfence();                                           // the records before the arrivals
-  int second = 0;                                            // bit 0: head boundary, bit 1: tail boundary
-  if (lane == 0) {
-    if (mid && (atomicAdd(p.xc + blockIdx.x, 1) & 1)) second |= 1;
-    if (tail && (atomicAdd(p.xc + blockIdx.x + 1, 1) & 1)) second |= 2;
-  }
-  second = __builtin_amdgcn_readfirstlane(second);
-  for (int h = 0; h < 2; ++h) {
-    if (!(second & (1 << h))) continue;
-    const int64_t r = (int64_t)blockIdx.x + h;                 // the boundary's (later) wave
-    __threadfence();                                         // the other side's record after its arrival
-    lds_order();
-    for (int e = 4 * lane; e < SDR_XWAVE_REC; e += 256)
-      *reinterpret_cast<f4v*>(&dh[e]) = *reinterpret_cast<const f4v*>(p.xw + r * SDR_XWAVE_REC + e);
-    const f4v o = audio_fir();
-    const int64_t rb = r * p.total / gridDim.x;               // that wave's first block
-    const int rs = (int)(rb / p.bps);
-    const int64_t j = (int64_t)TO * (rb - (int64_t)rs * p.bps) + 4 * lane;
-    float* ao = p.audio + (int64_t)rs * p.audio_stride + j;
-    const float ov[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (4 * lane + i < XJ && j + i < p.A) ao[i] = ov[i];
-    lds_order();
-  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -588,6 +489,36 @@ __device__ inline double unwrap_step_f64_m(double dd, int* w) {   // fe.hip unwr
   if (ddmod == -kPi && dd > 0) ddmod = kPi;
   *w = (int)llrint((ddmod - dd) / k2Pi);
   return ddmod;
+}
+
+// The phase of ONE decimated output m (10 m >= T - 1: no lfilter zi) of stream s, exactly as
+// a tile computes it: each tap digit's sum over the T samples in int32 (the matrix cores' sums
+// are exact, so the order does not matter), combined and taken through the same atan2.  A run
+// of tiles starting mid-stream needs the phase of the output before it (the demod's
+// predecessor); this replaces a whole warm-up tile (2 560 samples read and 24 MFMAs) with T
+// taps per channel over one wave.
+template <int T>
+__device__ __forceinline__ float output_phase(const unsigned char* iq_s, int64_t m, const float* taps, float qscale) {
+  const int lane = threadIdx.x;
+  int acc[2][3] = {};
+  for (int k = lane; k < T; k += 64) {
+    const int q = (int)rintf(taps[k] * qscale);
+    const unsigned short v = *reinterpret_cast<const unsigned short*>(iq_s + 2 * (D * m - k));
+    const int xi = (int)(signed char)((v & 0xff) ^ 0x80), xq = (int)(signed char)(((v >> 8) & 0xff) ^ 0x80);
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg) {
+      const int d = digit(q, dg);
+      acc[0][dg] += d * xi;
+      acc[1][dg] += d * xq;
+    }
+  }
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg) acc[ch][dg] = wave_sum_i(acc[ch][dg]);
+  const float yi = fmaf((float)acc[0][2], 65536.f, (float)(acc[0][1] * 256 + acc[0][0]));   // combine_digits
+  const float yq = fmaf((float)acc[1][2], 65536.f, (float)(acc[1][1] * 256 + acc[1][0]));
+  return fast_atan2f_x2(f2v{yq, yq}, f2v{yi, yi}).x;
 }
 
 template <int T>
@@ -925,10 +856,6 @@ hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps_rev, in
   });
 
   const int64_t grid = std::min<int64_t>(slots, p.total);
-  if (a.xwave != nullptr && grid <= SDR_XWAVE_MAX) {          // run-boundary hand-off instead of warm-up tiles
-    p.xw = static_cast<float*>(a.xwave);
-    p.xc = reinterpret_cast<int*>(static_cast<char*>(a.xwave) + (size_t)SDR_XWAVE_MAX * SDR_XWAVE_REC * 4);
-  }
   hipLaunchKernelGGL(fe_mfma_mono_kernel, dim3((unsigned)grid), dim3(64), 0, st, p);
   return hipGetLastError();
 }

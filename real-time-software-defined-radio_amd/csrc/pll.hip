@@ -771,8 +771,12 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // chunk" predicate (its selects and compares were a fifth of the check loop's VALU); the wave
   // holding the last, partial chunk (and the unused ones) keeps them.  wfast: also every chunk
   // after a long call's pre-roll, so every step's wrap margin counts and every phase is stored.
+#ifdef SDR_PLL_NOFAST     // A/B builds only: every wave on the general step loops
+  const bool wfull = false, wfast = false;
+#else
   const bool wfull = __all(len == L);
   const bool wfast = wfull && __all(k0 >= pre);
+#endif
   // 0. where the locked phase estimate goes within the block, measured from the input: a
   // locked loop keeps its angle th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's
   // phase, so z_j = sum over chunk j of x_k exp(-i w (off + k)) ~ (A/2) exp(i phaseEst) (+ an
@@ -810,10 +814,19 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
           for (int u = 0; u < SB; ++u) {
             // x > 0: +exp(-i a); x < 0: -exp(-i a) (the pi of sel); 0 / NaN / past the chunk: 0
             const float sg = (F || i0 + u < len) ? (float)cd[u] : 0.f;
+#ifdef SDR_PLL_OLDCORR    // A/B builds only: the scalar rotation of round 4
+            z.x = fmaf(sg, c.x, z.x);
+            z.y = fmaf(sg, c.y, z.y);
+            const float nr = c.x * dc - c.y * ds;
+            c.y = fmaf(c.x, ds, c.y * dc);
+            c.x = nr;
+            (void)rs;
+#else
             const f2v sgv = f2v{sg, sg};
             asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(z) : "v"(sgv), "v"(c));
             const f2v t = c * dcv;
             asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1]" : "=v"(c) : "v"(c), "v"(rs), "v"(t));
+#endif
           }
         }
       };

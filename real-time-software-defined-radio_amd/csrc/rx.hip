@@ -1135,6 +1135,9 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
                              sizeof(float) * (size_t)r->out_stride[o], sizeof(float) * (size_t)n, (size_t)r->S,
                              hipMemcpyDeviceToHost, st));
   }
+  // the row set is free for block k+nq once these copies have read it too (the event the
+  // front half of block k+nq waits for is recorded again, after them)
+  if (r->pipe) HIP_TRY(hipEventRecord(r->ev_back[(r->blocks - 1) % r->nq], st));
   HIP_TRY(hipEventRecord(r->ev_done[slot], st));
   ++r->subs;
   P.slot = slot;

@@ -46,8 +46,6 @@ struct sdr_ctx {
   // PLL solve counters (SDR_PLL_NSTATS, device; sdr_pll_stats): every PLL launch of the
   // context and of its receivers adds to them
   unsigned long long* pll_stats = nullptr;
-  // u8 FE + mono hand-off records (SDR_XWAVE_BYTES, zeroed once: the arrival counters count on)
-  void* xwave = nullptr;
 };
 
 namespace sdrint {

@@ -43,13 +43,7 @@ struct FeLaunch {
   const double* zi_i; const double* zi_q; int64_t zi_stride; const double* prev_phase;
   float* demod; int64_t out_stride; float* i_ds; float* q_ds; float* last_phi; int* wraps;
   const int* afr;   // nullable: the taps' MFMA A fragments (TapSet::dev_afr; else built in-kernel)
-  void* xwave;      // nullable: SDR_XWAVE_BYTES of the context's zeroed hand-off records (fe_mfma.hip)
 };
-// fe_mfma_mono_kernel's cross-wave hand-off: per run boundary one record of 312 floats (the
-// history one wave leaves, the block head the next one starts with) and one arrival counter
-constexpr int SDR_XWAVE_MAX = 8192;
-constexpr int SDR_XWAVE_REC = 312;
-constexpr size_t SDR_XWAVE_BYTES = (size_t)SDR_XWAVE_MAX * (SDR_XWAVE_REC * 4 + 4);
 
 // Real-channel FIR with decimation (fir.hip); `pre` selects a fused pre-op on the input
 // (0 none, 1 x^2, 2 x*c*gain mixer).

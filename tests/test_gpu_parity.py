@@ -410,32 +410,6 @@ def test_fm_mono_streams_u8_mfma_tap_scale(sdr, gpu_ctx, oracle, gain):
         assert rms(got[s], ref) < AUDIO_RMS and maxabs(got[s], ref) < AUDIO_MAX, (s, rms(got[s], ref))
 
 
-@pytest.mark.parametrize("iq_dtype,S,n", [("f32", 3, 1_024_000 + 640), ("u8", 4, 1_024_000 + 16),
-                                           ("u8", 48, 64_000 * 3 + 16)])
-def test_fused_run_boundary_handoff_bit_identical(sdr, gpu_ctx, oracle, monkeypatch, iq_dtype, S, n):
-    """r04b: a fused kernel's run that starts mid-stream takes the 30 audio outputs whose windows
-    cross the run boundary from the boundary's hand-off (the second of the two waves to arrive
-    computes them from the record both wrote) instead of running a warm-up tile.  The same
-    samples in the same order: bit-identical to the warm-up path (SDR_XWAVE=0), over repeated
-    launches (the arrival counters carry their parity), with runs of 1-2 tiles (f32: 1 605
-    tiles on 1 024 waves) and of one audio block (u8, 48 streams: every run boundary but the
-    stream starts is a hand-off); and == the f64 oracle."""
-    rf_b, au_b = sdr.design.mono_coeffs(101, 151)
-    dt = np.uint8 if iq_dtype == "u8" else np.float32
-    iq = np.stack([sdr.synth.fm_iq(n, seed=300 + s, dtype=dt) for s in range(S)])
-    monkeypatch.setenv("SDR_XWAVE", "0")
-    warm = sdr.fm_mono_streams(iq, rf_b, au_b)
-    monkeypatch.delenv("SDR_XWAVE")
-    for _ in range(3):
-        got = sdr.fm_mono_streams(iq, rf_b, au_b)
-        bad = np.argwhere(got != warm)
-        assert bad.size == 0, (len(bad), bad[:5])
-    s = S // 2
-    x = iq[s].astype(np.float64)
-    ref, _ = oracle.mono_basic_coeffs((x - 128.0) / 128.0 if iq_dtype == "u8" else x, rf_b, au_b)
-    assert rms(got[s], ref) < AUDIO_RMS and maxabs(got[s], ref) < AUDIO_MAX
-
-
 # ---------------------------------------------------------------------------- split stream
 @pytest.mark.parametrize("taps", [101, 151])
 def test_split_stream_ranges_equal_single_pass(sdr, gpu_ctx, taps):
