@@ -738,10 +738,12 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // out SG at a time before the first is used.  (Slots of steps past N hold whatever was
   // there: only discarded steps read them, and every slot is in the array.)
   {
-    // r04b: no per-element guard (its branches were ~13 SALU a step): every thread loads and
-    // writes all SG of its elements, a load past N clamped into the array and its code written
-    // to the unused slot of step kk (i = kk mod L, j = kk / L is one-to-one and stays inside
-    // code[] for every L the launchers produce: (L-1) CSTR + (SG SPEC_T - 1) / L < SPEC_LDS)
+    // r04b: no per-element branch (the guards' branches were ~13 SALU a step): every thread
+    // loads and writes all SG of its elements, a load past N clamped into the array.  Such an
+    // element's slot (kk mod L, kk / L) is a step past its chunk's end or of an unused chunk
+    // (only discarded steps read them) -- or, when kk / L passes the row's end (L = 24: up to
+    // 682 > CSTR), the next row's real slot: its column is clamped to the padding column
+    // (chunk SPEC_T, never in use)
     constexpr int SG = SPEC_T == 512 ? 32 : 40;
     static_assert(SG * SPEC_T >= (SPEC_T == 512 ? SPEC_NMAX : SPEC_N256) - 1, "one pass of SG loads covers a call");
     float xv[SG];
@@ -750,10 +752,12 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     auto cod = [](float x) { return (int8_t)(x > 0.f ? 1 : (x < 0.f ? -1 : 0)); };
     if (SPEC_T % L == 0) {
       // element kk = tid + u SPEC_T: i = tid mod L for every u, j = tid / L + u SPEC_T / L
-      int8_t* cb = code + (tid % L) * CSTR + tid / L;
-      const int js = SPEC_T / L;
+      const int i = tid % L, j0 = tid / L, js = SPEC_T / L;
 #pragma unroll
-      for (int u = 0; u < SG; ++u) cb[u * js] = cod(xv[u]);
+      for (int u = 0; u < SG; ++u) {
+        const int j = j0 + u * js;
+        code[i * CSTR + min(j, SPEC_T)] = cod(xv[u]);
+      }
     } else {
       // kk / L by a multiply-high (L <= 64, kk < 2^16: exact with m = floor(2^32 / L) + 1)
       const unsigned mL = 0xffffffffu / (unsigned)L + 1u;
@@ -761,7 +765,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       for (int u = 0; u < SG; ++u) {
         const int kk = tid + u * SPEC_T;
         const int j = (int)__umulhi((unsigned)kk, mL), i = kk - j * L;
-        code[i * CSTR + j] = cod(xv[u]);
+        code[i * CSTR + min(j, SPEC_T)] = cod(xv[u]);
       }
     }
   }

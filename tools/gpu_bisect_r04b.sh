@@ -8,7 +8,7 @@ O=$R/gpurun_out/r04b_bis
 mkdir -p "$O"
 cd "$R"
 export TMPDIR=/tmp
-for v in prod nofast oldcorr both; do
+for v in prod nofast oldcorr; do
   lib=$R/real-time-software-defined-radio_amd/libsdr.so
   [ "$v" = prod ] || lib=$R/real-time-software-defined-radio_amd/libsdr_$v.so
   SDR_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_span.py tests/test_pll_spec.py -m gpu -v -s \
