@@ -14,7 +14,7 @@ rc=$?
 tail -3 "$O/pytest_gpu.txt"
 [ $rc -le 1 ] || { echo "pytest rc $rc: stopping"; exit $rc; }
 set -e
-bash tools/ab_bench.sh gpurun_out/r04b/ab_ring 3 "--no-extras,--no-cpu" base prod
+bash tools/ab_bench.sh gpurun_out/r04b/ab_ring 3 "--no-extras,--no-cpu" base prod q16
 bash tools/ab_bench.sh gpurun_out/r04b/ab_c5 2 "--workload,c5,--steps,5,--no-cpu" base prod nofast oldcorr
 bash tools/ab_bench.sh gpurun_out/r04b/ab_c4 2 "--workload,c4,--no-cpu" base prod
 bash tools/ab_bench.sh gpurun_out/r04b/ab_c4d1 2 "--workload,c4,--no-cpu,--depth,1" base prod
