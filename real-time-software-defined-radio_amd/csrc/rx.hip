@@ -583,7 +583,7 @@ struct sdr_rx {
     float* out[SDR_RX_MAXOUT] = {};
     int64_t os[SDR_RX_MAXOUT] = {};
     size_t region[SDR_RX_NOUTPUTS] = {};
-  } pq[3];
+  } pq[4];                             // depth + 1 at most (the new block before k-depth leaves)
   int pq_head = 0, pq_n = 0;
   bool timing = false;                 // events between the stages of each block
   hipEvent_t ev[SDR_RX_NSTAGES + 1] = {};
@@ -1047,7 +1047,7 @@ bool stage_output(int o) {
 int deliver(sdr_rx* r) {
   if (r->pq_n == 0) return SDR_OK;
   const sdr_rx::Pending& P = r->pq[r->pq_head];
-  r->pq_head = (r->pq_head + 1) % 3;
+  r->pq_head = (r->pq_head + 1) % 4;
   --r->pq_n;
   HIP_TRY(hipEventSynchronize(r->ev_done[P.slot]));
   const float* base = r->pin_out + (size_t)P.slot * r->out_slot / sizeof(float);
@@ -1142,7 +1142,7 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
   ++r->subs;
   P.slot = slot;
   P.nout = nout;
-  r->pq[(r->pq_head + r->pq_n) % 3] = P;
+  r->pq[(r->pq_head + r->pq_n) % 4] = P;
   ++r->pq_n;
   while (r->pq_n > r->depth) TRY(deliver(r));            // block k-depth
   return SDR_OK;
