@@ -550,8 +550,11 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
   int wacc = 0;                                    // per-lane 2*pi correction count
 
   // ---- deferred outputs (OutQ3): FE demod tiles / FUSED audio blocks ----
+  // FUSED, r04b: 16 audio blocks (48 VGPRs of queue, 20 of them AGPRs) hold a whole run of the
+  // 128-block step (13.4 blocks per wave), so no flush goes out mid-run beside the read stream
+  // (12: one at block 12 of every wave at once); A/B 0.738 -> 0.747 of HBM on one box
 #ifndef SDR_RING_QN
-#define SDR_RING_QN 12
+#define SDR_RING_QN 16
 #endif
   constexpr int QN = FUSED ? SDR_RING_QN : 36;
   OutQ3<QN> oq;
