@@ -529,7 +529,10 @@ constexpr int SPEC_W_LONG = SDR_SPEC_W_LONG;
 constexpr int SPEC_IT = 3;           // solve / check rounds before the sequential kernel takes over
 constexpr int SPEC_NMAX = SDR_PLL_BLOCK_MAX; // samples per call (the sign codes of steps 1.. in LDS: 16 KiB)
 static_assert(SPEC_NMAX == 16384 + 1, "LDS sizing");
-constexpr int SPEC_N256 = 10240;             // longest call the 256-thread solve takes (512 above)
+#ifndef SDR_SPEC_N256
+#define SDR_SPEC_N256 10240
+#endif
+constexpr int SPEC_N256 = SDR_SPEC_N256;     // longest call the 256-thread solve takes (512 above; A/B builds: -DSDR_SPEC_N256=)
 constexpr int SPEC_LDS = 32 * 513;           // padded transposed bytes: 512 chunks of <= 32 steps (or 256 of <= 40)
 constexpr int SB = 8;                        // steps per batch of LDS reads in the step loops
 
