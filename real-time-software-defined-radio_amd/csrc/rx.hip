@@ -568,6 +568,7 @@ struct sdr_rx {
   // sdr_rx_set_pipeline: block k's front half (FE, stage A) runs on `front` while block
   // k-1's back half (B, PLLs, C, D, E) runs on the context stream; row set k % nq
   int pipe = 0;
+  hipStream_t last_fs = nullptr;        // the stream block k-1's front half ran on
   int nq = 2;                           // row sets when pipelined (3 with sdr_rx_set_depth >= 2)
   hipStream_t front = nullptr;          // FE, stages A and B
   hipStream_t mid = nullptr;            // the PLLs (prep, lanes, NCO)
@@ -806,6 +807,7 @@ int sdr_rx_reset(sdr_rx* r) {
   HIP_TRY(hipStreamSynchronize(st));
   r->parity = 0;
   r->blocks = 0;
+  r->last_fs = nullptr;
   std::memcpy(r->out, r->outs[0], sizeof r->out);
   return SDR_OK;
 }
@@ -851,7 +853,9 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
                     ((uintptr_t)iq % (r->u8 ? 4 : 16)) == 0;
   hipStream_t fs = (r->pipe && fast) ? r->front : st;
   if (r->pipe) {
-    if (r->blocks >= 1) HIP_TRY(hipStreamWaitEvent(fs, r->ev_front[(q + r->nq - 1) % r->nq], 0));   // states of block k-1
+    // states of block k-1 (r04b: not when its front half ran on this same stream, in order)
+    if (r->blocks >= 1 && r->last_fs != fs) HIP_TRY(hipStreamWaitEvent(fs, r->ev_front[(q + r->nq - 1) % r->nq], 0));
+    r->last_fs = fs;
     if (r->blocks >= r->nq) HIP_TRY(hipStreamWaitEvent(fs, r->ev_back[q], 0));    // set q read by k-nq
   }
   auto mark = [&](int k, hipStream_t s) { return r->timing ? hipEventRecord(r->ev[k], s) : hipSuccess; };
@@ -1128,8 +1132,10 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
   const int rc = sdr_rx_process_dev(r, pin, xs);
   for (float*& m : r->mirror) m = nullptr;
   TRY(rc);
+  bool copied = false;
   for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) {
     if (!want[o] || stage_output(o)) continue;
+    copied = true;
     const int64_t n = r->out_n[o];
     HIP_TRY(hipMemcpy2DAsync(pout + P.region[o], sizeof(float) * (size_t)n, r->out[o],
                              sizeof(float) * (size_t)r->out_stride[o], sizeof(float) * (size_t)n, (size_t)r->S,
@@ -1137,7 +1143,7 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
   }
   // the row set is free for block k+nq once these copies have read it too (the event the
   // front half of block k+nq waits for is recorded again, after them)
-  if (r->pipe) HIP_TRY(hipEventRecord(r->ev_back[(r->blocks - 1) % r->nq], st));
+  if (r->pipe && copied) HIP_TRY(hipEventRecord(r->ev_back[(r->blocks - 1) % r->nq], st));
   HIP_TRY(hipEventRecord(r->ev_done[slot], st));
   ++r->subs;
   P.slot = slot;
