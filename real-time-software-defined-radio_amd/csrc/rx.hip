@@ -580,6 +580,7 @@ struct sdr_rx {
   int64_t subs = 0;
   struct Pending {
     int slot = 0, nout = 0;
+    hipEvent_t ev = nullptr;           // the block's completion (ev_done[slot], or its row set's ev_back)
     int which[SDR_RX_MAXOUT] = {};
     float* out[SDR_RX_MAXOUT] = {};
     int64_t os[SDR_RX_MAXOUT] = {};
@@ -1053,7 +1054,7 @@ int deliver(sdr_rx* r) {
   const sdr_rx::Pending& P = r->pq[r->pq_head];
   r->pq_head = (r->pq_head + 1) % 4;
   --r->pq_n;
-  HIP_TRY(hipEventSynchronize(r->ev_done[P.slot]));
+  HIP_TRY(hipEventSynchronize(P.ev));
   const float* base = r->pin_out + (size_t)P.slot * r->out_slot / sizeof(float);
   for (int i = 0; i < P.nout; ++i) {
     const int64_t n = r->out_n[P.which[i]];
@@ -1141,10 +1142,19 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
                              sizeof(float) * (size_t)r->out_stride[o], sizeof(float) * (size_t)n, (size_t)r->S,
                              hipMemcpyDeviceToHost, st));
   }
-  // the row set is free for block k+nq once these copies have read it too (the event the
-  // front half of block k+nq waits for is recorded again, after them)
-  if (r->pipe && copied) HIP_TRY(hipEventRecord(r->ev_back[(r->blocks - 1) % r->nq], st));
-  HIP_TRY(hipEventRecord(r->ev_done[slot], st));
+  const int qb = (int)((r->blocks - 1) % r->nq);
+  if (r->pipe && !copied) {
+    // nothing after the back half: its row-set event marks the block's completion (one event
+    // call fewer per block; a later block of the same set re-recording it before this one is
+    // delivered -- depth 3 -- only makes the wait longer)
+    P.ev = r->ev_back[qb];
+  } else {
+    // the row set is free for block k+nq once these copies have read it too (the event the
+    // front half of block k+nq waits for is recorded again, after them)
+    if (r->pipe) HIP_TRY(hipEventRecord(r->ev_back[qb], st));
+    HIP_TRY(hipEventRecord(r->ev_done[slot], st));
+    P.ev = r->ev_done[slot];
+  }
   ++r->subs;
   P.slot = slot;
   P.nout = nout;
