@@ -569,6 +569,7 @@ struct sdr_rx {
   // k-1's back half (B, PLLs, C, D, E) runs on the context stream; row set k % nq
   int pipe = 0;
   hipStream_t last_fs = nullptr;        // the stream block k-1's front half ran on
+  int64_t host_done = -1;               // the latest block the host has waited for (deliver)
   int nq = 2;                           // row sets when pipelined (3 with sdr_rx_set_depth >= 2)
   hipStream_t front = nullptr;          // FE, stages A and B
   hipStream_t mid = nullptr;            // the PLLs (prep, lanes, NCO)
@@ -581,6 +582,7 @@ struct sdr_rx {
   struct Pending {
     int slot = 0, nout = 0;
     hipEvent_t ev = nullptr;           // the block's completion (ev_done[slot], or its row set's ev_back)
+    int64_t blk = 0;                   // its index (sdr_rx::blocks numbering)
     int which[SDR_RX_MAXOUT] = {};
     float* out[SDR_RX_MAXOUT] = {};
     int64_t os[SDR_RX_MAXOUT] = {};
@@ -809,6 +811,7 @@ int sdr_rx_reset(sdr_rx* r) {
   r->parity = 0;
   r->blocks = 0;
   r->last_fs = nullptr;
+  r->host_done = -1;
   std::memcpy(r->out, r->outs[0], sizeof r->out);
   return SDR_OK;
 }
@@ -857,7 +860,8 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     // states of block k-1 (r04b: not when its front half ran on this same stream, in order)
     if (r->blocks >= 1 && r->last_fs != fs) HIP_TRY(hipStreamWaitEvent(fs, r->ev_front[(q + r->nq - 1) % r->nq], 0));
     r->last_fs = fs;
-    if (r->blocks >= r->nq) HIP_TRY(hipStreamWaitEvent(fs, r->ev_back[q], 0));    // set q read by k-nq
+    // set q read by k-nq (not when the host has already waited for that block: submissions)
+    if (r->blocks >= r->nq && r->blocks - r->nq > r->host_done) HIP_TRY(hipStreamWaitEvent(fs, r->ev_back[q], 0));
   }
   auto mark = [&](int k, hipStream_t s) { return r->timing ? hipEventRecord(r->ev[k], s) : hipSuccess; };
   HIP_TRY(mark(0, fs));
@@ -963,7 +967,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     HIP_TRY(hipEventRecord(r->ev_front[q], fs));
     if (plls && mid) {
       HIP_TRY(hipStreamWaitEvent(ps, r->ev_front[q], 0));
-      if (r->blocks >= r->nq) HIP_TRY(hipStreamWaitEvent(ps, r->ev_back[q], 0));
+      if (r->blocks >= r->nq && r->blocks - r->nq > r->host_done) HIP_TRY(hipStreamWaitEvent(ps, r->ev_back[q], 0));
     } else {
       HIP_TRY(hipStreamWaitEvent(st, r->ev_front[q], 0));
     }
@@ -1055,6 +1059,7 @@ int deliver(sdr_rx* r) {
   r->pq_head = (r->pq_head + 1) % 4;
   --r->pq_n;
   HIP_TRY(hipEventSynchronize(P.ev));
+  r->host_done = std::max(r->host_done, P.blk);
   const float* base = r->pin_out + (size_t)P.slot * r->out_slot / sizeof(float);
   for (int i = 0; i < P.nout; ++i) {
     const int64_t n = r->out_n[P.which[i]];
@@ -1158,6 +1163,7 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
   ++r->subs;
   P.slot = slot;
   P.nout = nout;
+  P.blk = r->blocks - 1;
   r->pq[(r->pq_head + r->pq_n) % 4] = P;
   ++r->pq_n;
   while (r->pq_n > r->depth) TRY(deliver(r));            // block k-depth
