@@ -29,6 +29,15 @@ from .dsp import _taps
 _PLL_INIT = (0.0, 0.0, 1.0, 0.0, 1.0, 0.0)       # model/fmMonoBlock.py:76, model/fmRDSblock.py:96
 
 
+def _addr(a):
+    """The data address of a C-contiguous array: a writable one through the buffer protocol
+    (~0.6 us), anything else through ndarray.ctypes (~1.5-2 us, a ctypes object per call).
+    At the reference's block sizes a block costs ~30-45 us, so per-call pointer lookups show."""
+    if a.flags.writeable and a.nbytes:
+        return ctypes.addressof(ctypes.c_char.from_buffer(a))
+    return a.ctypes.data
+
+
 class Receiver:
     """`nstreams` independent FM streams through the block receiver (sdr_rx).
 
@@ -105,15 +114,21 @@ class Receiver:
             raise ValueError(f"expected {self.S} x {2 * self.B} interleaved values, got {iq.shape}")
         key = tuple(fetch) if fetch is not None else None
         plan = self._plans.get(key)
-        if plan is None:                      # output names -> (which[], lengths), built once
+        if plan is None:                      # output names -> (which[], lengths, offsets), built once
             names = list(fetch) if fetch is not None else \
                 [n for n in ("audio", "left", "right", "rrc_i", "rrc_q") if n in self.outputs]
             which = (ctypes.c_int * len(names))(*[RX_OUTPUTS.index(n) for n in names])
-            plan = self._plans[key] = (names, which, [self._length(n) for n in names])
-        names, which, lengths = plan
-        outs = {n: np.empty((self.S, m), dtype=np.float32) for n, m in zip(names, lengths)}
-        ptrs = (ctypes.c_void_p * len(names))(*[outs[n].ctypes.data for n in names])
-        check(getattr(self.lib, fn)(self.handle, iq.ctypes.data, self.B, len(names), which, ptrs, None), fn)
+            lengths = [self._length(n) for n in names]
+            offs = [self.S * sum(lengths[:i]) for i in range(len(names))]
+            plan = self._plans[key] = (names, which, lengths, offs, self.S * sum(lengths),
+                                       ctypes.c_void_p * len(names))
+        names, which, lengths, offs, total, ptr_array = plan
+        # one allocation per call, the outputs (S, n) views of it
+        buf = np.empty(max(total, 1), dtype=np.float32)
+        base = _addr(buf)
+        ptrs = ptr_array(*[base + 4 * o for o in offs])
+        outs = {n: buf[o:o + self.S * m].reshape(self.S, m) for n, o, m in zip(names, offs, lengths)}
+        check(getattr(self.lib, fn)(self.handle, _addr(iq), self.B, len(names), which, ptrs, None), fn)
         return outs
 
     def process(self, iq, fetch=None):
