@@ -934,14 +934,13 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   // (which waited for its recurrence) is done.
   const bool plls = stx || rd;
   // The recurrences get a stream of their own (block k's beside block k-1's NCO and stages
-  // C-E) when they are the long part of the back half: many recurrences, or a span's long
-  // call.  A few per-block recurrences (c4: one, ~20 us) run on the back stream instead -- each
-  // cross-stream hop costs ~10 us of queue hand-off, more than the overlap returns (c4
-  // pipelined 790-840 -> 950 MS/s; 64-stream C5 blocks 98 -> 92 k MS/s the other way).
-  // SDR_RX_PLL_STREAM=0 / 1 forces either (A/B).
+  // C-E) whenever the receiver is pipelined.  Round 4 kept a few per-block recurrences (c4:
+  // one, ~26 us) on the back stream, where each cross-stream hop then cost more than the
+  // overlap returned (c4 790-840 -> 950 MS/s); with two blocks in flight and the trimmed
+  // event calls (r04b) the hop pays: c4 1 022 -> 1 090 MS/s (medians of 8 interleaved runs,
+  // profiles/r04/iter/r04b/pllstream/).  SDR_RX_PLL_STREAM=0 / 1 forces either (A/B).
   static const int pll_stream = [] { const char* e = getenv("SDR_RX_PLL_STREAM"); return e ? (e[0] == '0' ? 0 : 1) : -1; }();
-  const int njobs = (stx ? 1 : 0) + (rd ? 1 : 0);
-  const bool mid = r->pipe && (pll_stream >= 0 ? pll_stream == 1 : (S * njobs >= 8 || M > SDR_PLL_BLOCK_MAX));
+  const bool mid = r->pipe && (pll_stream >= 0 ? pll_stream == 1 : true);
   hipStream_t ps = mid ? r->mid : st;
   PllJobs P{};
   if (plls) {
