@@ -1147,10 +1147,11 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
                              hipMemcpyDeviceToHost, st));
   }
   const int qb = (int)((r->blocks - 1) % r->nq);
-  if (r->pipe && !copied) {
+  if (r->pipe && !copied && r->depth < r->nq) {
     // nothing after the back half: its row-set event marks the block's completion (one event
-    // call fewer per block; a later block of the same set re-recording it before this one is
-    // delivered -- depth 3 -- only makes the wait longer)
+    // call fewer per block).  Not at depth 3 (nq 3): block k+3 re-records the set's event
+    // before block k is delivered, and the host would wait for the newest block each time --
+    // the pipeline drained at every call (c4 1 163 -> 472 MS/s)
     P.ev = r->ev_back[qb];
   } else {
     // the row set is free for block k+nq once these copies have read it too (the event the
