@@ -95,6 +95,9 @@ def parse():
                          "line's n_gpus then counts distinct devices)")
     ap.add_argument("--cpu-samples", type=int, default=4_096_000, help="complex samples per CPU stream")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall time per CPU leg")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="mono with extras: the full record (every field of every configuration) is written here; "
+                         "the printed line is its compact form ('' prints the full record instead)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "fe_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per FE launch (written by tools/pmc_traffic.py)")
     a = ap.parse_args()
@@ -447,6 +450,7 @@ def main():
             "config": {"workload": f"RF front end ({args.taps}-tap LPF, decim 10, atan2 demod) + mono "
                                    f"({args.audio_taps}-tap LPF, decim 5): configs[1]+[2], one stream per GPU",
                        "block_complex": BLOCK, "blocks_per_step": args.blocks, "complex_per_step": n_total,
+                       "taps": args.taps,
                        "iq": args.iq, "path": args.path,
                        "parallelism": f"one stream in {ws} ranges + halo" if args.split_stream else
                        f"independent streams x{ws}"},
@@ -498,10 +502,80 @@ def main():
         if rank == 0:
             result.update(extras)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args)
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if d is not None and k in d}
+
+
+def compact_line(result: dict) -> dict:
+    """The printed line: every headline key, and each extra configuration by its numbers
+    (value, ms, stage times, solver counters, CPU baseline) -- short enough that the driver's
+    2 000-character tail of stdout holds all of it, c5 last.  The full
+    record (notes, samples, per-run strings) goes to the --detail file."""
+    out = {k: result[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data") if k in result}
+    dv = result.get("devices") or {}
+    out["devices"] = {"distinct": dv.get("distinct"), "ranks": dv.get("ranks")}
+    cfg = result.get("config", {})
+    out["config"] = _pick(cfg, ("blocks_per_step", "complex_per_step", "iq", "path"))
+    out["config"]["workload"] = (f"FE ({cfg.get('taps', '?')}-tap LPF, /10, atan2) + mono (151-tap LPF, /5): "
+                                 f"configs[1]+[2]") if "taps" in cfg else cfg.get("workload")
+    rf = result.get("roofline", {})
+    out["roofline"] = _pick(rf, ("bound", "achieved", "peak", "unit", "frac", "traffic", "avg_launch_ms",
+                                 "algorithmic_bytes_per_launch", "read_stream_gbs", "frac_of_stream_ceiling"))
+    out["roofline"]["kernel"] = (rf.get("kernel") or "").split(" (")[0]
+    cb = result.get("cpu_baseline")
+    if cb is not None:
+        c = _pick(cb, ("value", "unit", "cores", "kind"))
+        c["sample"] = (cb.get("sample") or "")[:80]
+        ref = cb.get("reference_cpp_fe") or {}
+        c["reference_cpp_fe"] = ref.get("value")
+        out["cpu_baseline"] = c
+    else:
+        out["cpu_baseline"] = None
+    cpu_v = lambda d: (d.get("cpu_baseline") or {}).get("value")   # noqa: E731
+    if "u8" in result:
+        u = result["u8"]
+        out["u8"] = dict(_pick(u, ("value", "avg_launch_ms")), frac=u["roofline"]["frac"])
+    for key in ("c3", "c4"):
+        if key in result:
+            r = result[key]
+            out[key] = dict(_pick(r, ("value",)), sync_ms=(r.get("sync") or {}).get("ms_per_block"), cpu=cpu_v(r))
+    for key in ("c4_span", "c5_1stream"):
+        if key in result:
+            out[key] = _pick(result[key], ("value", "ms_per_step"))
+    if result.get("detail"):
+        out["detail"] = result["detail"]
+    if "c5" in result:
+        r = result["c5"]
+        pl = r.get("pll_solver") or {}
+        c5 = _pick(r, ("value", "ms_per_step", "stage_ms", "stage_tflops"))
+        c5["pll"] = {k: pl.get(k) for k in ("recurrences", "spec_r0", "sequential", "long_stops", "long_tail")}
+        c5["frac"] = (r.get("roofline") or {}).get("frac")
+        c5["cpu"] = cpu_v(r)
+        out["c5"] = c5
+    return out
+
+
+def emit(result: dict, args):
+    """Rank 0's one JSON line: compact (compact_line) when the record carries the extra
+    configurations, with the whole record in args.detail; otherwise the record itself."""
+    line = result
+    if any(k in result for k in ("c5", "c3", "u8")) and args.detail:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+            with open(args.detail, "w") as f:
+                json.dump(result, f)
+            result["detail"] = os.path.relpath(os.path.abspath(args.detail), ROOT)
+        except OSError as e:
+            result["detail"] = f"not written: {e}"
+        line = compact_line(result)
+    print(json.dumps(line), flush=True)
 
 
 def cpu_cores():
@@ -802,6 +876,21 @@ def chain_flops_per_sample(rf_taps=151, taps=151, audio_decim=5, up=19, down=80)
     return 2.0 * (2 * rf_taps + macs_demod) / 10.0
 
 
+def stage_macs_per_demod(taps=151, audio_decim=5, up=19, down=80, stereo=True, rds=True):
+    """Multiply-adds per demod-rate sample of each receiver stage as the kernels run them
+    (csrc/rx.hip): stage A = audio LPF /5 + pilot BPF + stereo BPF + RDS extract BPF, B = the
+    RDS square BPF, C = stereo mixer LPF /5 + RDS I/Q mixer LPFs, D = the x19 /80 resamplers
+    (taps/19 per output, 19/80 outputs per sample), E = RRC I/Q at the resampled rate."""
+    m = {"filters_of_demod": taps / audio_decim + (2 * taps if stereo else 0) + (taps if rds else 0)}
+    if rds:
+        m["rds_square"] = taps
+    m["mix_lpf"] = (taps / audio_decim if stereo else 0) + (2 * taps if rds else 0)
+    if rds:
+        m["resample"] = 2 * (taps / up) * up / down
+        m["rrc"] = 2 * taps * up / down
+    return m
+
+
 def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, args=None, B=None, stereo=True,
                rds=True, u8=True, rf_taps=151):
     """configs[4] per GPU: S independent u8 streams of K reference blocks each, device-resident,
@@ -879,6 +968,14 @@ def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, arg
                            ("HBM: IQ in, demod out" if dom == "fe" else "FP32 VALU: FIR multiply-adds")},
         "pll_solver": pll,
     }
+    # per-stage achieved FP32 TFLOP/s (2 flops per multiply-add) against VALU_PEAK_TFLOPS, and the
+    # FE's HBM GB/s (IQ in, demod out)
+    demod = S * n / 10
+    out["stage_tflops"] = {k: round(2 * v * demod / (stage_ms[k] * 1e-3) / 1e12, 1)
+                           for k, v in stage_macs_per_demod(stereo=stereo, rds=rds).items()
+                           if stage_ms.get(k, 0) > 0}
+    out["fe_gbs"] = (round((S * n * (2 if u8 else 8) + 4 * demod) / (stage_ms["fe"] * 1e-3) / 1e9, 1)
+                     if stage_ms.get("fe") else None)
     pr = pll_roofline(stage_ms.get("pll", 0.0), S, K, B, (2 if rds else 1) * S * (n // 10)) if stereo else None
     if pr is not None:
         out["pll_roofline"] = pr

@@ -148,13 +148,11 @@ class Receiver:
         return self._pending.popleft() if len(self._pending) > self.depth else None
 
     def flush(self):
-        """Wait for every submitted block: depth 1, the last block's outputs (or None); deeper,
-        the list of the blocks' outputs not yet returned, oldest first."""
+        """Wait for every submitted block; returns the list of the blocks' outputs not yet
+        returned by submit(), oldest first (empty when none is in flight), at any depth."""
         check(self.lib.sdr_rx_flush(self.handle), "sdr_rx_flush")
         rest = list(self._pending)
         self._pending.clear()
-        if self.depth == 1:
-            return rest[-1] if rest else None
         return rest
 
     def _length(self, name):

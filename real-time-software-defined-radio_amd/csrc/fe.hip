@@ -1268,15 +1268,6 @@ static hipError_t launch_fe_t(const FeLaunch& a, hipStream_t st) {
 
 }  // namespace
 
-// SDR_FE_MFMA=0 keeps u8 calls on fe_slot_kernel (A/B runs; read once)
-static bool fe_mfma_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("SDR_FE_MFMA");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // Returns hipErrorInvalidValue for an unsupported (taps, decim) pair; the C-ABI
 // reports that as SDR_EUNSUPPORTED.  Supported: the reference's RF configs
 // (151 taps: model/fmMonoBlock.py:24; 101 taps: BASELINE configs) at decim 10.
@@ -1285,7 +1276,7 @@ hipError_t sdr_launch_fe(const FeLaunch& a, hipStream_t st) {
   // u8 IQ: the RF FIR on the int8 matrix cores where it covers the call (fe_mfma.hip)
   // (hipErrorInvalidValue: a call it does not cover, which the vector kernels take; any other
   // error is a failed launch and is returned, not retried on a different arithmetic path)
-  if (a.u8 && fe_mfma_enabled()) {
+  if (a.u8) {
     const hipError_t em = sdr_launch_fe_mfma(a, st);
     if (em != hipErrorInvalidValue) return em;
   }

@@ -45,23 +45,9 @@ constexpr float kPiF = 3.14159265358979323846f;
 #define SDR_FE_MFMA_ABL 0
 #endif
 constexpr int kAbl = SDR_FE_MFMA_ABL;
-// A/B builds: the A fragments built in every wave's prologue instead of loaded (-DSDR_FE_MFMA_HOST_AFR=0)
-#ifndef SDR_FE_MFMA_HOST_AFR
-#define SDR_FE_MFMA_HOST_AFR 1
-#endif
-constexpr bool kHostAfr = SDR_FE_MFMA_HOST_AFR != 0;
-// A/B builds of fe_mfma_mono_kernel: the A fragments loaded from the tap set's table (12 KB,
-// L1-resident) at every tile instead of held in 48 registers for the whole run, and the
-// occupancy target one wave per SIMD higher (-DSDR_FE_MFMA_AFR_L1=1)
-#ifndef SDR_FE_MFMA_AFR_L1
-#define SDR_FE_MFMA_AFR_L1 0
-#endif
-constexpr bool kAfrL1 = SDR_FE_MFMA_AFR_L1 != 0;
-#if SDR_FE_MFMA_AFR_L1
-#define SDR_FE_MFMA_WPE 4
-#else
+// fe_mfma_mono_kernel: 3 waves per SIMD (161 VGPRs).  r04b measured the A fragments loaded
+// from L1 at every tile (123 VGPRs, 4 waves per SIMD): 77 against 67 us
 #define SDR_FE_MFMA_WPE 3
-#endif
 
 constexpr float k2PiF = 6.28318530717958647692f;
 
@@ -184,10 +170,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDR_FE_MFMA_
 
   // A fragments: lane (r = l & 15, g = l >> 4), byte j of K-step ks <-> j' = 64 ks + 16 g + j;
   // from the tap set's table (one 16-B load each) or built here (~700 VALU per wave)
-  // (kAfrL1: loaded by each tile's MFMAs instead, the launcher guarantees the table)
   i4v afr[4][3];
-  if (kAfrL1) {
-  } else if (p.afr != nullptr) {
+  if (p.afr != nullptr) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
@@ -347,15 +331,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDR_FE_MFMA_
     for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
       for (int dg = 0; dg < 3; ++dg) acc[ch][dg] = i4v{0, 0, 0, 0};
-    // kAfrL1: an offset laundered per tile, so the loads are not hoisted out of the loop (the
-    // pointer itself stays a global one: a laundered pointer becomes a flat load)
-    int ao = 0;
-    if (kAfrL1) asm volatile("" : "+s"(ao));
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       i4v a[3];
 #pragma unroll
-      for (int dg = 0; dg < 3; ++dg) a[dg] = kAfrL1 ? p.afr[ao + (ks * 3 + dg) * 64 + lane] : afr[ks][dg];
+      for (int dg = 0; dg < 3; ++dg) a[dg] = afr[ks][dg];
       i4v bf[2];
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) bf[ch] = *reinterpret_cast<const i4v*>(&img[ch][160 * pl + 64 * ks + 16 * gl]);
@@ -773,7 +753,7 @@ hipError_t launch_demod_mfma_t(const FeLaunch& a, hipStream_t st) {
   if (p.total > 0x7fffffff) return hipErrorInvalidValue;
   p.taps = a.taps_dev;
   p.qscale = std::ldexp(1.0f, S);
-  p.afr = kHostAfr ? reinterpret_cast<const i4v*>(a.afr) : nullptr;
+  p.afr = reinterpret_cast<const i4v*>(a.afr);
   p.zi_i = a.zi_i;
   p.zi_q = a.zi_q;
   p.zi_stride = a.zi_stride;
@@ -866,8 +846,7 @@ hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps_rev, in
   if (p.total > 0x7fffffff) return hipErrorInvalidValue;
   p.taps = a.taps_dev;
   p.qscale = std::ldexp(1.0f, S);
-  p.afr = kHostAfr ? reinterpret_cast<const i4v*>(a.afr) : nullptr;
-  if (kAfrL1 && p.afr == nullptr) return hipErrorInvalidValue;
+  p.afr = reinterpret_cast<const i4v*>(a.afr);
   p.argev = ataps_rev;
   p.audio = audio;
   p.audio_stride = audio_stride;
@@ -875,8 +854,7 @@ hipError_t sdr_launch_fe_mono_mfma(const FeLaunch& a, const float* ataps_rev, in
   const int slots = per_device(slot_cache, [] {
     int per = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fe_mfma_mono_kernel, 64, 0) != hipSuccess || per <= 0) per = 1;
-    int cap = 4 * SDR_FE_MFMA_WPE;
-    if (const char* e = std::getenv("SDR_FE_MFMA_WPC")) cap = std::max(1, std::atoi(e));   // waves per CU (A/B)
+    const int cap = 4 * SDR_FE_MFMA_WPE;                 // waves per CU (r04b sweep: 12 of 8-16)
     return device_cus() * std::min(per, cap);
   });
 

@@ -512,7 +512,7 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 #define SDR_SPEC_W 32
 #endif
 // warm-up samples before each chunk (A/B builds: -DSDR_SPEC_W=).  r04: 32 -- the guess runs
-// the true step from the measured drift, and in the per-block solve of one recurrence (C4, a
+// the true step from the measured phase, and in the per-block solve of one recurrence (C4, a
 // 256-thread workgroup: one wave per SIMD, no other wave to hide the f64 latency behind) the
 // 128-step warm-up was 40 % of the kernel (spec_prof: 22 k of 52 k cycles).  r03, per-block solves at 64
 // streams x 2 PLLs (profiles/r03/iter/specw_*): 256 -> 86 us, 128 -> 73 us, 64 -> 66 us per
@@ -778,12 +778,8 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // chunk" predicate (its selects and compares were a fifth of the check loop's VALU); the wave
   // holding the last, partial chunk (and the unused ones) keeps them.  wfast: also every chunk
   // after a long call's pre-roll, so every step's wrap margin counts and every phase is stored.
-#ifdef SDR_PLL_NOFAST     // A/B builds only: every wave on the general step loops
-  const bool wfull = false, wfast = false;
-#else
   const bool wfull = __all(len == L);
   const bool wfast = wfull && __all(k0 >= pre);
-#endif
   // 0. where the locked phase estimate goes within the block, measured from the input: a
   // locked loop keeps its angle th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's
   // phase, so z_j = sum over chunk j of x_k exp(-i w (off + k)) ~ (A/2) exp(i phaseEst) (+ an
@@ -821,19 +817,10 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
           for (int u = 0; u < SB; ++u) {
             // x > 0: +exp(-i a); x < 0: -exp(-i a) (the pi of sel); 0 / NaN / past the chunk: 0
             const float sg = (F || i0 + u < len) ? (float)cd[u] : 0.f;
-#ifdef SDR_PLL_OLDCORR    // A/B builds only: the scalar rotation of round 4
-            z.x = fmaf(sg, c.x, z.x);
-            z.y = fmaf(sg, c.y, z.y);
-            const float nr = c.x * dc - c.y * ds;
-            c.y = fmaf(c.x, ds, c.y * dc);
-            c.x = nr;
-            (void)rs;
-#else
             const f2v sgv = f2v{sg, sg};
             asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(z) : "v"(sgv), "v"(c));
             const f2v t = c * dcv;
             asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1]" : "=v"(c) : "v"(c), "v"(rs), "v"(t));
-#endif
           }
         }
       };
@@ -879,13 +866,13 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   double xs_p = 0.0, xs_v = 0.0, xe_p = 0.0, xe_v = 0.0;
   {
     // the true step from a seed on the measured drift: phaseEst ~ p1 + D at the warm-up's
-    // start, integ ~ the measured drift per step; 256 steps of the loop then pull the guess
-    // onto the trajectory
+    // start, the integrator the block's first; the SW warm-up steps of the loop then pull the
+    // guess onto the trajectory (r05: the seed no longer estimates integ from the drift -- that
+    // needed a warm-up of >= 64 steps, longer than SW since r04)
     constexpr int SW = LONG ? SPEC_W_LONG : SPEC_W;
     const int kw = max(1, k0 - SW);
     const int jw = (kw - 1) / L;
     double p = p1 + yb[jw].x, V = v1;
-    if (k0 - kw >= 64 && tid < TE) V = (yb[tid].x - yb[jw].x) / (double)(k0 - kw) - kds;
     const int W = tid < TE ? k0 - kw : 0;        // warm-up steps (over the chunks before this one)
     if (wfull && SW <= 2 * L) {
       // every warm-up is the last SW steps before the chunk: the last SW - L of chunk j-2 when
@@ -1134,9 +1121,6 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     if (tid == 0 && nmiss == 0 && (bid == 0 || (bid % 479) == 3))
       printf("spec_prof blk %d L %d: stage %lld corr %lld guess %lld solve %lld check %lld (%d marks)\n", bid, L,
              tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], ntp);
-#endif
-#ifdef SDR_PLL_SPEC_DEBUG   // A/B builds only (make ... CXXFLAGS+=-DSDR_PLL_SPEC_DEBUG): never in libsdr.so
-    if (tid == 0) printf("pll_spec q%d s%d n%ld T%d L%d TE%d round %d: %d chunks missed\n", q, s, (long)n, SPEC_T, L, TE, round, nmiss);
 #endif
     if (nmiss == 0) {
       if constexpr (LONG) {
@@ -1583,9 +1567,6 @@ __device__ int chain_pass(const PllJobs& P, const int r) {
         sp = sE[0][tid - 1] + (pp[0] * sR[0][tid - 1] + pp[1] * sR[1][tid - 1]);
         si = sE[1][tid - 1] + (pp[2] * sR[0][tid - 1] + pp[3] * sR[1][tid - 1]);
       }
-#ifdef SDR_PLL_LONG_DEBUG
-      printf("chain r%d b%d/%d status %d: err %.3e rho %.3e %.3e n %.0f\n", r, j, nb, sj, err, rp, rv, nj);
-#endif
       LongBlk* B = long_blk(P, r, j);
       B->u[0] = ai;
       B->u[1] = ap;
@@ -1853,19 +1834,11 @@ int pll_lpw(const PllJobs& P) {
   while (lpw < 64 && P.njobs * ((P.nstreams + lpw - 1) / lpw) > kMaxPllWaves) lpw *= 2;
   return lpw;
 }
-// the parallel solve runs ahead of the loop kernel unless SDR_PLL_SPEC=0 (A/B runs)
-bool pll_spec_enabled() {
-  static const bool on = [] { const char* e = getenv("SDR_PLL_SPEC"); return !(e && e[0] == '0'); }();
-  return on;
-}
-// a per-block call solved by pll_spec_kernel alone (its own sequential fallback): no prep or
-// loop kernel, plain (not Q-form) phase rows
-bool spec_only(const PllJobs& P) { return pll_spec_enabled() && P.n >= 2; }
-// a spec-only call's NCO rows by the solve's own launch unless SDR_PLL_NCO_FUSE=0 (A/B runs)
-bool nco_fused(const PllJobs& P) {
-  static const bool on = [] { const char* e = getenv("SDR_PLL_NCO_FUSE"); return !(e && e[0] == '0'); }();
-  return on && spec_only(P);
-}
+// a per-block call (n >= 2) is solved by pll_spec_kernel alone (its own sequential fallback):
+// no prep or loop kernel, plain (not Q-form) phase rows, and its NCO rows written by the
+// solve's own launch.  The sequential kernels run 1-sample calls.
+bool spec_only(const PllJobs& P) { return P.n >= 2; }
+bool nco_fused(const PllJobs& P) { return spec_only(P); }
 hipError_t pll_check(const PllJobs& P, bool* vec) {
   if (P.njobs < 1 || P.njobs > SDR_PLL_MAXJ || P.nstreams <= 0 || P.n < 0) return hipErrorInvalidValue;
   *vec = true;
@@ -1881,18 +1854,9 @@ hipError_t pll_check(const PllJobs& P, bool* vec) {
 
 namespace {
 // ---- long calls: host-side setup ---------------------------------------------------
-// A per-block call is split the same way when it is long enough: pseudo-blocks of about
-// SDR_PLL_SPLIT steps (default 0 = off: one workgroup per recurrence, the per-block
-// solve).  A block's recurrence then runs on several workgroups (C4: 5 120 steps -> 4; C5:
-// 15 360 -> 10) instead of one, whose 256-512 threads' warm-ups were most of its time.
-int split_pb() {
-  static const int v = [] {
-    const char* e = getenv("SDR_PLL_SPLIT");
-    return e ? std::max(0, atoi(e)) : 0;
-  }();
-  return v;
-}
-bool long_n(int64_t n) { return n > SPEC_NMAX || (split_pb() > 0 && n >= 2 * (int64_t)split_pb()); }
+// (r04 measured splitting per-block calls into pseudo-blocks too -- slower: every
+// pseudo-block pays its pre-roll; removed in r05)
+bool long_n(int64_t n) { return n > SPEC_NMAX; }
 bool pll_long(const PllJobs& P) { return long_n(P.n); }
 
 // pseudo-blocks of <= LONG_PB steps: with a pre-roll of <= LONG_PRE_MAX steps one solve is at
@@ -1900,8 +1864,7 @@ bool pll_long(const PllJobs& P) { return long_n(P.n); }
 constexpr int LONG_PRE_MAX = 2048;
 constexpr int LONG_PB = SPEC_NMAX - 1 - LONG_PRE_MAX;
 void long_geom(int64_t n, int64_t* pb, int* nb) {
-  const int64_t per = n > SPEC_NMAX ? LONG_PB : split_pb();
-  const int64_t k = (n + per - 1) / per;
+  const int64_t k = (n + LONG_PB - 1) / LONG_PB;
   *nb = (int)k;
   *pb = (n + k - 1) / k;
 }
@@ -1948,14 +1911,10 @@ void loop_bounds(const PllCfg& c, double* c1, double* c2) {
 
 // pre-roll length: the error contracts by sqrt(1 - Kp) per step; enough steps to bring the
 // seed's error (the measured phase: ~0.1 rad) within LONG_ACCEPT (the stereo loop: ~1 500),
-// unless that exceeds SDR_PLL_WARM_MAX (default and most LONG_PRE_MAX = 2 048: the RDS loop
-// would need ~15 000) -- then 1 024 steps, enough for the linear bound; such blocks are fixed
-// up from the chained start.
+// unless that exceeds LONG_PRE_MAX = 2 048 (the RDS loop would need ~15 000) -- then 1 024
+// steps, enough for the linear bound; such blocks are fixed up from the chained start.
 int warm_len(const PllCfg& c, double c1, int64_t pb) {
-  static const int cap = [] {
-    const char* e = getenv("SDR_PLL_WARM_MAX");
-    return e ? std::min(std::max(64, atoi(e)), LONG_PRE_MAX) : LONG_PRE_MAX;
-  }();
+  constexpr int cap = LONG_PRE_MAX;
   const double rate = -0.5 * std::log1p(-std::min(std::max(c.kp, 1e-12), 0.999));
   const double want = std::log(std::max(c1, 1.0) * 0.1 / LONG_ACCEPT) / rate;   // from a 0.1 rad seed
   int64_t wl = (int64_t)std::ceil(want / 256.0) * 256;

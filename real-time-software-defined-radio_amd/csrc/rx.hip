@@ -938,9 +938,8 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   // one, ~26 us) on the back stream, where each cross-stream hop then cost more than the
   // overlap returned (c4 790-840 -> 950 MS/s); with two blocks in flight and the trimmed
   // event calls (r04b) the hop pays: c4 1 022 -> 1 090 MS/s (medians of 8 interleaved runs,
-  // profiles/r04/iter/r04b/pllstream/).  SDR_RX_PLL_STREAM=0 / 1 forces either (A/B).
-  static const int pll_stream = [] { const char* e = getenv("SDR_RX_PLL_STREAM"); return e ? (e[0] == '0' ? 0 : 1) : -1; }();
-  const bool mid = r->pipe && (pll_stream >= 0 ? pll_stream == 1 : true);
+  // profiles/r04/iter/r04b/pllstream/).
+  const bool mid = r->pipe;
   hipStream_t ps = mid ? r->mid : st;
   PllJobs P{};
   if (plls) {

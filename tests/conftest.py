@@ -71,9 +71,5 @@ LONG_PB = 14336
 
 def long_blocks(n):
     """pseudo-blocks of a PLL call of n samples (csrc/pll.hip long_geom): beyond 16 385 steps
-    pseudo-blocks of <= 14 336; a per-block call of >= 2 x SDR_PLL_SPLIT steps
-    in pseudo-blocks of about that size (off by default); else 1"""
-    if n > 16385:
-        return -(-n // LONG_PB)
-    split = max(0, int(os.environ.get("SDR_PLL_SPLIT", "0")))
-    return -(-n // split) if split > 0 and n >= 2 * split else 1
+    pseudo-blocks of <= 14 336; else 1"""
+    return -(-n // LONG_PB) if n > 16385 else 1

@@ -154,31 +154,38 @@ def test_receiver_argument_errors(sdr, gpu_ctx):
         _lib.check(gpu_ctx.lib.sdr_rx_create(gpu_ctx.handle, 1, 100, 0, 8, ctypes.byref(h)), "bad flags")
 
 
-@pytest.mark.parametrize("pipeline,depth", [(False, 1), (True, 1), (False, 2), (True, 2), (True, 3)])
-def test_receiver_submit_equals_process(sdr, gpu_ctx, pipeline, depth):
+@pytest.mark.parametrize("pipeline,depth,fetch", [(False, 1, "all"), (True, 1, "all"), (False, 2, "all"),
+                                                  (True, 2, "all"), (True, 3, "all"), (True, 1, "stage"),
+                                                  (True, 2, "stage"), (True, 3, "stage")])
+def test_receiver_submit_equals_process(sdr, gpu_ctx, pipeline, depth, fetch):
     """sdr_rx_submit / sdr_rx_flush (block k launched, block k-depth delivered; r04b: depth 2
     and 3 keep that many blocks in flight, a pipelined receiver then three row sets) ==
-    sdr_rx_run block by block, bit for bit, for every output -- the stage-stored ones (pinned
-    host stores) and the copied ones (demod, NCOs) -- with and without the two-stream pipeline."""
+    sdr_rx_run block by block, bit for bit -- with and without the two-stream pipeline.
+    fetch "all": every output, the stage-stored ones (pinned host stores) and the copied ones
+    (demod, NCOs); "stage": only the outputs stage kernels store (the default fetch, the shape
+    bench c3 / c4 time), where nothing follows the back half on the stream and the row-set
+    event doubles as the block's completion event (csrc/rx.hip sdr_rx_submit)."""
     B, S, nb = 51_200, 2, 6
     iq = np.stack([sdr.synth.fm_iq(nb * B, seed=60 + s) for s in range(S)])
     kw = dict(stereo=True, rds=True, iq_dtype=np.float32)
     ref_rx = sdr.Receiver(S, B, **kw)
     rx = sdr.Receiver(S, B, pipeline=pipeline, depth=depth, **kw)
-    names = ref_rx.outputs
+    names = ref_rx.outputs if fetch == "all" else None
     want = [ref_rx.process(iq[:, 2 * k * B:2 * (k + 1) * B], fetch=names) for k in range(nb)]
+    if fetch != "all":
+        assert sorted(want[0]) == sorted(["audio", "left", "right", "rrc_i", "rrc_q"])
     got = []
     for k in range(nb):
         prev = rx.submit(iq[:, 2 * k * B:2 * (k + 1) * B], fetch=names)
         assert (prev is None) == (k < depth)
         if prev is not None:
             got.append(prev)
-    rest = rx.flush()
-    got.extend([rest] if depth == 1 else rest)
+    got.extend(rx.flush())
     assert len(got) == nb
-    assert rx.flush() == (None if depth == 1 else [])
+    assert rx.flush() == []
     for k in range(nb):
-        for name in names:
+        assert sorted(got[k]) == sorted(want[k])
+        for name in want[k]:
             assert np.array_equal(got[k][name], want[k][name]), (name, k)
     # state after the last block, and a synchronous call after submits
     for a, b in zip(rx.state(), ref_rx.state()):

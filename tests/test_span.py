@@ -157,3 +157,76 @@ def test_span_bench_shape_matches_block_loop_and_oracle(sdr, gpu_ctx, oracle):
             scale = max(float(np.max(np.abs(want))), 1e-3)
             em, er = maxabs(gv, want) / scale, rms(gv, want) / scale
             assert em < tmax and er < trms, (key, k, em, er)
+
+
+def test_span_c5_timed_shape_eight_streams(sdr, gpu_ctx, oracle):
+    """The exact shape bench.py's `c5` line times: EIGHT u8 streams in one
+    receiver, spans of K = 256 blocks from device memory (sdr_rx_process_dev, as the bench),
+    i.e. a PLL job table of 16 recurrences x 275 pseudo-blocks chained in one launch.  Two spans
+    of a continuous stream per stream (the second is the locked, timed state); the 8 streams
+    are distinct windows of one synthetic capture.  Checked:
+      (a) stream s of the 8-stream span == a 1-stream span over the same IQ, bit for bit, for
+          every output (the streams of a job table are independent: same tiles, same solves);
+      (b) streams 0 and 7 against the oracle (model/fmMonoBlock.py:80-173,
+          model/fmRDSblock.py:127-204 with the C restatement of fmPll) on the first two and
+          last two blocks of the second span;
+      (c) the solver counters: 16 x 275 recurrences per span, no sequential tail; the locked
+          span all in round 0, no chain stop."""
+    from importlib import import_module
+    _lib = import_module("real-time-software-defined-radio_amd._lib")
+    S, K, spans = 8, 256, 2
+    n = K * B5
+    delta = 1_000_050                                   # window offset between streams (x 50: whole audio samples)
+    base = sdr.synth.fm_iq(spans * n + (S - 1) * delta + 1, seed=91, dtype=np.uint8)
+    win = lambda s: base[2 * s * delta:2 * (s * delta + spans * n + 1)]   # noqa: E731  (+1: the oracle's strict <)
+    rows = np.ascontiguousarray(np.stack([win(s)[:2 * spans * n] for s in range(S)]))
+    d = _lib.DeviceBuffer.from_array(gpu_ctx, rows)
+    row_bytes = rows.shape[1]
+    del rows
+    kw = dict(stereo=True, rds=True, iq_dtype=np.uint8)
+    rx = sdr.Receiver(S, n, **kw)
+    nb = long_blocks(K * (B5 // 10))
+    stats = []
+    for sp in range(spans):
+        gpu_ctx.pll_stats(reset=True)
+        rx.process_dev(d.ptr + sp * 2 * n, spans * n)     # stride: the row of every stream
+        stats.append(rx.pll_stats())
+        print(f"S8 span {sp} solver counters:", stats[-1])
+    for sp, st in enumerate(stats):
+        assert st["recurrences"] == 2 * S * nb and st["long_tail"] == 0, (sp, st)
+    st = stats[-1]
+    assert st["spec_r0"] == 2 * S * nb and st["sequential"] == 0 and st["long_stops"] == 0, st
+    got = {name: rx.output(name) for name in NAMES}
+    rx.close()
+    # (a) every stream against a 1-stream receiver over the same two spans
+    one = sdr.Receiver(1, n, **kw)
+    for s in range(S):
+        one.reset()
+        for sp in range(spans):
+            one.process_dev(d.ptr + s * row_bytes + sp * 2 * n, n)
+        for name in NAMES:
+            assert np.array_equal(one.output(name)[0], got[name][s]), (name, s)
+    one.close()
+    d.free()
+    # (b) streams 0 and 7 against the oracle on the second span's first two and last two blocks
+    M = B5 // 10
+    for s in (0, S - 1):
+        iq = win(s)
+        mono = oracle.mono_stereo_blocks((iq.astype(np.float64) - 128.0) / 128.0, B5, rf_taps=151, audio_taps=151,
+                                         nblocks=spans * K, pll_fn=oracle.fm_pll_c)
+        rds = oracle.rds_blocks(iq, 2 * B5, taps=151, nblocks=spans * K, pll_fn=oracle.fm_pll_c)
+        A = len(mono[0]["audio"])
+        for kk in (0, 1, K - 2, K - 1):
+            k = K + kk
+            for key in ("audio", "stereo", "left", "right"):
+                gv, want = got[key][s][kk * A:(kk + 1) * A], mono[k][key]
+                assert rms(gv, want) < AUDIO_RMS and maxabs(gv, want) < AUDIO_MAX, (key, s, k, rms(gv, want))
+            assert maxabs(got["nco"][s][kk * M:kk * M + M + 1], mono[k]["nco"]) < 3e-7, (s, k)
+            for key, (tmax, trms) in RDS_TOL.items():
+                want = rds[k][key]
+                m = len(want) - 1 if key in NCO_NAMES else len(want)
+                gv = got[key][s][kk * m:kk * m + len(want)]
+                scale = max(float(np.max(np.abs(want))), 1e-3)
+                em, er = maxabs(gv, want) / scale, rms(gv, want) / scale
+                assert em < tmax and er < trms, (key, s, k, em, er)
+        del mono, rds
