@@ -666,7 +666,8 @@ def rx_measure(ctx, workload, args, rank, ws, steps, warmup, cpu=False):
     two_streams = pipe and (stereo or rds)
     depth = 1 if c5 else max(1, args.depth)
     mk = lambda two, d=1: rtsdr.Receiver(S, B, stereo=stereo, rds=rds, iq_dtype=np.uint8 if u8 else np.float32,
-                                         rf_coeff=rf_b, audio_coeff=au_b, pipeline=two, depth=d, ctx=ctx)
+                                         rf_coeff=rf_b, audio_coeff=au_b, pipeline=two, depth=d, keep=LEAN_KEEP,
+                                         ctx=ctx)
     rx = mk(two_streams, depth if pipe else 1)
     rx_sync = mk(False) if (pipe and not c5) else rx     # the one-block-at-a-time call
     nres = 16                                           # distinct blocks per stream, cycled
@@ -824,6 +825,10 @@ def rx_measure(ctx, workload, args, rank, ws, steps, warmup, cpu=False):
     return result
 
 C5_B = 153_600                 # complex samples per reference block (src/fm_radio.cpp:23)
+# what the receivers materialise on their device-resident path: every output but the NCO rows
+# and the RDS LPF rows, intermediates the chain does not need (sdr_rx_set_keep; the same values)
+LEAN_KEEP = ("demod", "audio", "bpf_recovery", "bpf_extraction", "stereo", "left", "right", "extract", "pre_pll",
+             "resample_i", "resample_q", "rrc_i", "rrc_q")
 VALU_PEAK_TFLOPS = 157.3       # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 # f64 VALU issue: a wave64 f64 instruction holds its SIMD 4 cycles (half the f32 rate: 78.6
 # TFLOP/s FMA), 256 CUs x 4 SIMDs x 2.4 GHz / 4 (tools/f64_probe.hip measured a lone wave at
@@ -865,28 +870,30 @@ def pll_roofline(stage_ms_pll, S, K, B, steps_per_span, path=None):
 
 
 def chain_flops_per_sample(rf_taps=151, taps=151, audio_decim=5, up=19, down=80):
-    """FP32 flops (2 per multiply-add) of the C5 chain's FIR work per complex input sample
-    (DESIGN.md §4): the RF FIR on I and Q at 1/10 of the input rate, then
-    per demod sample the stage filters -- audio LPF /5, pilot BPF, stereo BPF, RDS extract
-    (stage A), RDS square BPF (B), stereo LPF /5 and RDS I/Q LPFs (C), the x19 /80 resamplers
-    (taps/19 per output, 19/80 outputs per sample; D) and the RRC I/Q at the resampled rate
-    (E).  The demod atan2 and the PLLs (f64) are not counted."""
-    macs_demod = (taps / audio_decim + 3 * taps + taps + taps / audio_decim + 2 * taps
-                  + 2 * (taps / up) * up / down + 2 * taps * up / down)
+    """FP32 flops (2 per multiply-add) of the C5 chain's FIR work per complex input sample, as
+    the kernels run it: the RF FIR on I and Q at 1/10 of the
+    input rate, then per demod sample the stage filters (stage_macs_per_demod: the RDS LPF and
+    resampler as the composite filter).  The demod atan2, the NCOs and the PLLs (f64) are not
+    counted."""
+    macs_demod = sum(stage_macs_per_demod(taps, audio_decim, up, down).values())
     return 2.0 * (2 * rf_taps + macs_demod) / 10.0
 
 
 def stage_macs_per_demod(taps=151, audio_decim=5, up=19, down=80, stereo=True, rds=True):
     """Multiply-adds per demod-rate sample of each receiver stage as the kernels run them
-    (csrc/rx.hip): stage A = audio LPF /5 + pilot BPF + stereo BPF + RDS extract BPF, B = the
-    RDS square BPF, C = stereo mixer LPF /5 + RDS I/Q mixer LPFs, D = the x19 /80 resamplers
-    (taps/19 per output, 19/80 outputs per sample), E = RRC I/Q at the resampled rate."""
+    (csrc/rx.hip, the bench's keep set): stage A = audio LPF /5 + pilot BPF + stereo BPF + RDS
+    extract BPF, B = the RDS square BPF, C = the stereo mixer LPF /5, D = the RDS I/Q mixers +
+    3 kHz LPF + x19 /80 resampler as one composite filter (158 taps per output, 19/80 outputs
+    per sample), E = RRC I/Q at the resampled rate.  The NCOs the mixers form (f64 sincos) are
+    not counted."""
     m = {"filters_of_demod": taps / audio_decim + (2 * taps if stereo else 0) + (taps if rds else 0)}
     if rds:
         m["rds_square"] = taps
-    m["mix_lpf"] = (taps / audio_decim if stereo else 0) + (2 * taps if rds else 0)
+    m["mix_lpf"] = taps / audio_decim if stereo else 0
     if rds:
-        m["resample"] = 2 * (taps / up) * up / down
+        # the RDS mixers + LPF + resampler as one composite polyphase filter: (taps + 7)
+        # multiply-adds per output and channel, up/down outputs per demod sample
+        m["resample"] = 2 * (taps + (taps - 1) // up) * up / down
         m["rrc"] = 2 * taps * up / down
     return m
 
@@ -914,7 +921,7 @@ def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, arg
     cpu_rows = rows[0, :16 * 2 * B].copy() if cpu else None
     del rows
     rx = rtsdr.Receiver(S, n, stereo=stereo, rds=rds, iq_dtype=dt, rf_coeff=rf_b, audio_coeff=au_b,
-                        pipeline=pipeline, ctx=ctx)
+                        pipeline=pipeline, keep=LEAN_KEEP, ctx=ctx)
 
     def step():
         rx.process_dev(d_iq.ptr, n)

@@ -303,6 +303,15 @@ int sdr_rx_set_depth(sdr_rx* rx, int depth);
 int sdr_rx_set_pipeline(sdr_rx* rx, int on);
 int sdr_rx_output(sdr_rx* rx, int which, float** dev, int64_t* stride, int64_t* n);
 int sdr_rx_fetch(sdr_rx* rx, int which, float* host, int64_t host_stride); /* sync, all streams */
+/* Outputs sdr_rx_process_dev materialises (bit 1 << SDR_RX_O_*; default: every output of the
+ * flags).  The NCO rows (SDR_RX_O_STEREO_NCO, _RDS_NCO_I/_Q) and the RDS LPF rows (_RDS_LPF_I/_Q)
+ * are intermediates the chain itself does not need: without them the mixers form the NCO
+ * from the PLL phases where they stage their inputs and the RDS LPF runs inside the composite
+ * LPF + x19/80 resampler, so neither round-trips through HBM (the other outputs, which later
+ * stages read, are always written; every output's values are the same either way).
+ * sdr_rx_run / sdr_rx_submit materialise what they are asked for.  sdr_rx_fetch of an output
+ * the latest block did not materialise is SDR_EINVAL (sdr_rx_output still gives its row). */
+int sdr_rx_set_keep(sdr_rx* rx, uint64_t mask);
 /* per-stage timing of the last block (HIP events between the receiver's launches, on the
  * context stream): FE, stage A (filters of demod), B (RDS square), PLL, C (mixers + LPFs),
  * D (resamplers), E (RRC); ms: SDR_RX_NSTAGES floats.  Timing adds event records between

@@ -26,6 +26,8 @@ RX_FILTERS = ("rf", "audio", "pilot", "stereo_bpf", "stereo_lpf", "rds_extract",
 RX_OUTPUTS = ("demod", "audio", "bpf_recovery", "nco", "bpf_extraction", "stereo", "left", "right",
               "extract", "pre_pll", "nco_i", "nco_q", "lpf_i", "lpf_q", "resample_i", "resample_q",
               "rrc_i", "rrc_q")
+# stage C: the stereo mixer + LPF (and the RDS LPF rows when kept); "resample": the RDS mixers +
+# LPF + x19/80 resampler (the composite filter, csrc/rx.hip rx_cres_kernel)
 RX_STAGES = ("fe", "filters_of_demod", "rds_square", "pll", "mix_lpf", "resample", "rrc")
 # PLL solve counters (include/sdr.h SDR_PLL_ST_*)
 PLL_STATS = ("recurrences", "spec_r0", "spec_r1", "spec_r2", "sequential", "long_guessed", "long_chained",
@@ -103,6 +105,7 @@ SIGNATURES = {
     "sdr_rx_flush": (_i32, [_vp]),
     "sdr_rx_set_pipeline": (_i32, [_vp, _i32]),
     "sdr_rx_set_depth": (_i32, [_vp, _i32]),
+    "sdr_rx_set_keep": (_i32, [_vp, _c.c_uint64]),
     "sdr_rx_output": (_i32, [_vp, _i32, _c.POINTER(_vp), _c.POINTER(_i64), _c.POINTER(_i64)]),
     "sdr_rx_fetch": (_i32, [_vp, _i32, _fp, _i64]),
     "sdr_rx_state": (_i32, [_vp, _dp, _dp, _dp]),

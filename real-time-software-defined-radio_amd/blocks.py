@@ -52,7 +52,7 @@ class Receiver:
     def __init__(self, nstreams: int, block_complex: int, *, mono: bool = True, stereo: bool = False,
                  rds: bool = False, iq_dtype=np.uint8, rf_coeff=None, audio_coeff=None, stereo_taps: int = 151,
                  rds_taps: int = 151, rf_decim: int = 10, audio_decim: int = 5, pipeline: bool = False,
-                 depth: int = 1, ctx=None):
+                 depth: int = 1, keep=None, ctx=None):
         self.ctx = ctx if ctx is not None else _lib.get_context()
         self.lib = self.ctx.lib
         self.S, self.B = int(nstreams), int(block_complex)
@@ -88,6 +88,8 @@ class Receiver:
                   "sdr_rx_set_filter")
         check(self.lib.sdr_rx_set_decim(self.handle, int(rf_decim), int(audio_decim), design.RDS_UP,
                                         design.RDS_DOWN), "sdr_rx_set_decim")
+        if keep is not None:
+            self.set_keep(keep)
         self.M = (self.B + rf_decim - 1) // rf_decim
         self.A = (self.M + audio_decim - 1) // audio_decim
         self.R = (self.M * design.RDS_UP + design.RDS_DOWN - 1) // design.RDS_DOWN
@@ -159,6 +161,17 @@ class Receiver:
         if name not in self._lengths:
             self._lengths[name] = self.output_ptr(name)[2]
         return self._lengths[name]
+
+    def set_keep(self, names):
+        """Outputs process_dev materialises (sdr_rx_set_keep; default: all).  Leaving out the
+        NCO rows ("nco", "nco_i", "nco_q") and the RDS LPF rows ("lpf_i", "lpf_q") -- which the
+        chain itself does not need -- keeps them out of HBM: the mixers form the NCO from the PLL
+        phases and the RDS LPF runs inside the composite resampler (the same values either way).
+        process() / submit() materialise what they are asked for."""
+        mask = 0
+        for n in names:
+            mask |= 1 << RX_OUTPUTS.index(n)
+        check(self.lib.sdr_rx_set_keep(self.handle, mask), "sdr_rx_set_keep")
 
     def process_dev(self, iq_ptr: int, iq_stride: int):
         """One block from device memory (async on the context stream); outputs stay on the

@@ -110,6 +110,29 @@ int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T) 
   return SDR_OK;
 }
 
+int get_resp(sdr_ctx* c, const PllCfg& cfg, int64_t n, const double** out) {
+  *out = nullptr;
+  int64_t pb;
+  int nb;
+  if (!sdr_pll_long_geom(n, &pb, &nb)) return SDR_OK;
+  for (const RespTable& t : c->resp)
+    if (t.kp == cfg.kp && t.ki == cfg.ki && t.pb == pb) {
+      *out = t.dev;
+      return SDR_OK;
+    }
+  std::vector<double> h;
+  sdr_pll_resp_table(cfg, n, &h);
+  RespTable t;
+  t.kp = cfg.kp;
+  t.ki = cfg.ki;
+  t.pb = pb;
+  HIP_TRY(hipMalloc(&t.dev, sizeof(double) * h.size()));
+  HIP_TRY(hipMemcpy(t.dev, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+  c->resp.push_back(t);
+  *out = t.dev;
+  return SDR_OK;
+}
+
 }  // namespace sdrint
 
 namespace {
@@ -221,6 +244,7 @@ void sdr_destroy(sdr_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (int s = 0; s < S_NSLOT; ++s) if (c->slot[s]) (void)hipFree(c->slot[s]);
   for (TapSet& t : c->taps) { (void)hipFree(t.dev_f32); (void)hipFree(t.dev_f64); (void)hipFree(t.dev_afr); }
+  for (RespTable& t : c->resp) (void)hipFree(t.dev);
   if (c->pll_stats) (void)hipFree(c->pll_stats);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -582,6 +606,8 @@ int sdr_pll_dev(sdr_ctx* c, const float* in, int64_t n, int64_t in_stride, int n
                   nstreams > 1 ? out_stride : n + 1,
                   PllCfg{freq, fs, nco_scale, phase_adj, norm_bw * 2.666, norm_bw * norm_bw * 3.555}, cbuf, cst};
   P.stats = c->pll_stats;
+  P.nco_rows = 1;                                   // fmPll's outputs are the NCO rows
+  TRY(get_resp(c, P.j[0].cfg, n, &P.j[0].resp));
   const int64_t wb = sdr_pll_work_bytes(1, nstreams, n);    // long calls: pseudo-block records
   if (wb > 0) TRY(scratch(c, S_PLLW, (size_t)wb, &P.work));
   HIP_TRY(sdr_launch_pll_jobs(P, c->stream));

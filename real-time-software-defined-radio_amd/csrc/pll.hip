@@ -41,7 +41,10 @@
 #include <mutex>
 
 #include "sdr_launch.h"
+#include "sdr_nco.h"
 #include "../../include/sdr.h"
+
+using namespace sdrnco;
 
 namespace {
 
@@ -63,62 +66,6 @@ __device__ __forceinline__ void stat_max_wave(unsigned long long* s, int k, bool
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o, 64));
   if ((threadIdx.x & 63) == 0) stat_max(s, k, x);
-}
-
-// 2*pi split into three parts (Cody-Waite), so n*P1 and n*P2 are exact for |n| < 2^26.
-constexpr double kP1 = 6.2831854820251465;       // float32(2 pi), 24 significant bits
-constexpr double kP2 = -1.748455600074497e-07;    // double(2 pi - kP1)
-constexpr double kP3 = -1.0687562935444062e-23;   // remainder
-constexpr double kInv2Pi = 0.15915494309189535;
-constexpr double kPi = 3.14159265358979323846;
-constexpr double k2Pi = 6.28318530717958647692;
-
-// r = a - 2*pi*n, n = rint(a / 2pi), |r| <= pi (up to one ulp at the boundary).
-__device__ inline double reduce_2pi(double a) {
-  const double n = rint(a * kInv2Pi);
-  double r = fma(-n, kP1, a);
-  r = fma(-n, kP2, r);
-  r = fma(-n, kP3, r);
-  return r;
-}
-
-// sin and cos of a reduced angle |a| <= pi (+ an ulp), for the NCO outputs (f32: 6e-8 is their
-// rounding): quadrant n = rint(a 2/pi) (a two-part pi/2: exact to ~1e-32 for |n| <= 2), then
-// Taylor polynomials on |y| <= pi/4 to y^13 / y^14 (truncation < 3e-14).  ~35 VALU against
-// the library sincos's general-argument path.
-// OPAQUE: each coefficient is made an SGPR at its use (a volatile asm): in kernels that call
-// this once per call (end states) the compiler otherwise keeps all 14 in VGPRs for the whole
-// kernel, which spilled the long-call fix kernel
-template <bool OPAQUE = false>
-__device__ __forceinline__ void sincos_red(double a, double* sv, double* cv) {
-  auto K = [](double c) {
-    if constexpr (OPAQUE) asm volatile("" : "+s"(c));
-    return c;
-  };
-  constexpr double kPio2Hi = 1.5707963267948966, kPio2Lo = 6.123233995736766e-17, k2oPi = 0.6366197723675814;
-  const double n = rint(a * k2oPi);
-  double y = fma(-n, kPio2Hi, a);
-  y = fma(-n, kPio2Lo, y);
-  const double z = y * y;
-  double ps = K(1.0 / 6227020800.0);                        // 1/13!
-  ps = fma(ps, z, K(-1.0 / 39916800.0));
-  ps = fma(ps, z, K(1.0 / 362880.0));
-  ps = fma(ps, z, K(-1.0 / 5040.0));
-  ps = fma(ps, z, K(1.0 / 120.0));
-  ps = fma(ps, z, K(-1.0 / 6.0));
-  const double sn = fma(ps * z, y, y);
-  double pc = K(1.0 / 87178291200.0);                       // 1/14!
-  pc = fma(pc, z, K(-1.0 / 479001600.0));
-  pc = fma(pc, z, K(1.0 / 3628800.0));
-  pc = fma(pc, z, K(-1.0 / 40320.0));
-  pc = fma(pc, z, K(1.0 / 720.0));
-  pc = fma(pc, z, K(-1.0 / 24.0));
-  pc = fma(pc, z, K(0.5));
-  const double cs = fma(-pc, z, 1.0);
-  const int q = (int)n & 3;
-  const double s0 = (q & 1) ? cs : sn, c0 = (q & 1) ? sn : cs;
-  *sv = (q == 2 || q == 3) ? -s0 : s0;
-  *cv = (q == 1 || q == 2) ? -c0 : c0;
 }
 
 // A call's end state from its last angle arg (fmPll.py:39-44): feedbackI/Q = cos/sin(arg) and
@@ -536,23 +483,10 @@ constexpr int SPEC_N256 = SDR_SPEC_N256;     // longest call the 256-thread solv
 constexpr int SPEC_LDS = 32 * 513;           // padded transposed bytes: 512 chunks of <= 32 steps (or 256 of <= 40)
 constexpr int SB = 8;                        // steps per batch of LDS reads in the step loops
 
-// ---- long calls: pseudo-block bookkeeping (device scratch P.work) --------------------
-// Per recurrence r = job * nstreams + stream: a header (the chain's position and the exact
-// state at it), then one LongBlk per pseudo-block: its start guess g (warm-up), its chained
-// start x (when re-solved), the end state e of its latest solve, the 2 pi shift the chain
-// found for it, and its status.  States are in fmPll's 6-double order.
+// ---- long calls: pseudo-block bookkeeping (device scratch P.work; LongBlk / LongHdr in
+// sdr_nco.h, which the receiver's mixers read too) ---------------------------------------
 enum { LB_NEED_G = 0, LB_DONE_G = 1, LB_NEED_X = 2, LB_DONE_X = 3, LB_ACCEPTED = 4 };
 constexpr int SOLVER_SEQ = 3;        // solver codes: 0..2 = parallel solve round, 3 = sequential
-// u: the start (phaseEst, integrator) the current solution (theta row, e) was solved from.
-// shift: the chain's whole turns for the block's phases; d: the start error (dphaseEst, dV)
-// the chain accepted the block with (its stored phases + the loop's linear response to d are
-// the recurrence's, nco_long_kernel adds both); margin: the solve's smallest distance of a
-// step's fract(t_k) from a wrap, in turns (-1: none, the sequential kernels' solves).
-struct LongBlk {
-  double g[6]; double x[6]; double e[6]; double u[2]; double shift; double d[2]; double margin; int status; int solver;
-};
-struct LongHdr { double sp, si; int pos; int pad; double pad2; };
-static_assert(sizeof(LongBlk) == 200 && sizeof(LongHdr) == 32, "long-call scratch layout");
 __device__ __forceinline__ LongHdr* long_hdr(const PllJobs& P, int r) { return static_cast<LongHdr*>(P.work) + r; }
 __device__ __forceinline__ LongBlk* long_blk(const PllJobs& P, int r, int b) {
   return reinterpret_cast<LongBlk*>(static_cast<char*>(P.work) + (int64_t)P.njobs * P.nstreams * sizeof(LongHdr)) +
@@ -1227,7 +1161,8 @@ __device__ void spec_fallback(const PllJobs& P, const int bid) {
 }
 
 // nco[k+1] from phaseEst_k for step k of recurrence g = (job, stream): th_k by the reference's
-// formula (fmPll.py:33), the Q-form row converted back when the loop kernels left one.
+// formula (fmPll.py:33, sdr_nco.h nco_value), the Q-form row converted back when the loop
+// kernels left one.
 __device__ __forceinline__ void nco_out(const PllJobs& P, const PllJob& J, int s, double off, int64_t k, double p) {
 #pragma clang fp contract(off)
   const double w = 2.0 * kPi * (J.cfg.freq / J.cfg.fs);
@@ -1235,13 +1170,10 @@ __device__ __forceinline__ void nco_out(const PllJobs& P, const PllJob& J, int s
     const double i = (double)(k % PG);
     p = p - (kPi * J.cfg.ki) * ((i + 1.0) * i * 0.5);
   }
-  const double th = w * ((off + (double)k) + 1.0) + p;
-  const double a = th * J.cfg.scale + J.cfg.adj;
-  // the reference's angle grows with the stream (~1e7 rad after a minute): reduced here by the
-  // 3-part Cody-Waite step (exact multiples of 2 pi for |n| < 2^26), sincos then takes its
-  // small-argument path instead of the large-argument reduction
+  // the reference's angle grows with the stream (~1e7 rad after a minute): nco_value reduces it
+  // by the 3-part Cody-Waite step (exact multiples of 2 pi for |n| < 2^26)
   double sv, cv;
-  sincos_red<true>(reduce_2pi(a), &sv, &cv);
+  nco_value<true>(w, J.cfg.scale, J.cfg.adj, k + 1, p, off, &cv, &sv);
   J.nco_i[(int64_t)s * J.out_stride + k + 1] = (float)cv;
   if (J.nco_q) J.nco_q[(int64_t)s * J.out_stride + k + 1] = (float)sv;
 }
@@ -1747,18 +1679,15 @@ __global__ void nco_jobs_kernel(PllJobs P) {
 
 // The NCO of a long call: phaseEst_k = the stored phase + 2 pi (the chain's turns for its
 // pseudo-block) + (A^(kk+1) d)_phase, the loop's linear response to the start error d the
-// chain accepted the pseudo-block with (kk: the step within it; zero for most blocks).
+// chain accepted the pseudo-block with (kk: the step within it; zero for most blocks), from
+// the response table (sdr_nco.h nco_phase_in: the receiver's mixers form the same double).
 // Workgroup: 256 x NCO_NR consecutive steps of ONE pseudo-block (grid.x = pseudo-blocks x
-// tiles per block), thread t the steps t + 256 i (coalesced): the shift and d are uniform and
-// the response branch with them; its responses 256 steps apart by A^256, A^(2^i) in LDS.
-#ifndef SDR_NCO_NR
-#define SDR_NCO_NR 8
-#endif
-constexpr int NCO_NR = SDR_NCO_NR;     // outputs per thread of nco_long_kernel (A/B builds: -DSDR_NCO_NR=)
+// tiles per block), thread t the steps t + 256 i (coalesced).  Runs only when an NCO row is an
+// output (P.nco_rows); the receiver's mixers otherwise take the phases directly.
+constexpr int NCO_NR = 8;              // outputs per thread of nco_long_kernel
 __host__ __device__ inline int nco_tiles_per_block(int64_t pb) { return (int)((pb + 256 * NCO_NR - 1) / (256 * NCO_NR)); }
 __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
 #pragma clang fp contract(off)
-  __shared__ Mat2 ap[15];
   const int g = blockIdx.y;                 // uniform: (job, stream) = the recurrence
   const int q = g / P.nstreams;
   const int s = g - q * P.nstreams;
@@ -1772,23 +1701,6 @@ __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
   const int64_t len = min(pb, P.n - kb);
   if (kk0 >= len) return;                                      // uniform
   const LongBlk* B = long_blk(P, g, b);
-  const double sh = B->shift;
-  double vp = B->d[0], vv = B->d[1];
-  const bool lin = vp != 0.0 || vv != 0.0;                     // uniform
-  if (lin) {
-    if (threadIdx.x == 0) {
-      Mat2 x{1.0 - (k2Pi * (cfg.kp + cfg.ki)) * kInv2Pi, 1.0, -(k2Pi * cfg.ki) * kInv2Pi, 1.0};
-      for (int i = 0; i < 15; ++i, x = mmul(x, x)) ap[i] = x;
-    }
-    __syncthreads();
-    int e = (int)kk0 + (int)threadIdx.x + 1;                   // A^(kk+1) d, kk < pb < 2^15
-    for (int j = 0; e > 0; ++j, e >>= 1)
-      if (e & 1) {
-        const Mat2 m = ap[j];
-        const double np = m.a * vp + m.b * vv, nv = m.c * vp + m.d * vv;
-        vp = np; vv = nv;
-      }
-  }
   const double* ph = J.theta + (int64_t)s * J.th_stride;
   const double off = ph[P.n];
   const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
@@ -1807,17 +1719,9 @@ __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
   for (int i = 0; i < NCO_NR; ++i) {
     const int64_t k = k0 + (int64_t)i * 256;
     if (k >= kend) break;
-    double p = fma(sh, kP1, fma(sh, kP2, phv[i]));
-    if (lin) {
-      p = p + vp;
-      const Mat2 m = ap[8];                                    // 256 steps on: A^256
-      const double np = m.a * vp + m.b * vv, nv = m.c * vp + m.d * vv;
-      vp = np; vv = nv;
-    }
-    const double th = w * ((off + (double)k) + 1.0) + p;
-    const double a = th * cfg.scale + cfg.adj;
+    const double p = nco_phase_in(B, k - kb, J.resp, phv[i]);
     double sv, cv;
-    sincos_red<true>(reduce_2pi(a), &sv, &cv);
+    nco_value<true>(w, cfg.scale, cfg.adj, k + 1, p, off, &cv, &sv);
     oi[k] = (float)cv;
     if (oq) oq[k] = (float)sv;
   }
@@ -1835,10 +1739,9 @@ int pll_lpw(const PllJobs& P) {
   return lpw;
 }
 // a per-block call (n >= 2) is solved by pll_spec_kernel alone (its own sequential fallback):
-// no prep or loop kernel, plain (not Q-form) phase rows, and its NCO rows written by the
-// solve's own launch.  The sequential kernels run 1-sample calls.
+// no prep or loop kernel, plain (not Q-form) phase rows, and its NCO rows (when asked for,
+// P.nco_rows) written by the solve's own launch.  The sequential kernels run 1-sample calls.
 bool spec_only(const PllJobs& P) { return P.n >= 2; }
-bool nco_fused(const PllJobs& P) { return spec_only(P); }
 hipError_t pll_check(const PllJobs& P, bool* vec) {
   if (P.njobs < 1 || P.njobs > SDR_PLL_MAXJ || P.nstreams <= 0 || P.n < 0) return hipErrorInvalidValue;
   *vec = true;
@@ -1941,6 +1844,29 @@ hipError_t long_setup(PllJobs& L) {
 }
 }  // namespace
 
+bool sdr_pll_long_geom(int64_t n, int64_t* pb, int* nb) {
+  if (!long_n(n)) return false;
+  long_geom(n, pb, nb);
+  return true;
+}
+
+void sdr_pll_resp_table(const PllCfg& c, int64_t n, std::vector<double>* out) {
+  out->clear();
+  int64_t pb;
+  int nb;
+  if (!sdr_pll_long_geom(n, &pb, &nb)) return;
+  const M2 A = loop_matrix(c);
+  out->resize(2 * (size_t)(pb + 1));
+  double r0 = 1.0, r1 = 0.0;                        // row 0 of A^j, j = 0, 1, ...
+  for (int64_t j = 0; j <= pb; ++j) {
+    (*out)[2 * j] = r0;
+    (*out)[2 * j + 1] = r1;
+    const double n0 = r0 * A.a + r1 * A.c, n1 = r0 * A.b + r1 * A.d;
+    r0 = n0;
+    r1 = n1;
+  }
+}
+
 int64_t sdr_pll_work_bytes(int njobs, int nstreams, int64_t n) {
   if (!long_n(n)) return 0;
   int64_t pb;
@@ -1983,7 +1909,7 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     // when the solve cannot complete it (lpw = 0 tells the kernel so)
     L.lpw = 0;
     L.qform = 0;
-    L.nco_fused = nco_fused(P) ? 1 : 0;
+    L.nco_fused = P.nco_rows ? 1 : 0;
     const dim3 g((unsigned)(L.njobs * L.nstreams));
     if (L.n > SPEC_N256) hipLaunchKernelGGL((pll_spec_kernel<512, false>), g, dim3(512), 0, st, L);
     else hipLaunchKernelGGL((pll_spec_kernel<256, false>), g, dim3(256), 0, st, L);
@@ -2008,12 +1934,16 @@ hipError_t sdr_launch_pll_nco(const PllJobs& P, hipStream_t st) {
     e = long_setup(L);
     if (e != hipSuccess) return e;
   }
-  if (pll_long(P))
+  if (pll_long(P)) {
+    if (!P.nco_rows) return hipSuccess;                // the consumer forms the NCO (sdr_nco.h)
+    for (int q = 0; q < P.njobs; ++q)
+      if (P.j[q].resp == nullptr) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nco_long_kernel, dim3((unsigned)(L.lg.nb * nco_tiles_per_block(L.lg.pb)), (unsigned)(P.njobs * P.nstreams)),
                        dim3(256), 0, st, L);
-  else if (P.n > 0 && !nco_fused(P))                  // (fused: the solve's launch wrote the rows)
+  } else if (P.n > 0 && !spec_only(P)) {              // (spec-only: the solve's launch wrote the rows)
     hipLaunchKernelGGL(nco_jobs_kernel, dim3((unsigned)((P.n + 255) / 256), (unsigned)(P.njobs * P.nstreams)),
                        dim3(256), 0, st, L);
+  }
   return hipGetLastError();
 }
 

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "sdr_ctx.h"
+#include "sdr_nco.h"
 
 using namespace sdrint;
 
@@ -41,7 +42,9 @@ constexpr int RX_TO = RX_NT * RX_R;  // outputs per generic tile
 constexpr int RX_LDS = 6144;        // floats of LDS per workgroup (largest: 151 taps, decim 5: 5 796)
 
 enum { JK_FIR = 0, JK_RESAMPLE = 1 };
-enum { PRE_NONE = SDR_PRE_NONE, PRE_SQUARE = SDR_PRE_SQUARE, PRE_MIX = SDR_PRE_MIX };
+// PRE_NCO: the mixer of PRE_MIX whose second operand, the PLL's NCO, is formed from the PLL's
+// phase rows where the input is staged (sdr_nco.h) instead of read from an NCO row
+enum { PRE_NONE = SDR_PRE_NONE, PRE_SQUARE = SDR_PRE_SQUARE, PRE_MIX = SDR_PRE_MIX, PRE_NCO = 3 };
 
 // One filter of a stage, applied to `nstreams` streams.
 struct StageJob {
@@ -64,6 +67,8 @@ struct StageJob {
   float gain;
   int pre, D, U, kind, T, tiles;
   int small;             // D = 1 FIR: 4 outputs per lane (a launch with few tiles: more workgroups)
+  int nco_sin;           // PRE_NCO: the quadrature NCO (sin) instead of cos
+  NcoSrc nco;            // PRE_NCO: where the NCO comes from
 };
 
 // The front end's carried state, finished by the first stage launch after the FE kernel:
@@ -94,7 +99,28 @@ struct StageJobs {
 };
 
 __device__ __forceinline__ float pre_op(int pre, float x, float c, float g) {
-  return pre == PRE_SQUARE ? x * x : pre == PRE_MIX ? (x * c) * g : x;
+  return pre == PRE_SQUARE ? x * x : (pre == PRE_MIX || pre == PRE_NCO) ? (x * c) * g : x;
+}
+
+// ncoOut[k] and ncoOutQ[k] of stream s as f32 (the values the PLL's NCO rows hold, bit for bit):
+// [0] is the carried value the PLL kernel stored, [k >= 1] is formed from phaseEst_{k-1}
+__device__ __forceinline__ void nco_at(const NcoSrc& N, int s, int64_t k, float* c, float* sn) {
+  if (k == 0) {
+    *c = N.nco_i[(int64_t)s * N.out_stride];
+    *sn = N.nco_q ? N.nco_q[(int64_t)s * N.out_stride] : 0.f;
+    return;
+  }
+  const double* th = N.theta + (int64_t)s * N.th_stride;
+  const double p = nco_phase(N, s, k - 1, th[k - 1]);
+  double cv, sv;
+  nco_value(N.w, N.scale, N.adj, k, p, th[N.n], &cv, &sv);
+  *c = (float)cv;
+  *sn = (float)sv;
+}
+__device__ __forceinline__ float nco_one(const StageJob& J, int s, int64_t k) {
+  float c, sn;
+  nco_at(J.nco, s, k, &c, &sn);
+  return J.nco_sin ? sn : c;
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -134,7 +160,7 @@ struct FirShape {
   __device__ static constexpr int slot(int u) { return u < DELTA ? u : u + 2 * ((u - DELTA) / DR); }
 };
 
-template <int T, int D, int R_ = (D == 1 ? 16 : 4)>
+template <int T, int D, int R_ = (D == 1 ? 16 : 4), bool NCO = false>
 __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile, float* lds) {
   using S = FirShape<T, D, R_>;
   constexpr int R = S::R, DR = S::DR, DELTA = S::DELTA;
@@ -175,6 +201,10 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
       const int q = t + j * S::NT;
       if (q < NCH) {
         const int u = q * S::G;
+        if (NCO && pre == PRE_NCO) {                 // the NCO of these 4 inputs, from the PLL phases
+          const int64_t nn = n_lo + u;
+          cv[j] = make_float4(nco_one(J, s, nn), nco_one(J, s, nn + 1), nco_one(J, s, nn + 2), nco_one(J, s, nn + 3));
+        }
         lds[S::slot(u + 0)] = pre_op(pre, v[j].x, cv[j].x, g);
         lds[S::slot(u + 1)] = pre_op(pre, v[j].y, cv[j].y, g);
         lds[S::slot(u + 2)] = pre_op(pre, v[j].z, cv[j].z, g);
@@ -185,7 +215,8 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
     for (int u = t; u < S::LG; u += S::NT) {
       const int64_t nn = n_lo + u;
       float x = 0.f;
-      if (nn >= 0 && nn < J.n) x = pre_op(pre, xb[nn], pre == PRE_MIX ? cb[nn] : 0.f, g);
+      if (nn >= 0 && nn < J.n)
+        x = pre_op(pre, xb[nn], pre == PRE_MIX ? cb[nn] : (NCO && pre == PRE_NCO) ? nco_one(J, s, nn) : 0.f, g);
       lds[S::slot(u)] = x;
     }
   }
@@ -331,6 +362,7 @@ __device__ __forceinline__ void resample_tile(const StageJob& J, int s, int64_t 
 // lfilter final state of one (job, stream), f64, on the (zero-stuffed when U > 1) input:
 //   zf[k] = sum_{j=k+1}^{T-1} b[j] u[NU+k-j] + (NU+k < T-1 ? zi[NU+k] : 0),  NU = n*U
 // (the zf_kernel of fir.hip as extra workgroups of the producing stage).
+template <bool NCO>
 __device__ __forceinline__ void zf_block(const StageJobs& P, int64_t zb, float* lds) {
   const int q = P.zfj[zb / P.nstreams];
   const int s = (int)(zb % P.nstreams);
@@ -350,6 +382,7 @@ __device__ __forceinline__ void zf_block(const StageJobs& P, int64_t zb, float* 
     double v = (double)x[xi];
     if (J.pre == PRE_SQUARE) v = v * v;
     else if (J.pre == PRE_MIX) v = (double)((x[xi] * c[xi]) * J.gain);
+    else if (NCO && J.pre == PRE_NCO) v = (double)((x[xi] * nco_one(J, s, xi)) * J.gain);
     us[i] = v;
   }
   for (int i = threadIdx.x; i < T; i += RX_NT) bs[i] = J.taps64[i];
@@ -427,14 +460,16 @@ __device__ __forceinline__ void fe_state_block(const FeState& F, int s, float* l
 
 // One stage launch.  T > 0: every FIR job of the launch has T taps (compile-time tiles for
 // D = 1 and 5); T == 0: any tap count.  Workgroups map to (job, stream, tile) in job order,
-// then to the zf work.
-template <int T>
+// then to the zf work.  NCO: the launch has PRE_NCO jobs (stage C's mixers; T > 0 only) --
+// a separate instantiation, so the other stages keep their registers.
+template <int T, bool NCO = false>
 __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
+  static_assert(!NCO || T > 0, "PRE_NCO jobs run on the compile-time tiles");
   __shared__ __attribute__((aligned(16))) float lds[RX_LDS];
   const int64_t b = blockIdx.x;
   if (b >= P.tile_blocks) {
     const int64_t zb = b - P.tile_blocks;
-    if (zb < (int64_t)P.nzf * P.nstreams) zf_block(P, zb, lds);
+    if (zb < (int64_t)P.nzf * P.nstreams) zf_block<NCO>(P, zb, lds);
     else fe_state_block(P.fe, (int)(zb - (int64_t)P.nzf * P.nstreams), lds);
     return;
   }
@@ -451,11 +486,11 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
   }
   if constexpr (T > 0) {
     if (J.D == 1) {
-      if (J.small) fir_tile<T, 1, 4>(J, s, tile, lds);
-      else fir_tile<T, 1>(J, s, tile, lds);
+      if (J.small) fir_tile<T, 1, 4, NCO>(J, s, tile, lds);
+      else fir_tile<T, 1, 16, NCO>(J, s, tile, lds);
       return;
     }
-    if (J.D == 5) { fir_tile<T, 5>(J, s, tile, lds); return; }
+    if (J.D == 5) { fir_tile<T, 5, 4, NCO>(J, s, tile, lds); return; }
   }
   fir_tile_any(J, s, tile, lds);
 }
@@ -511,13 +546,305 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
     const int64_t grid = blocks + (int64_t)P.nzf * S + (P.fe.on ? S : 0);
     if (grid <= 0) continue;
     if (grid > 0x7fffffff) return hipErrorInvalidValue;
-    if (key == 151) hipLaunchKernelGGL(rx_stage_kernel<151>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
+    bool nco = false;
+    for (int i = 0; i < P.njobs; ++i) nco = nco || P.j[i].pre == PRE_NCO;
+    if (nco && key == 0) return hipErrorInvalidValue;     // (the receiver never asks: stage_nco_ok)
+    if (key == 151 && nco) hipLaunchKernelGGL((rx_stage_kernel<151, true>), dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
+    else if (key == 151) hipLaunchKernelGGL(rx_stage_kernel<151>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
+    else if (key == 101 && nco) hipLaunchKernelGGL((rx_stage_kernel<101, true>), dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
     else if (key == 101) hipLaunchKernelGGL(rx_stage_kernel<101>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
     else hipLaunchKernelGGL(rx_stage_kernel<0>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+// ---- RDS: I/Q mixers + 3 kHz LPF + x19 zero-stuff + anti-image LPF + [::80] x19 as ONE
+// composite polyphase filter (model/fmRDSblock.py:172-199) ------------
+// With mixed_{I,Q}[i] = 2 x[i] nco_{I,Q}[i], lpf = h * mixed (151 taps at 240 kS/s) and
+// u[19 i] = lpf[i] (zero elsewhere), the resampler's output is
+//   r[m] = 19 sum_j g[j] u[80 m - j] = 19 sum_{s} g[rho + 19 s] lpf[i0 - s],
+//   i0 = floor(80 m / 19), rho = 80 m mod 19 (only j = rho + 19 s hits a stuffed sample)
+//        = sum_{t=0}^{157} C_rho[t] x[i0 - t] nco[i0 - t],   C_rho[t] = 38 sum_s g[rho + 19 s] h[t - s]
+// -- 158 multiply-adds per output and channel where the two-stage form spends 151 per INPUT
+// (4.2 inputs per output) plus the resampler: 4x fewer.  Block starts carry the lfilter
+// states exactly: the LPF's zi enters lpf[i < 150] and the anti-image zi enters a[q < 150]
+// (the head corrections below), and one workgroup per stream writes both filters' final
+// states (the LPF's from the last 150 mixed inputs, the anti-image's from the last 8 lpf
+// values, as lfilter would).  The lpf rows themselves are only computed when asked for.
+//
+// Tile: 64 groups x 19 phases = 1 216 outputs m = m0 + 19 L + c (m0 = 1 216 tile): output
+// (c, L) reads the 158 inputs before i0 = I0 + 80 L + base_c (I0 = 80 m0 / 19, base_c =
+// floor(80 c / 19)), so group L's 19 outputs share a window of 234 inputs starting at
+// I0 + 80 L - 158.  The tile's window (5 274 inputs, I and Q mixed) is staged in LDS once;
+// lane L of wave w computes phases [5w, 5w + 5) of group L: per pair of window samples one
+// 16-B LDS read, and per phase one tap pair (a 64-bit SGPR operand, compile-time offset) and
+// two v_pk_fma_f32 (I and Q together, the tap broadcast by op_sel).  The phase's taps are
+// uniform across the wave because 80 * 19 = 4 * 19 * 20: outputs 19 apart share rho.
+constexpr int CR_U = 19, CR_D = 80, CR_T = 151;
+constexpr int CR_CT = CR_T + (CR_T - 1) / CR_U;          // 158 composite taps per phase
+constexpr int CR_G = 64, CR_NW = 4, CR_NT = 64 * CR_NW;
+constexpr int CR_TO = CR_U * CR_G;                       // outputs per tile
+constexpr int CR_IN = CR_D * CR_G;                       // inputs per tile
+__host__ __device__ constexpr int cr_base(int c) { return (CR_D * c) / CR_U; }
+constexpr int CR_LW = cr_base(CR_U - 1) + CR_CT + 1;     // 234 window pairs per group (pair 0 unused)
+constexpr int CR_NP = CR_IN - CR_D + CR_LW;              // 5 274 window pairs per tile
+// LDS float offset of window pair p: 4 pad floats after every group's 80 pairs (group stride
+// 164 floats = 41 x 16 B, odd: conflict-free 16-B reads across the lanes)
+__host__ __device__ constexpr int cr_addr(int p) { return 2 * p + 4 * (p / CR_D); }
+constexpr int CR_LDS = cr_addr(CR_NP + 1) + 4;
+__host__ __device__ constexpr int cr_c0(int w) { return 5 * w; }
+__host__ __device__ constexpr int cr_c1(int w) { return 5 * w + 5 < CR_U ? 5 * w + 5 : CR_U; }
+__host__ __device__ constexpr int cr_ulo(int w) { return (cr_base(cr_c0(w)) + 1) & ~1; }
+__host__ __device__ constexpr int cr_uhi(int w) { return cr_base(cr_c1(w) - 1) + CR_CT; }      // inclusive
+__host__ __device__ constexpr int cr_npair(int w) { return (cr_uhi(w) - cr_ulo(w)) / 2 + 1; }
+// the taps of wave w start at float cr_toff(w): [pair u2][phase c - c0][(tap at u2, at u2 + 1)]
+__host__ __device__ constexpr int cr_toff(int w) {
+  int o = 0;
+  for (int i = 0; i < w; ++i) o += cr_npair(i) * (cr_c1(i) - cr_c0(i)) * 2;
+  return o;
+}
+constexpr int CR_NTAPS = cr_toff(CR_NW);
+static_assert(cr_c1(CR_NW - 1) == CR_U && cr_uhi(CR_NW - 1) < CR_LW, "phases and window");
+static_assert((80 * CR_U) % CR_U == 0 && CR_D % 2 == 0, "16-B pair reads stay inside a group's block");
+
+struct CresJob {
+  const float* x;            // RDS extract rows (x_stride apart), M samples
+  int64_t n, x_stride;
+  NcoSrc nco;                // the RDS PLL's NCO: from its phases (theta != null) or rows
+  const float* ctaps;        // composite taps (device, CR_NTAPS floats)
+  const double* h64;         // LPF taps (f64, 151)
+  const double* g64;         // anti-image taps (f64, 151)
+  const double* zi_l[2];     // LPF I / Q lfilter state in (150 per stream, zs apart)
+  const double* zi_a[2];     // anti-image I / Q state in
+  double* zf_l[2];           // ... out
+  double* zf_a[2];
+  int64_t zs;
+  float* y[2];               // resample I / Q rows (y_stride apart), R = ceil(19 M / 80) outputs
+  float* yh[2];              // pinned host mirrors (yh_stride apart), nullable
+  int64_t y_stride, yh_stride, R;
+  int tiles, nstreams;
+};
+
+typedef const __attribute__((address_space(4))) f2a4* ctaps2c_t;
+// acc.xy += h.{lo or hi} * x.xy: the tap broadcast from a 64-bit SGPR pair by op_sel
+template <bool HI>
+__device__ __forceinline__ void pk_fma_sb(f2& acc, f2 h, f2 x) {
+  if (HI) asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(h), "v"(x));
+  else asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "s"(h), "v"(x));
+}
+
+template <int W>
+__device__ __forceinline__ void cres_fir(const float* win, const float* taps, f2 (&acc)[5]) {
+  constexpr int c0 = cr_c0(W), nc = cr_c1(W) - c0, ulo = cr_ulo(W);
+  const ctaps2c_t tw = (ctaps2c_t)(taps + cr_toff(W));
+  static_for<0, cr_npair(W)>([&](auto I) {
+    constexpr int u2 = ulo + 2 * I;
+    const float4 v = *reinterpret_cast<const float4*>(win + 2 * u2 + 4 * (u2 / CR_D));
+    static_for<0, nc>([&](auto C) {
+      constexpr int c = c0 + C;
+      constexpr bool v0 = u2 >= cr_base(c) + 1 && u2 <= cr_base(c) + CR_CT;
+      constexpr bool v1 = u2 + 1 >= cr_base(c) + 1 && u2 + 1 <= cr_base(c) + CR_CT;
+      if constexpr (v0 || v1) {
+        const f2a4 hp = tw[I * nc + C];
+        if constexpr (v0) pk_fma_sb<false>(acc[C], f2{hp.x, hp.y}, f2{v.x, v.y});
+        if constexpr (v1) pk_fma_sb<true>(acc[C], f2{hp.x, hp.y}, f2{v.z, v.w});
+      }
+    });
+  });
+}
+
+// the NCO pair of inputs i, i+1 of stream s (from the phases, or from the NCO rows)
+__device__ __forceinline__ void cres_nco2(const NcoSrc& N, int s, int64_t i, float4* cs) {
+  if (N.theta == nullptr) {
+    const float* ri = N.nco_i + (int64_t)s * N.out_stride;
+    const float* rq = N.nco_q + (int64_t)s * N.out_stride;
+    *cs = make_float4(ri[i], rq[i], ri[i + 1], rq[i + 1]);
+    return;
+  }
+  nco_at(N, s, i, &cs->x, &cs->y);
+  nco_at(N, s, i + 1, &cs->z, &cs->w);
+}
+
+// final states of one stream: the LPF's (I, Q) from the last 150 mixed inputs and the
+// anti-image filter's from the last 8 lpf values (f32, as the lpf rows hold them), each as
+// rx.hip's zf_block computes it (on the x19 stream for the anti-image)
+__device__ void cres_zf_block(const CresJob& J, int s, float* lds) {
+  constexpr int T = CR_T, L8 = (CR_T - 1) / CR_U + 1;      // 8 lpf values
+  constexpr int NM = T - 1 + L8;                             // 158 mixed inputs
+  double* mx = reinterpret_cast<double*>(lds);               // mx[ch][i] = mixed_ch[n-1-i]
+  double* hs = mx + 2 * NM;
+  double* gs = hs + T;
+  double* lp = gs + T;                                       // lp[ch][i] = lpf_ch[n-1-i]
+  const int t = threadIdx.x;
+  const int64_t n = J.n;
+  const float* x = J.x + (int64_t)s * J.x_stride;
+  for (int i = t; i < NM; i += CR_NT) {
+    const int64_t xi = n - 1 - i;
+    double vi = 0.0, vq = 0.0;
+    if (xi >= 0) {
+      float c, sn;
+      if (J.nco.theta) nco_at(J.nco, s, xi, &c, &sn);
+      else { c = J.nco.nco_i[(int64_t)s * J.nco.out_stride + xi]; sn = J.nco.nco_q[(int64_t)s * J.nco.out_stride + xi]; }
+      vi = (double)((x[xi] * c) * 2.0f);                     // the mixer (fmRDSblock.py:173-176)
+      vq = (double)((x[xi] * sn) * 2.0f);
+    }
+    mx[i] = vi;
+    mx[NM + i] = vq;
+  }
+  for (int i = t; i < T; i += CR_NT) { hs[i] = J.h64[i]; gs[i] = J.g64[i]; }
+  __syncthreads();
+  // the LPF's final states, and the last 8 lpf values
+  for (int w = t; w < 2 * (T - 1) + 2 * L8; w += CR_NT) {
+    const int ch = w < 2 * (T - 1) ? w / (T - 1) : (w - 2 * (T - 1)) / L8;
+    const double* m = mx + ch * NM;
+    const double* zi = J.zi_l[ch] + (int64_t)s * J.zs;
+    if (w < 2 * (T - 1)) {
+      const int k = w - ch * (T - 1);
+      const int jhi = (int)min<int64_t>(T - 1, n + k);
+      double a0 = 0.0, a1 = 0.0;
+      int j = k + 1;
+      for (; j + 1 <= jhi; j += 2) {
+        a0 = fma(hs[j], m[j - k - 1], a0);
+        a1 = fma(hs[j + 1], m[j - k], a1);
+      }
+      if (j <= jhi) a0 = fma(hs[j], m[j - k - 1], a0);
+      double acc = a0 + a1;
+      if (n + k < T - 1) acc += zi[n + k];
+      J.zf_l[ch][(int64_t)s * J.zs + k] = acc;
+    } else {
+      const int i = w - 2 * (T - 1) - ch * L8;                // lpf[n-1-i]
+      const int64_t li = n - 1 - i;
+      double acc = 0.0;
+      if (li >= 0) {
+        for (int k = 0; k < T && i + k < NM && li - k >= 0; ++k) acc = fma(hs[k], m[i + k], acc);
+        if (li < T - 1) acc += zi[li];
+      }
+      lp[ch * L8 + i] = (double)(float)acc;
+    }
+  }
+  __syncthreads();
+  // the anti-image filter's final states: zf[k] = sum_{m >= 1, k + 19 m <= 150} g[k + 19 m] lpf[n - m]
+  const int64_t nu = n * CR_U;
+  for (int w = t; w < 2 * (T - 1); w += CR_NT) {
+    const int ch = w / (T - 1), k = w - ch * (T - 1);
+    double acc = 0.0;
+    for (int m = 1; k + CR_U * m <= T - 1 && m <= n; ++m) acc = fma(gs[k + CR_U * m], lp[ch * L8 + m - 1], acc);
+    if (nu + k < T - 1) acc += J.zi_a[ch][(int64_t)s * J.zs + nu + k];
+    J.zf_a[ch][(int64_t)s * J.zs + k] = acc;
+  }
+}
+
+__global__ __launch_bounds__(CR_NT) void rx_cres_kernel(CresJob J) {
+  __shared__ __attribute__((aligned(16))) float lds[CR_LDS];
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  if (b >= J.tiles * J.nstreams) {
+    cres_zf_block(J, b - J.tiles * J.nstreams, lds);
+    return;
+  }
+  const int s = b / J.tiles;
+  const int64_t tile = b - (int64_t)s * J.tiles;
+  const int64_t I0 = tile * CR_IN, ws = I0 - (CR_CT + 0);   // window pair p <-> input ws + p
+  const float* x = J.x + (int64_t)s * J.x_stride;
+  const int64_t n = J.n;
+  // stage the window: pairs (2j, 2j + 1) per chunk j, mixed I and Q (the gain 2 is in the taps)
+  constexpr int NCHK = (CR_NP + 1) / 2, NR = (NCHK + CR_NT - 1) / CR_NT;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int j = t + r * CR_NT;
+    if (j < NCHK) {
+      const int64_t i = ws + 2 * j;
+      float2 xv;
+      float4 cs;
+      if (i >= 0 && i + 1 < n) {
+        xv = *reinterpret_cast<const float2*>(x + i);
+        cres_nco2(J.nco, s, i, &cs);
+      } else {
+        xv = make_float2(0.f, 0.f);
+        cs = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i >= 0 && i < n) {
+          xv.x = x[i];
+          if (J.nco.theta) nco_at(J.nco, s, i, &cs.x, &cs.y);
+          else { cs.x = J.nco.nco_i[(int64_t)s * J.nco.out_stride + i]; cs.y = J.nco.nco_q[(int64_t)s * J.nco.out_stride + i]; }
+        }
+      }
+      *reinterpret_cast<float4*>(lds + cr_addr(2 * j)) = make_float4(xv.x * cs.x, xv.x * cs.y, xv.y * cs.z, xv.y * cs.w);
+    }
+  }
+  __syncthreads();
+  const int w = t >> 6, L = t & 63;
+  const float* win = lds + (2 * CR_D + 4) * L;
+  f2 acc[5];
+#pragma unroll
+  for (int c = 0; c < 5; ++c) acc[c] = f2{0.f, 0.f};
+  if (w == 0) cres_fir<0>(win, J.ctaps, acc);
+  else if (w == 1) cres_fir<1>(win, J.ctaps, acc);
+  else if (w == 2) cres_fir<2>(win, J.ctaps, acc);
+  else cres_fir<3>(win, J.ctaps, acc);
+  const int c0 = cr_c0(w), nc = cr_c1(w) - c0;
+  const int64_t m0 = tile * CR_TO + (int64_t)CR_U * L;
+#pragma unroll
+  for (int C = 0; C < 5; ++C) {
+    if (C >= nc) break;
+    const int c = c0 + C;
+    const int64_t m = m0 + c;
+    if (m >= J.R) continue;
+    float yi = acc[C].x, yq = acc[C].y;
+    const int64_t i0 = (CR_D * m) / CR_U;
+    if (i0 < CR_CT - 1 || CR_D * m < CR_T - 1) {
+      // block head: the LPF's zi (in lpf[i < 150]) and the anti-image zi (in a[q < 150])
+      const int rho = (int)(CR_D * m - (int64_t)CR_U * i0);
+      double ci = 0.0, cq = 0.0;
+      for (int ss = 0; rho + CR_U * ss <= CR_T - 1; ++ss) {
+        const int64_t li = i0 - ss;
+        if (li >= 0 && li < CR_T - 1) {
+          ci = fma(J.g64[rho + CR_U * ss], J.zi_l[0][(int64_t)s * J.zs + li], ci);
+          cq = fma(J.g64[rho + CR_U * ss], J.zi_l[1][(int64_t)s * J.zs + li], cq);
+        }
+      }
+      if (CR_D * m < CR_T - 1) {
+        ci += J.zi_a[0][(int64_t)s * J.zs + CR_D * m];
+        cq += J.zi_a[1][(int64_t)s * J.zs + CR_D * m];
+      }
+      yi += (float)(CR_U * ci);
+      yq += (float)(CR_U * cq);
+    }
+    J.y[0][(int64_t)s * J.y_stride + m] = yi;
+    J.y[1][(int64_t)s * J.y_stride + m] = yq;
+    if (J.yh[0]) J.yh[0][(int64_t)s * J.yh_stride + m] = yi;
+    if (J.yh[1]) J.yh[1][(int64_t)s * J.yh_stride + m] = yq;
+  }
+}
+
+// the composite taps (host, f64 then f32) in the kernel's order; empty unless both filters
+// have CR_T taps
+void cres_taps(const std::vector<double>& h, const std::vector<double>& g, std::vector<float>* out) {
+  out->clear();
+  if ((int)h.size() != CR_T || (int)g.size() != CR_T) return;
+  std::vector<double> C((size_t)CR_U * CR_CT, 0.0);            // C[rho][t]
+  for (int rho = 0; rho < CR_U; ++rho)
+    for (int ss = 0; rho + CR_U * ss < CR_T; ++ss)
+      for (int k = 0; k < CR_T; ++k) C[(size_t)rho * CR_CT + ss + k] += g[rho + CR_U * ss] * h[k];
+  out->assign(CR_NTAPS, 0.f);
+  auto tap = [&](int c, int u) -> float {
+    const int tt = cr_base(c) + CR_CT - u;
+    if (tt < 0 || tt >= CR_CT) return 0.f;
+    const int rho = CR_D * c - CR_U * cr_base(c);
+    return (float)(2.0 * CR_U * C[(size_t)rho * CR_CT + tt]);
+  };
+  for (int w = 0; w < CR_NW; ++w) {
+    const int c0 = cr_c0(w), nc = cr_c1(w) - c0;
+    for (int I = 0; I < cr_npair(w); ++I) {
+      const int u2 = cr_ulo(w) + 2 * I;
+      for (int C2 = 0; C2 < nc; ++C2) {
+        const int o = cr_toff(w) + (I * nc + C2) * 2;
+        (*out)[o] = tap(c0 + C2, u2);
+        (*out)[o + 1] = tap(c0 + C2, u2 + 1);
+      }
+    }
+  }
 }
 
 // state-bank slots (f64 lfilter states, T-1 per stream each)
@@ -591,6 +918,13 @@ struct sdr_rx {
   int pq_head = 0, pq_n = 0;
   bool timing = false;                 // events between the stages of each block
   hipEvent_t ev[SDR_RX_NSTAGES + 1] = {};
+  // outputs process_dev materialises (sdr_rx_set_keep; bit o = SDR_RX_O_o): the NCO rows and
+  // the RDS LPF rows are intermediates the chain does not need (the mixers form the NCO from
+  // the PLL phases, the RDS LPF runs inside the composite resampler)
+  uint64_t keep = ~0ull;
+  uint64_t keep_now = ~0ull;           // this call's (sdr_rx_submit: what it was asked for)
+  bool made[SDR_RX_NOUTPUTS] = {};     // what the latest block materialised
+  float* ctaps = nullptr;              // the composite RDS taps (rx_cres_kernel), device; null: two-stage path
 };
 
 namespace {
@@ -708,6 +1042,14 @@ int rx_finalize(sdr_rx* r) {
   r->theta = r->pll_state[1] + 6 * S2;
   r->pllc = r->theta + nsets * 2 * S * r->ths;
   r->pllw = reinterpret_cast<char*>(round_up((int64_t)(uintptr_t)(r->pllc + nsets * 2 * S * r->cst), 256));
+  if ((r->flags & SDR_RX_RDS) && r->rds_up == CR_U && r->rds_down == CR_D) {
+    std::vector<float> ct;
+    cres_taps(r->taps[SDR_RX_F_RDS_LPF], r->taps[SDR_RX_F_RDS_ANTI], &ct);
+    if (!ct.empty()) {
+      HIP_TRY(hipMalloc(&r->ctaps, sizeof(float) * ct.size()));
+      HIP_TRY(hipMemcpy(r->ctaps, ct.data(), sizeof(float) * ct.size(), hipMemcpyHostToDevice));
+    }
+  }
   r->ready = true;
   return sdr_rx_reset(r);
 }
@@ -746,6 +1088,7 @@ void sdr_rx_destroy(sdr_rx* r) {
     (void)hipStreamSynchronize(r->c->stream);
   }
   if (r->mem) (void)hipFree(r->mem);
+  if (r->ctaps) (void)hipFree(r->ctaps);
   if (r->pin_in) (void)hipHostFree(r->pin_in);
   if (r->pin_out) (void)hipHostFree(r->pin_out);
   for (hipEvent_t e : r->ev)
@@ -933,6 +1276,17 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   // and constant rows alternate with the row set; set q is free once block k-2's back half
   // (which waited for its recurrence) is done.
   const bool plls = stx || rd;
+  // What this block materialises beyond what the chain needs (sdr_rx_set_keep / the outputs a
+  // submit asks for): the NCO rows, and the RDS LPF rows.  Without them the stage-C mixers
+  // form the NCO from the PLL phase rows where they stage their inputs (PRE_NCO, sdr_nco.h) and
+  // the RDS LPF + resampler is the composite filter (rx_cres_kernel), which runs either way.
+  auto kept = [&](int o) { return (r->keep_now >> o) & 1ull; };
+  const bool cres = rd && r->ctaps != nullptr;
+  const int tsl = stx ? (int)r->taps[SDR_RX_F_STEREO_LPF].size() : 151;
+  const bool tiles_ok = (tsl == 101 || tsl == 151) && (r->audio_decim == 1 || r->audio_decim == 5);   // PRE_NCO tiles
+  const bool nco_rows = (stx && kept(SDR_RX_O_STEREO_NCO)) || (rd && (kept(SDR_RX_O_RDS_NCO_I) || kept(SDR_RX_O_RDS_NCO_Q))) ||
+                        M < 2 || (rd && !cres) || !tiles_ok;
+  const bool lpf_rows = rd && (!cres || kept(SDR_RX_O_RDS_LPF_I) || kept(SDR_RX_O_RDS_LPF_Q));
   // The recurrences get a stream of their own (block k's beside block k-1's NCO and stages
   // C-E) whenever the receiver is pipelined.  Round 4 kept a few per-block recurrences (c4:
   // one, ~26 us) on the back stream, where each cross-stream hop then cost more than the
@@ -942,23 +1296,49 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   const bool mid = r->pipe;
   hipStream_t ps = mid ? r->mid : st;
   PllJobs P{};
+  NcoSrc nsrc[2] = {};                 // per PLL (0 stereo, 1 RDS): where stage C takes its NCO from
   if (plls) {
     P.nstreams = S;
     P.n = M;
     P.stats = c->pll_stats;
+    P.nco_rows = nco_rows ? 1 : 0;
     P.work = r->pllw_bytes ? r->pllw + (int64_t)q * r->pllw_bytes : nullptr;
     double* th = r->theta + (int64_t)q * 2 * S * r->ths;
     double* pc = r->pllc + (int64_t)q * 2 * S * r->cst;
     const double off = (double)M * (double)r->blocks;
-    if (stx) {
-      P.j[P.njobs++] = PllJob{o[SDR_RX_O_BPF_RECOVERY], ms, r->pll_state[0], th, r->ths,
-                              o[SDR_RX_O_STEREO_NCO], nullptr, ms, r->pll[0], pc, r->cst, off, 1};
-    }
-    if (rd) {
-      P.j[P.njobs++] = PllJob{o[SDR_RX_O_RDS_PRE_PLL], ms, r->pll_state[1], th + (int64_t)S * r->ths, r->ths,
-                              o[SDR_RX_O_RDS_NCO_I], o[SDR_RX_O_RDS_NCO_Q], ms, r->pll[1],
-                              pc + (int64_t)S * r->cst, r->cst, off, 1};
-    }
+    int64_t pb = 0;
+    int nb = 0;
+    const bool lng = sdr_pll_long_geom(M, &pb, &nb);
+    auto add = [&](int k, const float* in, double* thk, float* ni, float* nq, double* pck) -> int {
+      const double* resp = nullptr;
+      TRY(get_resp(c, r->pll[k], M, &resp));
+      const int jq = P.njobs;
+      P.j[P.njobs++] = PllJob{in, ms, r->pll_state[k], thk, r->ths, ni, nq, ms, r->pll[k], pck, r->cst, off, 1, resp};
+      NcoSrc& N = nsrc[k];
+      N.theta = nco_rows ? nullptr : thk;
+      N.th_stride = r->ths;
+      N.nco_i = ni;
+      N.nco_q = nq;
+      N.out_stride = ms;
+      N.w = 2.0 * M_PI * (r->pll[k].freq / r->pll[k].fs);
+      N.scale = r->pll[k].scale;
+      N.adj = r->pll[k].adj;
+      N.n = M;
+      if (lng) {
+        N.blk = long_blk0(P.work, 0, S, nb, jq * S);        // njobs fixed up below
+        N.blk_stride = nb;
+        N.pb = pb;
+        N.resp = resp;
+      }
+      return SDR_OK;
+    };
+    if (stx) TRY(add(0, o[SDR_RX_O_BPF_RECOVERY], th, o[SDR_RX_O_STEREO_NCO], nullptr, pc));
+    if (rd) TRY(add(1, o[SDR_RX_O_RDS_PRE_PLL], th + (int64_t)S * r->ths, o[SDR_RX_O_RDS_NCO_I], o[SDR_RX_O_RDS_NCO_Q],
+                    pc + (int64_t)S * r->cst));
+    if (lng)                                                // the records follow P.njobs x S headers
+      for (NcoSrc& N : nsrc)
+        if (N.blk) N.blk = reinterpret_cast<const LongBlk*>(reinterpret_cast<const char*>(N.blk) +
+                                                              (int64_t)P.njobs * S * sizeof(LongHdr));
     HIP_TRY(sdr_launch_pll_prep(P, fs));
   }
   if (r->pipe) {
@@ -977,7 +1357,17 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     HIP_TRY(hipStreamWaitEvent(st, r->ev_mid[q], 0));
   }
   if (plls) HIP_TRY(sdr_launch_pll_nco(P, st));
-  // stage C: mixers + LPFs; the stereo LPF's store also forms L and R
+  // stage C: the stereo mixer + LPF (its store also forms L and R); the RDS I/Q mixer + LPF
+  // rows only when they are kept (or without the composite filter)
+  auto mixer = [&](StageJob j, int k, int sin_) {
+    if (nsrc[k].theta != nullptr && (j.T == 101 || j.T == 151) && (j.D == 1 || j.D == 5)) {
+      j.pre = PRE_NCO;
+      j.nco = nsrc[k];
+      j.nco_sin = sin_;
+      j.c = nullptr;
+    }
+    return j;
+  };
   std::vector<StageJob> C;
   if (stx) {
     StageJob j = fir(SDR_RX_F_STEREO_LPF, Z_SLPF, o[SDR_RX_O_BPF_EXTRACTION], M, ms, o[SDR_RX_O_STEREO], as,
@@ -988,28 +1378,60 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     j.lh = r->mirror[SDR_RX_O_LEFT];
     j.rh = r->mirror[SDR_RX_O_RIGHT];
     j.yh_stride = r->out_n[SDR_RX_O_STEREO];                                    // == out_n of L and R
-    C.push_back(j);
+    C.push_back(mixer(j, 0, 0));
   }
-  if (rd) {                                                                     // fmRDSblock.py:173-182
-    C.push_back(fir(SDR_RX_F_RDS_LPF, Z_RLPF_I, o[SDR_RX_O_RDS_EXTRACT], M, ms, o[SDR_RX_O_RDS_LPF_I], ms, 1, PRE_MIX,
-                    o[SDR_RX_O_RDS_NCO_I]));
-    C.push_back(fir(SDR_RX_F_RDS_LPF, Z_RLPF_Q, o[SDR_RX_O_RDS_EXTRACT], M, ms, o[SDR_RX_O_RDS_LPF_Q], ms, 1, PRE_MIX,
-                    o[SDR_RX_O_RDS_NCO_Q]));
+  if (lpf_rows) {                                                              // fmRDSblock.py:173-182
+    for (int k = 0; k < 2; ++k) {
+      StageJob j = fir(SDR_RX_F_RDS_LPF, k ? Z_RLPF_Q : Z_RLPF_I, o[SDR_RX_O_RDS_EXTRACT], M, ms,
+                       o[k ? SDR_RX_O_RDS_LPF_Q : SDR_RX_O_RDS_LPF_I], ms, 1, PRE_MIX,
+                       o[k ? SDR_RX_O_RDS_NCO_Q : SDR_RX_O_RDS_NCO_I]);
+      if (cres) j.zf = nullptr;                 // the composite kernel writes the LPF's final states
+      C.push_back(mixer(j, 1, k));
+    }
   }
   HIP_TRY(launch_stage(C, S, st));
   HIP_TRY(mark(1 + SDR_RX_ST_C, st));
   if (rd) {
-    // stage D: rational resamplers (fmRDSblock.py:184-199)
     const int64_t rs = r->out_stride[SDR_RX_O_RDS_RES_I];
-    std::vector<StageJob> Dj;
-    for (int k = 0; k < 2; ++k) {
-      StageJob j = fir(SDR_RX_F_RDS_ANTI, k ? Z_ANTI_Q : Z_ANTI_I, o[k ? SDR_RX_O_RDS_LPF_Q : SDR_RX_O_RDS_LPF_I], M, ms,
-                       o[k ? SDR_RX_O_RDS_RES_Q : SDR_RX_O_RDS_RES_I], rs, r->rds_down);
-      j.kind = JK_RESAMPLE;
-      j.U = r->rds_up;
-      Dj.push_back(j);
+    if (cres) {
+      // stage D: the RDS mixers + LPF + x19 / 80 resampler as one composite filter, and the
+      // LPF's and anti-image filter's final states
+      CresJob J{};
+      J.x = o[SDR_RX_O_RDS_EXTRACT];
+      J.n = M;
+      J.x_stride = ms;
+      J.nco = nsrc[1];
+      J.ctaps = r->ctaps;
+      J.h64 = ts[SDR_RX_F_RDS_LPF]->dev_f64;
+      J.g64 = ts[SDR_RX_F_RDS_ANTI]->dev_f64;
+      J.zi_l[0] = zin(Z_RLPF_I); J.zi_l[1] = zin(Z_RLPF_Q);
+      J.zi_a[0] = zin(Z_ANTI_I); J.zi_a[1] = zin(Z_ANTI_Q);
+      J.zf_l[0] = zout(Z_RLPF_I); J.zf_l[1] = zout(Z_RLPF_Q);
+      J.zf_a[0] = zout(Z_ANTI_I); J.zf_a[1] = zout(Z_ANTI_Q);
+      J.zs = r->zlen[Z_RLPF_I];
+      J.y[0] = o[SDR_RX_O_RDS_RES_I]; J.y[1] = o[SDR_RX_O_RDS_RES_Q];
+      J.yh[0] = r->mirror[SDR_RX_O_RDS_RES_I]; J.yh[1] = r->mirror[SDR_RX_O_RDS_RES_Q];
+      J.y_stride = rs;
+      J.yh_stride = r->out_n[SDR_RX_O_RDS_RES_I];
+      J.R = r->R;
+      J.tiles = (int)ceil_div(r->R, CR_TO);
+      J.nstreams = S;
+      const int64_t grid = (int64_t)J.tiles * S + S;
+      if (grid > 0x7fffffff || r->zlen[Z_ANTI_I] != J.zs) return fail(SDR_EINVAL, "sdr_rx: composite RDS geometry");
+      hipLaunchKernelGGL(rx_cres_kernel, dim3((unsigned)grid), dim3(CR_NT), 0, st, J);
+      HIP_TRY(hipGetLastError());
+    } else {
+      // stage D: rational resamplers (fmRDSblock.py:184-199)
+      std::vector<StageJob> Dj;
+      for (int k = 0; k < 2; ++k) {
+        StageJob j = fir(SDR_RX_F_RDS_ANTI, k ? Z_ANTI_Q : Z_ANTI_I, o[k ? SDR_RX_O_RDS_LPF_Q : SDR_RX_O_RDS_LPF_I], M, ms,
+                         o[k ? SDR_RX_O_RDS_RES_Q : SDR_RX_O_RDS_RES_I], rs, r->rds_down);
+        j.kind = JK_RESAMPLE;
+        j.U = r->rds_up;
+        Dj.push_back(j);
+      }
+      HIP_TRY(launch_stage(Dj, S, st));
     }
-    HIP_TRY(launch_stage(Dj, S, st));
     HIP_TRY(mark(1 + SDR_RX_ST_D, st));
     // stage E: RRC (fmRDSblock.py:202-204)
     HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_RRC, Z_RRC_I, o[SDR_RX_O_RDS_RES_I], r->R, rs, o[SDR_RX_O_RDS_RRC_I], rs, 1),
@@ -1017,6 +1439,11 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
                          S, st));
   } else {
     HIP_TRY(mark(1 + SDR_RX_ST_D, st));
+  }
+  for (int oo = 0; oo < SDR_RX_NOUTPUTS; ++oo) {
+    const bool nco_o = oo == SDR_RX_O_STEREO_NCO || oo == SDR_RX_O_RDS_NCO_I || oo == SDR_RX_O_RDS_NCO_Q;
+    const bool lpf_o = oo == SDR_RX_O_RDS_LPF_I || oo == SDR_RX_O_RDS_LPF_Q;
+    r->made[oo] = need_out(r, oo) && (!nco_o || nco_rows) && (!lpf_o || lpf_rows);
   }
   HIP_TRY(mark(1 + SDR_RX_ST_E, st));
   if (r->pipe) HIP_TRY(hipEventRecord(r->ev_back[q], st));
@@ -1133,7 +1560,12 @@ int sdr_rx_submit(sdr_rx* r, const void* iq_host, int64_t iq_stride, int nout, c
   float* pout = r->pin_out + (size_t)slot * r->out_slot / sizeof(float);
   std::memcpy(pin, iq_host, bytes);
   for (int o = 0; o < SDR_RX_NOUTPUTS; ++o) r->mirror[o] = want[o] && stage_output(o) ? pout + P.region[o] : nullptr;
+  uint64_t wmask = 0;                                     // materialise what this call returns
+  for (int o = 0; o < SDR_RX_NOUTPUTS; ++o)
+    if (want[o]) wmask |= 1ull << o;
+  r->keep_now = wmask;
   const int rc = sdr_rx_process_dev(r, pin, xs);
+  r->keep_now = r->keep;
   for (float*& m : r->mirror) m = nullptr;
   TRY(rc);
   bool copied = false;
@@ -1205,10 +1637,18 @@ int sdr_rx_output(sdr_rx* r, int which, float** dev, int64_t* stride, int64_t* n
   return SDR_OK;
 }
 
+int sdr_rx_set_keep(sdr_rx* r, uint64_t mask) {
+  if (r == nullptr) return fail(SDR_EINVAL, "sdr_rx is NULL");
+  r->keep = r->keep_now = mask;
+  return SDR_OK;
+}
+
 int sdr_rx_fetch(sdr_rx* r, int which, float* host, int64_t host_stride) {
   float* d;
   int64_t ds, n;
   TRY(sdr_rx_output(r, which, &d, &ds, &n));
+  if (!r->made[which])
+    return fail(SDR_EINVAL, "sdr_rx_fetch: output %d was not materialised by the latest block (sdr_rx_set_keep)", which);
   if (host == nullptr) return fail(SDR_EINVAL, "sdr_rx_fetch: host is NULL");
   if (r->S > 1 && host_stride < n) return fail(SDR_EINVAL, "sdr_rx_fetch: host_stride %lld < %lld", (long long)host_stride, (long long)n);
   TRY(set_dev(r->c));

@@ -29,6 +29,13 @@ struct TapSet {
   int* dev_afr = nullptr;     // T = 101 / 151: the u8 MFMA front end's A fragments (fe_mfma.hip)
 };
 
+// a PLL loop's response table on the device (sdr_pll_resp_table), per (Kp, Ki, pseudo-block length)
+struct RespTable {
+  double kp = 0.0, ki = 0.0;
+  int64_t pb = 0;
+  double* dev = nullptr;
+};
+
 // the calling thread's last error message; returns `code`
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
@@ -43,6 +50,8 @@ struct sdr_ctx {
   // is spliced to the back and an overflow evicts the front, so no pointer handed out by
   // a lookup is invalidated by the other lookups of the same entry point (<= 4 per call).
   std::list<sdrint::TapSet> taps;
+  // PLL response tables of the long calls made on the context (a few loops; never evicted)
+  std::list<sdrint::RespTable> resp;
   // PLL solve counters (SDR_PLL_NSTATS, device; sdr_pll_stats): every PLL launch of the
   // context and of its receivers adds to them
   unsigned long long* pll_stats = nullptr;
@@ -56,6 +65,10 @@ int scratch(sdr_ctx* c, Slot s, size_t bytes, void** out);
 // device copies (f32, f64) of the tap set b[0..T) (cached per context).  max_T: SDR_MAX_TAPS
 // for the FIR kernels, up to SDR_MAX_RESAMPLE_TAPS for the resampler.
 int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T = SDR_MAX_TAPS);
+
+// the device response table of loop cfg for a long call of n steps (cached per context);
+// *out = NULL when n is not a long call
+int get_resp(sdr_ctx* c, const PllCfg& cfg, int64_t n, const double** out);
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -99,6 +99,7 @@ struct PllJob {
   const float* in; int64_t in_stride; double* state; double* theta; int64_t th_stride;
   float* nco_i; float* nco_q; int64_t out_stride; PllCfg cfg; double* cbuf; int64_t c_stride;
   double off; int off_given;   // the prep kernel's trigOffset, when not read from state[5]
+  const double* resp;          // long calls: the loop's response table (sdr_pll_resp_table), device
 };
 // Long calls (n > SDR_PLL_BLOCK_MAX samples): the recurrence is cut into nb pseudo-blocks of
 // pb samples, solved in parallel from warm-up guesses of their start states and chained
@@ -115,12 +116,19 @@ struct PllJobs {
   PllJob j[SDR_PLL_MAXJ]; int njobs; int nstreams; int64_t n;
   int lpw; int qform;                  // set by the launchers
   int nco_fused;                       // per-block spec-only calls: the solve's launch writes the NCO rows
+  int nco_rows;                        // 0: write only each NCO row's [0] (the carried value) and leave the
+                                       //   rest to the consumer (the receiver's mixers, sdr_nco.h); 1: whole rows
   unsigned long long* stats;           // device counters (SDR_PLL_NSTATS, include/sdr.h), nullable
   void* work;                          // long calls: sdr_pll_work_bytes() of device scratch
   PllLong lg;                          // long calls: set by the launcher
 };
 // device scratch a long call needs (0 when n <= SDR_PLL_BLOCK_MAX)
 int64_t sdr_pll_work_bytes(int njobs, int nstreams, int64_t n);
+// a long call of n steps: its pseudo-block length and count (false: not a long call)
+bool sdr_pll_long_geom(int64_t n, int64_t* pb, int* nb);
+// the loop's response table for a long call of n steps: 2 (pb + 1) doubles, row 0 of A^j for
+// j = 0 .. pb (sdr_nco.h); empty when n is not a long call
+void sdr_pll_resp_table(const PllCfg& c, int64_t n, std::vector<double>* out);
 // prep (per-sample constants) -> loop (one lane per recurrence) -> NCO; the three launches
 // separately (the receiver puts them on different streams) or together
 hipError_t sdr_launch_pll_prep(const PllJobs& jobs, hipStream_t st);

@@ -1,0 +1,149 @@
+// The NCO of fmPll (model/fmPll.py:33-37) as a function of the PLL's stored phase rows, shared
+// by the PLL kernels (pll.hip: NCO rows, when an output asks for them) and the receiver's mixer
+// stage (rx.hip: the mixers form cos / sin of the PLL phase where they stage their inputs, so a
+// block's NCO never round-trips through HBM -- VERDICT r04 item 2).
+//
+//   th_k   = 2 pi (freq / Fs) (trigOffset + k + 1) + phaseEst_k        (fmPll.py:33)
+//   nco[k+1] = cos(th_k scale + adj),  ncoQ[k+1] = sin(th_k scale + adj)  (:36-37)
+//   nco[0] = the previous call's last value (the carried state)
+//
+// Per-block calls store phaseEst_k itself.  Long calls (spans) store each pseudo-block's own
+// solve: the recurrence's phase is that + 2 pi x the chain's whole turns for the block + the
+// loop's linear response (A^(kk+1) d)_phase to the start error d the chain accepted it with (kk:
+// the step within the pseudo-block).  The response row of A^(kk+1) is a table built once per
+// loop (PllResp), so every consumer forms the same double.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sdr_launch.h"
+
+namespace sdrnco {
+
+// 2*pi split into three parts (Cody-Waite), so n*P1 and n*P2 are exact for |n| < 2^26.
+constexpr double kP1 = 6.2831854820251465;       // float32(2 pi), 24 significant bits
+constexpr double kP2 = -1.748455600074497e-07;    // double(2 pi - kP1)
+constexpr double kP3 = -1.0687562935444062e-23;   // remainder
+constexpr double kInv2Pi = 0.15915494309189535;
+constexpr double kPi = 3.14159265358979323846;
+constexpr double k2Pi = 6.28318530717958647692;
+
+// r = a - 2*pi*n, n = rint(a / 2pi), |r| <= pi (up to one ulp at the boundary).
+__device__ inline double reduce_2pi(double a) {
+  const double n = rint(a * kInv2Pi);
+  double r = fma(-n, kP1, a);
+  r = fma(-n, kP2, r);
+  r = fma(-n, kP3, r);
+  return r;
+}
+
+// sin and cos of a reduced angle |a| <= pi (+ an ulp), for the NCO outputs (f32: 6e-8 is their
+// rounding): quadrant n = rint(a 2/pi) (a two-part pi/2: exact to ~1e-32 for |n| <= 2), then
+// Taylor polynomials on |y| <= pi/4 to y^13 / y^14 (truncation < 3e-14).  ~35 VALU against
+// the library sincos's general-argument path.
+// OPAQUE: each coefficient is made an SGPR at its use (a volatile asm): in kernels that call
+// this once per call (end states) the compiler otherwise keeps all 14 in VGPRs for the whole
+// kernel, which spilled the long-call fix kernel
+template <bool OPAQUE = false>
+__device__ __forceinline__ void sincos_red(double a, double* sv, double* cv) {
+  auto K = [](double c) {
+    if constexpr (OPAQUE) asm volatile("" : "+s"(c));
+    return c;
+  };
+  constexpr double kPio2Hi = 1.5707963267948966, kPio2Lo = 6.123233995736766e-17, k2oPi = 0.6366197723675814;
+  const double n = rint(a * k2oPi);
+  double y = fma(-n, kPio2Hi, a);
+  y = fma(-n, kPio2Lo, y);
+  const double z = y * y;
+  double ps = K(1.0 / 6227020800.0);                        // 1/13!
+  ps = fma(ps, z, K(-1.0 / 39916800.0));
+  ps = fma(ps, z, K(1.0 / 362880.0));
+  ps = fma(ps, z, K(-1.0 / 5040.0));
+  ps = fma(ps, z, K(1.0 / 120.0));
+  ps = fma(ps, z, K(-1.0 / 6.0));
+  const double sn = fma(ps * z, y, y);
+  double pc = K(1.0 / 87178291200.0);                       // 1/14!
+  pc = fma(pc, z, K(-1.0 / 479001600.0));
+  pc = fma(pc, z, K(1.0 / 3628800.0));
+  pc = fma(pc, z, K(-1.0 / 40320.0));
+  pc = fma(pc, z, K(1.0 / 720.0));
+  pc = fma(pc, z, K(-1.0 / 24.0));
+  pc = fma(pc, z, K(0.5));
+  const double cs = fma(-pc, z, 1.0);
+  const int q = (int)n & 3;
+  const double s0 = (q & 1) ? cs : sn, c0 = (q & 1) ? sn : cs;
+  *sv = (q == 2 || q == 3) ? -s0 : s0;
+  *cv = (q == 1 || q == 2) ? -c0 : c0;
+}
+
+}  // namespace sdrnco
+
+// ---- long calls: pseudo-block bookkeeping (device scratch PllJobs::work) --------------
+// Per recurrence r = job * nstreams + stream: a header (the chain's position and the exact
+// state at it), then one LongBlk per pseudo-block: its start guess g (warm-up), its chained
+// start x (when re-solved), the end state e of its latest solve, the 2 pi shift the chain
+// found for it, and its status.  States are in fmPll's 6-double order.
+// u: the start (phaseEst, integrator) the current solution (theta row, e) was solved from.
+// shift: the chain's whole turns for the block's phases; d: the start error (dphaseEst, dV)
+// the chain accepted the block with (its stored phases + the loop's linear response to d are
+// the recurrence's); margin: the solve's smallest distance of a step's fract(t_k) from a wrap,
+// in turns (-1: none, the sequential kernels' solves).
+struct LongBlk {
+  double g[6]; double x[6]; double e[6]; double u[2]; double shift; double d[2]; double margin; int status; int solver;
+};
+struct LongHdr { double sp, si; int pos; int pad; double pad2; };
+static_assert(sizeof(LongBlk) == 200 && sizeof(LongHdr) == 32, "long-call scratch layout");
+// the first LongBlk of recurrence r in a long call's scratch
+__host__ __device__ inline const LongBlk* long_blk0(const void* work, int njobs, int nstreams, int nb, int r) {
+  return reinterpret_cast<const LongBlk*>(static_cast<const char*>(work) + (int64_t)njobs * nstreams * sizeof(LongHdr)) +
+         (int64_t)r * nb;
+}
+
+// Where one PLL job's NCO comes from, for every stream of a receiver block.
+struct NcoSrc {
+  const double* theta;     // phase rows (th_stride apart); theta[n] = the call's trigOffset
+  int64_t th_stride;
+  const float* nco_i;      // NCO rows (out_stride apart): only [0], the carried value, is read
+  const float* nco_q;      //   (nullable: no quadrature output)
+  int64_t out_stride;
+  double w, scale, adj;    // 2 pi freq / Fs, ncoScale, phaseAdjust
+  int64_t n;               // steps of the call
+  // long calls (blk != null): stream s's pseudo-blocks at blk + s * blk_stride, pb steps each;
+  // resp[2 (kk + 1) + {0, 1}] = row 0 of A^(kk+1), kk < pb
+  const LongBlk* blk;
+  int64_t blk_stride, pb;
+  const double* resp;
+};
+
+// The recurrence's phaseEst for step kk of a long call's pseudo-block B whose solve stored
+// `stored` there (the chain's turns, then the linear response to its accepted start error).
+__device__ __forceinline__ double nco_phase_in(const LongBlk* B, int64_t kk, const double* resp, double stored) {
+#pragma clang fp contract(off)
+  const double sh = B->shift, d0 = B->d[0], d1 = B->d[1];
+  double p = fma(sh, sdrnco::kP1, fma(sh, sdrnco::kP2, stored));
+  if (d0 != 0.0 || d1 != 0.0) {
+    const double* rr = resp + 2 * (kk + 1);
+    p = p + (rr[0] * d0 + rr[1] * d1);
+  }
+  return p;
+}
+
+// phaseEst_j (j >= 0) of stream s.
+__device__ __forceinline__ double nco_phase(const NcoSrc& N, int s, int64_t j, double stored) {
+  if (N.blk == nullptr) return stored;
+  int64_t b = (int64_t)((double)j / (double)N.pb);
+  if (b * N.pb > j) --b;
+  else if ((b + 1) * N.pb <= j) ++b;
+  return nco_phase_in(N.blk + (int64_t)s * N.blk_stride + b, j - b * N.pb, N.resp, stored);
+}
+
+// ncoOut[k] / ncoOutQ[k] (k >= 1), in f64 (the caller rounds), from p = phaseEst_{k-1} and the
+// call's trigOffset off; every NCO row of the library is formed here.
+template <bool OPAQUE = false>
+__device__ __forceinline__ void nco_value(double w, double scale, double adj, int64_t k, double p, double off,
+                                          double* cv, double* sv) {
+#pragma clang fp contract(off)
+  const double th = w * ((off + (double)(k - 1)) + 1.0) + p;
+  const double a = th * scale + adj;
+  sdrnco::sincos_red<OPAQUE>(sdrnco::reduce_2pi(a), sv, cv);
+}
