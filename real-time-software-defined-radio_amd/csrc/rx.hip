@@ -67,6 +67,9 @@ struct StageJob {
   float gain;
   int pre, D, U, kind, T, tiles;
   int small;             // D = 1 FIR: 4 outputs per lane (a launch with few tiles: more workgroups)
+  int sym;               // the f32 taps are symmetric (linear phase: every firwin design)
+  int fold;              // > 1: the leader of `fold` consecutive symmetric jobs on the same input,
+                         //   computed together by fold_tile (the others get no tile workgroups)
   int nco_sin;           // PRE_NCO: the quadrature NCO (sin) instead of cos
   NcoSrc nco;            // PRE_NCO: where the NCO comes from
 };
@@ -102,20 +105,22 @@ __device__ __forceinline__ float pre_op(int pre, float x, float c, float g) {
   return pre == PRE_SQUARE ? x * x : (pre == PRE_MIX || pre == PRE_NCO) ? (x * c) * g : x;
 }
 
-// ncoOut[k] and ncoOutQ[k] of stream s as f32 (the values the PLL's NCO rows hold, bit for bit):
-// [0] is the carried value the PLL kernel stored, [k >= 1] is formed from phaseEst_{k-1}
+// ncoOut[k] and ncoOutQ[k] of stream s as the mixers take them (f32, sdr_nco.h nco_f32x2):
+// [0] is the carried value the PLL kernel stored, [k >= 1] is formed from phaseEst_{k-1}.
+// (Single samples: the tiles' cold paths and the final-state workgroups; the tiles' staging
+// takes two at a time with the pseudo-block records read once per tile.)
 __device__ __forceinline__ void nco_at(const NcoSrc& N, int s, int64_t k, float* c, float* sn) {
   if (k == 0) {
     *c = N.nco_i[(int64_t)s * N.out_stride];
     *sn = N.nco_q ? N.nco_q[(int64_t)s * N.out_stride] : 0.f;
     return;
   }
-  const double* th = N.theta + (int64_t)s * N.th_stride;
-  const double p = nco_phase(N, s, k - 1, th[k - 1]);
-  double cv, sv;
-  nco_value(N.w, N.scale, N.adj, k, p, th[N.n], &cv, &sv);
-  *c = (float)cv;
-  *sn = (float)sv;
+  const NcoTile T = nco_tile(N, s, k - 1);
+  const double p = nco_tile_p(N, T, k - 1, T.th[k - 1]);
+  ncof2 c2, s2;
+  nco_f32x2(N, T.off, k, p, p, &c2, &s2);
+  *c = c2.x;
+  *sn = s2.x;
 }
 __device__ __forceinline__ float nco_one(const StageJob& J, int s, int64_t k) {
   float c, sn;
@@ -133,6 +138,13 @@ typedef const __attribute__((address_space(4))) f2a4* ctaps2_t;
 // registers nor assembles packed operands with a v_mov per FMA
 __device__ __forceinline__ void pk_fma_s(f2& acc, f2 h, f2 x) {
   asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(acc) : "s"(h), "v"(x));
+}
+
+// acc.xy += h.{lo or hi} * x.xy: the tap broadcast from a 64-bit SGPR pair by op_sel
+template <bool HI>
+__device__ __forceinline__ void pk_fma_sb(f2& acc, f2 h, f2 x) {
+  if (HI) asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(h), "v"(x));
+  else asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "s"(h), "v"(x));
 }
 
 // The lfilter FIR tile for compile-time (T, D): lane t owns R consecutive outputs and slides
@@ -184,6 +196,8 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
     mr[r] = (J.mono != nullptr && mf + r < M) ? J.mono[(int64_t)s * J.y_stride + mf + r] : 0.f;
   }
   if (n_lo >= 0 && n_lo + S::LG <= J.n) {            // interior: 16-B loads (rows are aligned)
+    NcoTile nt{};
+    if (NCO && pre == PRE_NCO) nt = nco_tile(J.nco, s, n_lo - 1);   // the pseudo-block records, once
     // every load of the thread's chunks is issued before the first is used (one memory
     // round trip per tile, not one per chunk)
     constexpr int NCH = S::LG / S::G, NQ = (NCH + S::NT - 1) / S::NT;
@@ -203,7 +217,17 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
         const int u = q * S::G;
         if (NCO && pre == PRE_NCO) {                 // the NCO of these 4 inputs, from the PLL phases
           const int64_t nn = n_lo + u;
-          cv[j] = make_float4(nco_one(J, s, nn), nco_one(J, s, nn + 1), nco_one(J, s, nn + 2), nco_one(J, s, nn + 3));
+          if (nn >= 1) {
+            const double* th = nt.th + nn - 1;
+            const double t0 = th[0], t1 = th[1], t2 = th[2], t3 = th[3];
+            ncof2 c01, s01, c23, s23;
+            nco_f32x2(J.nco, nt.off, nn, nco_tile_p(J.nco, nt, nn - 1, t0), nco_tile_p(J.nco, nt, nn, t1), &c01, &s01);
+            nco_f32x2(J.nco, nt.off, nn + 2, nco_tile_p(J.nco, nt, nn + 1, t2), nco_tile_p(J.nco, nt, nn + 2, t3), &c23,
+                      &s23);
+            cv[j] = J.nco_sin ? make_float4(s01.x, s01.y, s23.x, s23.y) : make_float4(c01.x, c01.y, c23.x, c23.y);
+          } else {
+            cv[j] = make_float4(nco_one(J, s, nn), nco_one(J, s, nn + 1), nco_one(J, s, nn + 2), nco_one(J, s, nn + 3));
+          }
         }
         lds[S::slot(u + 0)] = pre_op(pre, v[j].x, cv[j].x, g);
         lds[S::slot(u + 1)] = pre_op(pre, v[j].y, cv[j].y, g);
@@ -271,6 +295,137 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
         if (lhb) lhb[mf + r] = lv;
         if (rhb) rhb[mf + r] = rv;
       }
+    }
+  }
+}
+
+// F symmetric 151-tap FIRs (D = 1, no pre-op) on the SAME input, together (stage A: the pilot,
+// stereo and RDS extract band-passes of the demod, model/fmMonoBlock.py:117,151 and
+// model/fmRDSblock.py:156).  Linear-phase taps (h[k] = h[150 - k], every firwin design) let
+// the three share the folded input sums:
+//   y_f[n] = sum_{k<75} h_f[k] (x[n-k] + x[n-150+k]) + h_f[75] x[n-75]
+// -- per output 75 adds shared by the F filters and 76 F multiply-adds, where the direct form
+// takes 151 F (F = 3: 303 against 453 flops per output).  One staged image for all F (the
+// direct form staged it F times).  Lane t owns outputs m0 + 16 t + r (16, as fir_tile<151, 1>,
+// whose image layout this is), two at a time: the sums (x[n-k] + x[n-150+k], x[n+1-k] +
+// x[n-149+k]) are one v_pk_add_f32 of two sample pairs, each filter's update one v_pk_fma_f32
+// with its tap broadcast from an SGPR pair.  Pair (i, i+1) of the lane's window at i even is
+// one ds_read_b64, at i odd a ds_read2_b32 (it may span the pad after a 16-sample block); the
+// unrolled k loop reads each pair once (it is reused by the 8 output pairs over 8 k steps).
+template <int F>
+__device__ __forceinline__ void fold_tile(const StageJob* Jf, int s, int64_t tile, float* lds) {
+  using S = FirShape<151, 1, 16>;
+  constexpr int T = 151, R = 16, DELTA = S::DELTA, C = (T - 1) / 2;
+  const StageJob& J = Jf[0];
+  const int t = threadIdx.x;
+  const int64_t m0 = tile * S::TO;
+  const int64_t M = J.n;
+  const int64_t n_lo = m0 - (T - 1) - DELTA;
+  const int64_t mf = m0 + (int64_t)t * R;
+  const float* xb = J.x + (int64_t)s * J.x_stride;
+  if (n_lo >= 0 && n_lo + S::LG <= J.n) {
+    constexpr int NCH = S::LG / S::G, NQ = (NCH + S::NT - 1) / S::NT;
+    float4 v[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const int q = t + j * S::NT;
+      if (q < NCH) v[j] = reinterpret_cast<const float4*>(xb + n_lo)[q];
+    }
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const int q = t + j * S::NT;
+      if (q < NCH) {
+        const int u = q * S::G;
+        lds[S::slot(u + 0)] = v[j].x;
+        lds[S::slot(u + 1)] = v[j].y;
+        lds[S::slot(u + 2)] = v[j].z;
+        lds[S::slot(u + 3)] = v[j].w;
+      }
+    }
+  } else {
+    for (int u = t; u < S::LG; u += S::NT) {
+      const int64_t nn = n_lo + u;
+      lds[S::slot(u)] = (nn >= 0 && nn < J.n) ? xb[nn] : 0.f;
+    }
+  }
+  __syncthreads();
+  const float* win = lds + DELTA + S::SR * t;
+  auto addr = [](int i) { return i + 2 * (i / R); };        // window index -> float offset
+  auto pair = [&](int i) -> f2 {                             // (x_i, x_{i+1}) of the lane's window
+    if (i % 2 == 0) return *reinterpret_cast<const f2*>(win + addr(i));
+    return f2{win[addr(i)], win[addr(i + 1)]};
+  };
+  ctaps2_t g2[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) g2[f] = (ctaps2_t)Jf[f].taps;  // forward taps, (h[k], h[k+1]) pairs
+  f2 acc[F][R / 2];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int r2 = 0; r2 < R / 2; ++r2) acc[f][r2] = f2{0.f, 0.f};
+  // output pair r2 (outputs 2 r2, 2 r2 + 1): x[n - k] is window index 150 + 2 r2 - k and
+  // x[n - 150 + k] index 2 r2 + k.  The even k first, then the odd ones: per parity the 8 left
+  // and 8 right pairs live in registers, and each step of k by 2 loads one of each (the left
+  // pair of r2 at k is that of r2 - 1 at k - 2, the right one that of r2 + 1)
+  static_for<0, 2>([&](auto PP) {
+    constexpr int par = PP;
+    f2 lw[R / 2], rw[R / 2];
+    static_for<0, R / 2>([&](auto RR) {
+      constexpr int r2 = RR;
+      lw[r2] = pair(T - 1 + 2 * r2 - par);
+      rw[r2] = pair(2 * r2 + par);
+    });
+    static_for<0, (C + 2 - par) / 2>([&](auto KI) {
+      constexpr int k = par + 2 * KI;
+      if constexpr (KI > 0) {
+#pragma unroll
+        for (int r2 = R / 2 - 1; r2 > 0; --r2) lw[r2] = lw[r2 - 1];
+        lw[0] = pair(T - 1 - k);
+        if constexpr (k < C) {
+#pragma unroll
+          for (int r2 = 0; r2 < R / 2 - 1; ++r2) rw[r2] = rw[r2 + 1];
+          rw[R / 2 - 1] = pair(R - 2 + k);
+        }
+      }
+      static_for<0, R / 2>([&](auto RR) {
+        constexpr int r2 = RR;
+        f2 sum = lw[r2];
+        if constexpr (k < C) sum = sum + rw[r2];             // v_pk_add_f32
+        static_for<0, F>([&](auto FF) {
+          constexpr int f = FF;
+          const f2a4 hp = g2[f][k / 2];                     // (h[k & ~1], h[(k & ~1) + 1])
+          pk_fma_sb<k % 2 == 1>(acc[f][r2], f2{hp.x, hp.y}, sum);
+        });
+      });
+      // one k step's loads stay with its arithmetic: hoisted, the 3 x 76 tap pairs and the
+      // window pairs outgrew the registers (183 VGPRs, 246 SGPR spills)
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  });
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    const StageJob& Jj = Jf[f];
+    float o[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t nn = mf + r;                           // lfilter zi: the block's first T - 1 outputs
+      const float z = (Jj.zi != nullptr && nn < T - 1) ? (float)Jj.zi[(int64_t)s * Jj.zi_stride + nn] : 0.f;
+      o[r] = ((r & 1) ? acc[f][r / 2].y : acc[f][r / 2].x) + z;
+    }
+    float* yb = Jj.y + (int64_t)s * Jj.y_stride;
+    if (mf + R <= M) {
+#pragma unroll
+      for (int r = 0; r < R; r += 4) *reinterpret_cast<float4*>(yb + mf + r) = make_float4(o[r], o[r + 1], o[r + 2], o[r + 3]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (mf + r < M) yb[mf + r] = o[r];
+    }
+    if (Jj.yh != nullptr) {
+      float* hb = Jj.yh + (int64_t)s * Jj.yh_stride;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (mf + r < M) hb[mf + r] = o[r];
     }
   }
 }
@@ -462,9 +617,10 @@ __device__ __forceinline__ void fe_state_block(const FeState& F, int s, float* l
 // D = 1 and 5); T == 0: any tap count.  Workgroups map to (job, stream, tile) in job order,
 // then to the zf work.  NCO: the launch has PRE_NCO jobs (stage C's mixers; T > 0 only) --
 // a separate instantiation, so the other stages keep their registers.
-template <int T, bool NCO = false>
+template <int T, bool NCO = false, bool FOLD = false>
 __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
   static_assert(!NCO || T > 0, "PRE_NCO jobs run on the compile-time tiles");
+  static_assert(!FOLD || (T == 151 && !NCO), "fold groups: 151 taps, no NCO jobs");
   __shared__ __attribute__((aligned(16))) float lds[RX_LDS];
   const int64_t b = blockIdx.x;
   if (b >= P.tile_blocks) {
@@ -483,6 +639,10 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
   if (J.kind == JK_RESAMPLE) {
     resample_tile(J, s, tile, lds);
     return;
+  }
+  if constexpr (FOLD) {
+    if (J.fold == 3) { fold_tile<3>(&J, s, tile, lds); return; }
+    if (J.fold == 2) { fold_tile<2>(&J, s, tile, lds); return; }
   }
   if constexpr (T > 0) {
     if (J.D == 1) {
@@ -524,14 +684,30 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
         big += (nout + 1023) / 1024 * S;
       }
     const bool small = key > 0 && big < 10 * 256;
-    for (const StageJob& j0 : jobs) {
+    // symmetric 151-tap D = 1 jobs on one input, consecutive in the list: folded together (fold_tile)
+    auto foldable = [&](const StageJob& a) {
+      return key == 151 && !small && a.kind == JK_FIR && a.D == 1 && a.pre == PRE_NONE && a.T == 151 && a.sym;
+    };
+    int follow = 0;                                  // jobs left in the current fold group
+    for (size_t ji = 0; ji < jobs.size(); ++ji) {
+      const StageJob& j0 = jobs[ji];
       if (cls(j0) != key) continue;
       if (P.njobs == RX_MAXJ) return hipErrorInvalidValue;
       StageJob j = j0;
       const int64_t nout = j.kind == JK_RESAMPLE ? (j.n * j.U + j.D - 1) / j.D : (j.n + j.D - 1) / j.D;
       j.small = (small && j.kind == JK_FIR && j.D == 1) ? 1 : 0;
+      j.fold = 0;
+      if (follow == 0 && foldable(j)) {
+        int g = 1;
+        while (g < 3 && ji + g < jobs.size() && foldable(jobs[ji + g]) && jobs[ji + g].x == j.x &&
+               jobs[ji + g].x_stride == j.x_stride && jobs[ji + g].n == j.n && P.njobs + g < RX_MAXJ)
+          ++g;
+        if (g > 1) { j.fold = g; follow = g; }
+      }
+      const bool follower = follow > 0 && j.fold == 0;
+      if (follow > 0) --follow;
       const int64_t to = tile_outputs(j, key);
-      j.tiles = (int)std::max<int64_t>((nout + to - 1) / to, 0);
+      j.tiles = follower ? 0 : (int)std::max<int64_t>((nout + to - 1) / to, 0);
       j.b0 = blocks;
       blocks += (int64_t)j.tiles * S;
       if (j.zf != nullptr && j.T > 1) P.zfj[P.nzf++] = P.njobs;
@@ -549,7 +725,11 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
     bool nco = false;
     for (int i = 0; i < P.njobs; ++i) nco = nco || P.j[i].pre == PRE_NCO;
     if (nco && key == 0) return hipErrorInvalidValue;     // (the receiver never asks: stage_nco_ok)
-    if (key == 151 && nco) hipLaunchKernelGGL((rx_stage_kernel<151, true>), dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
+    bool fold = false;
+    for (int i = 0; i < P.njobs; ++i) fold = fold || P.j[i].fold > 1;
+    if (fold && (nco || key != 151)) return hipErrorInvalidValue;
+    if (fold) hipLaunchKernelGGL((rx_stage_kernel<151, false, true>), dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
+    else if (key == 151 && nco) hipLaunchKernelGGL((rx_stage_kernel<151, true>), dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
     else if (key == 151) hipLaunchKernelGGL(rx_stage_kernel<151>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
     else if (key == 101 && nco) hipLaunchKernelGGL((rx_stage_kernel<101, true>), dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
     else if (key == 101) hipLaunchKernelGGL(rx_stage_kernel<101>, dim3((unsigned)grid), dim3(RX_NT), 0, st, P);
@@ -628,12 +808,6 @@ struct CresJob {
 };
 
 typedef const __attribute__((address_space(4))) f2a4* ctaps2c_t;
-// acc.xy += h.{lo or hi} * x.xy: the tap broadcast from a 64-bit SGPR pair by op_sel
-template <bool HI>
-__device__ __forceinline__ void pk_fma_sb(f2& acc, f2 h, f2 x) {
-  if (HI) asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(h), "v"(x));
-  else asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "s"(h), "v"(x));
-}
 
 template <int W>
 __device__ __forceinline__ void cres_fir(const float* win, const float* taps, f2 (&acc)[5]) {
@@ -655,16 +829,18 @@ __device__ __forceinline__ void cres_fir(const float* win, const float* taps, f2
   });
 }
 
-// the NCO pair of inputs i, i+1 of stream s (from the phases, or from the NCO rows)
-__device__ __forceinline__ void cres_nco2(const NcoSrc& N, int s, int64_t i, float4* cs) {
+// the NCO pair of inputs i, i+1 (i >= 1) of stream s (from the phases, or from the NCO rows)
+__device__ __forceinline__ void cres_nco2(const NcoSrc& N, const NcoTile& T, int s, int64_t i, float4* cs) {
   if (N.theta == nullptr) {
     const float* ri = N.nco_i + (int64_t)s * N.out_stride;
     const float* rq = N.nco_q + (int64_t)s * N.out_stride;
     *cs = make_float4(ri[i], rq[i], ri[i + 1], rq[i + 1]);
     return;
   }
-  nco_at(N, s, i, &cs->x, &cs->y);
-  nco_at(N, s, i + 1, &cs->z, &cs->w);
+  const double t0 = T.th[i - 1], t1 = T.th[i];
+  ncof2 c, sn;
+  nco_f32x2(N, T.off, i, nco_tile_p(N, T, i - 1, t0), nco_tile_p(N, T, i, t1), &c, &sn);
+  *cs = make_float4(c.x, sn.x, c.y, sn.y);
 }
 
 // final states of one stream: the LPF's (I, Q) from the last 150 mixed inputs and the
@@ -751,6 +927,8 @@ __global__ __launch_bounds__(CR_NT) void rx_cres_kernel(CresJob J) {
   const int64_t n = J.n;
   // stage the window: pairs (2j, 2j + 1) per chunk j, mixed I and Q (the gain 2 is in the taps)
   constexpr int NCHK = (CR_NP + 1) / 2, NR = (NCHK + CR_NT - 1) / CR_NT;
+  NcoTile nt{};
+  if (J.nco.theta != nullptr) nt = nco_tile(J.nco, s, ws - 1);   // the pseudo-block records, once
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     const int j = t + r * CR_NT;
@@ -758,16 +936,20 @@ __global__ __launch_bounds__(CR_NT) void rx_cres_kernel(CresJob J) {
       const int64_t i = ws + 2 * j;
       float2 xv;
       float4 cs;
-      if (i >= 0 && i + 1 < n) {
+      if (i >= 1 && i + 1 < n) {
         xv = *reinterpret_cast<const float2*>(x + i);
-        cres_nco2(J.nco, s, i, &cs);
+        cres_nco2(J.nco, nt, s, i, &cs);
       } else {
         xv = make_float2(0.f, 0.f);
         cs = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (i >= 0 && i < n) {
-          xv.x = x[i];
-          if (J.nco.theta) nco_at(J.nco, s, i, &cs.x, &cs.y);
-          else { cs.x = J.nco.nco_i[(int64_t)s * J.nco.out_stride + i]; cs.y = J.nco.nco_q[(int64_t)s * J.nco.out_stride + i]; }
+        for (int e = 0; e < 2; ++e) {                       // block ends (and the carried NCO[0])
+          const int64_t ie = i + e;
+          if (ie < 0 || ie >= n) continue;
+          float c, sn;
+          if (J.nco.theta) nco_at(J.nco, s, ie, &c, &sn);
+          else { c = J.nco.nco_i[(int64_t)s * J.nco.out_stride + ie]; sn = J.nco.nco_q[(int64_t)s * J.nco.out_stride + ie]; }
+          if (e == 0) { xv.x = x[ie]; cs.x = c; cs.y = sn; }
+          else { xv.y = x[ie]; cs.z = c; cs.w = sn; }
         }
       }
       *reinterpret_cast<float4*>(lds + cr_addr(2 * j)) = make_float4(xv.x * cs.x, xv.x * cs.y, xv.y * cs.z, xv.y * cs.w);
@@ -1246,6 +1428,9 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     j.y = y; j.y_stride = ys; j.n = n; j.x_stride = xs;
     j.gain = 2.0f;                      // the reference's mixer gain (fmMonoBlock.py:156, fmRDSblock.py:173)
     j.pre = pre; j.D = D; j.U = 1; j.kind = JK_FIR; j.T = (int)r->taps[f].size();
+    j.sym = 1;                          // linear phase (f32 taps mirror-equal): fold_tile may take it
+    for (int k = 0; k < j.T / 2 && j.T <= SDR_MAX_TAPS; ++k)
+      if (ts[f]->h.h[k] != ts[f]->h.h[j.T - 1 - k]) j.sym = 0;
     j.yh = mirror_of(y);
     j.yh_stride = host_n(y);
     return j;
@@ -1315,7 +1500,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       const int jq = P.njobs;
       P.j[P.njobs++] = PllJob{in, ms, r->pll_state[k], thk, r->ths, ni, nq, ms, r->pll[k], pck, r->cst, off, 1, resp};
       NcoSrc& N = nsrc[k];
-      N.theta = nco_rows ? nullptr : thk;
+      N.theta = M >= 2 ? thk : nullptr;   // (M < 2: the sequential kernels' Q-form rows; mix from the NCO rows)
       N.th_stride = r->ths;
       N.nco_i = ni;
       N.nco_q = nq;
@@ -1327,6 +1512,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       if (lng) {
         N.blk = long_blk0(P.work, 0, S, nb, jq * S);        // njobs fixed up below
         N.blk_stride = nb;
+        N.nb = nb;
         N.pb = pb;
         N.resp = resp;
       }

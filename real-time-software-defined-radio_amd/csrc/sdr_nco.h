@@ -112,6 +112,7 @@ struct NcoSrc {
   // resp[2 (kk + 1) + {0, 1}] = row 0 of A^(kk+1), kk < pb
   const LongBlk* blk;
   int64_t blk_stride, pb;
+  int nb;                  // pseudo-blocks of the call
   const double* resp;
 };
 
@@ -146,4 +147,93 @@ __device__ __forceinline__ void nco_value(double w, double scale, double adj, in
   const double th = w * ((off + (double)(k - 1)) + 1.0) + p;
   const double a = th * scale + adj;
   sdrnco::sincos_red<OPAQUE>(sdrnco::reduce_2pi(a), sv, cv);
+}
+
+// ---- the mixers' NCO (rx.hip): f32 cos / sin of the f64 angle ------------------------------
+// The mixers only need the NCO to the f32 rounding of their product: the angle a = th scale +
+// adj is formed and reduced in f64 exactly as above (|y| <= pi/4 after the quadrant), then
+// y is rounded to f32 (3e-8) and cos / sin come from f32 polynomials on two samples at once
+// (packed FMAs; Taylor to y^9 / y^10: truncation < 1e-9), ~1 ulp of the f32 result -- the
+// error of the NCO row a mixer would otherwise read, at a third of the f64 polynomial's work.
+// (The NCO rows, when an output asks for them, stay the f64 ones above.)
+// Per tile: the pseudo-block records its steps fall in (a tile spans < pb steps: at most
+// two), read once.
+struct NcoTile {
+  const double* th;        // the stream's phase row
+  double off;              // the call's trigOffset
+  int64_t kb, bound;       // steps j in [kb, bound): the first block, [bound, ...): the second
+  double sh[2], d0[2], d1[2];
+};
+
+__device__ __forceinline__ NcoTile nco_tile(const NcoSrc& N, int s, int64_t j0) {
+  NcoTile T;
+  T.th = N.theta + (int64_t)s * N.th_stride;
+  T.off = T.th[N.n];
+  T.kb = 0;
+  T.bound = INT64_MAX;
+  for (int h = 0; h < 2; ++h) T.sh[h] = T.d0[h] = T.d1[h] = 0.0;
+  if (N.blk != nullptr) {
+    const int64_t b = max(j0, (int64_t)0) / N.pb;
+    T.kb = b * N.pb;
+    T.bound = T.kb + N.pb;
+    const LongBlk* B = N.blk + (int64_t)s * N.blk_stride + b;
+    T.sh[0] = B->shift; T.d0[0] = B->d[0]; T.d1[0] = B->d[1];
+    if (b + 1 < N.nb) { T.sh[1] = B[1].shift; T.d0[1] = B[1].d[0]; T.d1[1] = B[1].d[1]; }
+  }
+  return T;
+}
+
+// phaseEst_j from its stored value (nco_phase_in's arithmetic)
+__device__ __forceinline__ double nco_tile_p(const NcoSrc& N, const NcoTile& T, int64_t j, double stored) {
+#pragma clang fp contract(off)
+  const bool h = j >= T.bound;
+  const double sh = h ? T.sh[1] : T.sh[0], d0 = h ? T.d0[1] : T.d0[0], d1 = h ? T.d1[1] : T.d1[0];
+  double p = fma(sh, sdrnco::kP1, fma(sh, sdrnco::kP2, stored));
+  if (d0 != 0.0 || d1 != 0.0) {
+    const int64_t kk = j - (h ? T.bound : T.kb);
+    const double* rr = N.resp + 2 * (kk + 1);
+    p = p + (rr[0] * d0 + rr[1] * d1);
+  }
+  return p;
+}
+
+typedef float ncof2 __attribute__((ext_vector_type(2)));
+// cos / sin (f32) of the NCO angles of outputs k and k + 1 (k >= 1) from p = phaseEst_{k-1}, _k
+__device__ __forceinline__ void nco_f32x2(const NcoSrc& N, double off, int64_t k, double p0, double p1, ncof2* c,
+                                          ncof2* sn) {
+#pragma clang fp contract(off)
+  constexpr double kPio2Hi = 1.5707963267948966, kPio2Lo = 6.123233995736766e-17, k2oPi = 0.6366197723675814;
+  double y[2];
+  int q[2];
+  const double pp[2] = {p0, p1};
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double th = N.w * ((off + (double)(k - 1 + i)) + 1.0) + pp[i];
+    const double a = sdrnco::reduce_2pi(th * N.scale + N.adj);
+    const double n = rint(a * k2oPi);
+    double yy = fma(-n, kPio2Hi, a);
+    y[i] = fma(-n, kPio2Lo, yy);
+    q[i] = (int)n & 3;
+  }
+  const ncof2 yf = ncof2{(float)y[0], (float)y[1]};
+  const ncof2 z = yf * yf;
+  auto K = [](float v) { return ncof2{v, v}; };
+  ncof2 ps = __builtin_elementwise_fma(K(2.7557319e-06f), z, K(-1.9841270e-04f));
+  ps = __builtin_elementwise_fma(ps, z, K(8.3333333e-03f));
+  ps = __builtin_elementwise_fma(ps, z, K(-1.6666667e-01f));
+  const ncof2 sv = __builtin_elementwise_fma(ps * z, yf, yf);
+  ncof2 pc = __builtin_elementwise_fma(K(-2.7557319e-07f), z, K(2.4801587e-05f));
+  pc = __builtin_elementwise_fma(pc, z, K(-1.3888889e-03f));
+  pc = __builtin_elementwise_fma(pc, z, K(4.1666668e-02f));
+  pc = __builtin_elementwise_fma(pc, z, K(-0.5f));
+  const ncof2 cv = __builtin_elementwise_fma(pc, z, K(1.0f));
+  float cs[2], ss[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float s0 = (q[i] & 1) ? cv[i] : sv[i], c0 = (q[i] & 1) ? sv[i] : cv[i];
+    ss[i] = (q[i] == 2 || q[i] == 3) ? -s0 : s0;
+    cs[i] = (q[i] == 1 || q[i] == 2) ? -c0 : c0;
+  }
+  *c = ncof2{cs[0], cs[1]};
+  *sn = ncof2{ss[0], ss[1]};
 }
