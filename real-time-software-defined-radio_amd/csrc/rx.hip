@@ -217,14 +217,10 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
         const int u = q * S::G;
         if (NCO && pre == PRE_NCO) {                 // the NCO of these 4 inputs, from the PLL phases
           const int64_t nn = n_lo + u;
-          if (nn >= 1) {
-            const double* th = nt.th + nn - 1;
-            const double t0 = th[0], t1 = th[1], t2 = th[2], t3 = th[3];
-            ncof2 c01, s01, c23, s23;
-            nco_f32x2(J.nco, nt.off, nn, nco_tile_p(J.nco, nt, nn - 1, t0), nco_tile_p(J.nco, nt, nn, t1), &c01, &s01);
-            nco_f32x2(J.nco, nt.off, nn + 2, nco_tile_p(J.nco, nt, nn + 1, t2), nco_tile_p(J.nco, nt, nn + 2, t3), &c23,
-                      &s23);
-            cv[j] = J.nco_sin ? make_float4(s01.x, s01.y, s23.x, s23.y) : make_float4(c01.x, c01.y, c23.x, c23.y);
+          if (nn >= 2) {                             // (nn is a multiple of 4: 16-B phase pairs)
+            float c4[4], s4[4];
+            nco_f32x4(J.nco, nt, nn, c4, s4);
+            cv[j] = J.nco_sin ? make_float4(s4[0], s4[1], s4[2], s4[3]) : make_float4(c4[0], c4[1], c4[2], c4[3]);
           } else {
             cv[j] = make_float4(nco_one(J, s, nn), nco_one(J, s, nn + 1), nco_one(J, s, nn + 2), nco_one(J, s, nn + 3));
           }
@@ -768,16 +764,18 @@ constexpr int CR_G = 64, CR_NW = 4, CR_NT = 64 * CR_NW;
 constexpr int CR_TO = CR_U * CR_G;                       // outputs per tile
 constexpr int CR_IN = CR_D * CR_G;                       // inputs per tile
 __host__ __device__ constexpr int cr_base(int c) { return (CR_D * c) / CR_U; }
-constexpr int CR_LW = cr_base(CR_U - 1) + CR_CT + 1;     // 234 window pairs per group (pair 0 unused)
-constexpr int CR_NP = CR_IN - CR_D + CR_LW;              // 5 274 window pairs per tile
+constexpr int CR_SH = 2;                                 // the window starts 160 inputs early (16-B aligned)
+constexpr int CR_LW = cr_base(CR_U - 1) + CR_CT + 1 + CR_SH;   // 236 window pairs per group (pairs 0-2 unused)
+constexpr int CR_NP = CR_IN - CR_D + CR_LW;              // 5 276 window pairs per tile
 // LDS float offset of window pair p: 4 pad floats after every group's 80 pairs (group stride
 // 164 floats = 41 x 16 B, odd: conflict-free 16-B reads across the lanes)
 __host__ __device__ constexpr int cr_addr(int p) { return 2 * p + 4 * (p / CR_D); }
 constexpr int CR_LDS = cr_addr(CR_NP + 1) + 4;
 __host__ __device__ constexpr int cr_c0(int w) { return 5 * w; }
 __host__ __device__ constexpr int cr_c1(int w) { return 5 * w + 5 < CR_U ? 5 * w + 5 : CR_U; }
-__host__ __device__ constexpr int cr_ulo(int w) { return (cr_base(cr_c0(w)) + 1) & ~1; }
-__host__ __device__ constexpr int cr_uhi(int w) { return cr_base(cr_c1(w) - 1) + CR_CT; }      // inclusive
+// window pair u of group L is input I0 - 160 + 80 L + u; phase c reads u in [base_c + 3, base_c + 160]
+__host__ __device__ constexpr int cr_ulo(int w) { return (cr_base(cr_c0(w)) + 1 + CR_SH) & ~1; }
+__host__ __device__ constexpr int cr_uhi(int w) { return cr_base(cr_c1(w) - 1) + CR_CT + CR_SH; }      // inclusive
 __host__ __device__ constexpr int cr_npair(int w) { return (cr_uhi(w) - cr_ulo(w)) / 2 + 1; }
 // the taps of wave w start at float cr_toff(w): [pair u2][phase c - c0][(tap at u2, at u2 + 1)]
 __host__ __device__ constexpr int cr_toff(int w) {
@@ -818,8 +816,8 @@ __device__ __forceinline__ void cres_fir(const float* win, const float* taps, f2
     const float4 v = *reinterpret_cast<const float4*>(win + 2 * u2 + 4 * (u2 / CR_D));
     static_for<0, nc>([&](auto C) {
       constexpr int c = c0 + C;
-      constexpr bool v0 = u2 >= cr_base(c) + 1 && u2 <= cr_base(c) + CR_CT;
-      constexpr bool v1 = u2 + 1 >= cr_base(c) + 1 && u2 + 1 <= cr_base(c) + CR_CT;
+      constexpr bool v0 = u2 >= cr_base(c) + 1 + CR_SH && u2 <= cr_base(c) + CR_CT + CR_SH;
+      constexpr bool v1 = u2 + 1 >= cr_base(c) + 1 + CR_SH && u2 + 1 <= cr_base(c) + CR_CT + CR_SH;
       if constexpr (v0 || v1) {
         const f2a4 hp = tw[I * nc + C];
         if constexpr (v0) pk_fma_sb<false>(acc[C], f2{hp.x, hp.y}, f2{v.x, v.y});
@@ -827,20 +825,6 @@ __device__ __forceinline__ void cres_fir(const float* win, const float* taps, f2
       }
     });
   });
-}
-
-// the NCO pair of inputs i, i+1 (i >= 1) of stream s (from the phases, or from the NCO rows)
-__device__ __forceinline__ void cres_nco2(const NcoSrc& N, const NcoTile& T, int s, int64_t i, float4* cs) {
-  if (N.theta == nullptr) {
-    const float* ri = N.nco_i + (int64_t)s * N.out_stride;
-    const float* rq = N.nco_q + (int64_t)s * N.out_stride;
-    *cs = make_float4(ri[i], rq[i], ri[i + 1], rq[i + 1]);
-    return;
-  }
-  const double t0 = T.th[i - 1], t1 = T.th[i];
-  ncof2 c, sn;
-  nco_f32x2(N, T.off, i, nco_tile_p(N, T, i - 1, t0), nco_tile_p(N, T, i, t1), &c, &sn);
-  *cs = make_float4(c.x, sn.x, c.y, sn.y);
 }
 
 // final states of one stream: the LPF's (I, Q) from the last 150 mixed inputs and the
@@ -922,37 +906,37 @@ __global__ __launch_bounds__(CR_NT) void rx_cres_kernel(CresJob J) {
   }
   const int s = b / J.tiles;
   const int64_t tile = b - (int64_t)s * J.tiles;
-  const int64_t I0 = tile * CR_IN, ws = I0 - (CR_CT + 0);   // window pair p <-> input ws + p
+  const int64_t I0 = tile * CR_IN, ws = I0 - (CR_CT + CR_SH);   // window pair p <-> input ws + p
   const float* x = J.x + (int64_t)s * J.x_stride;
   const int64_t n = J.n;
-  // stage the window: pairs (2j, 2j + 1) per chunk j, mixed I and Q (the gain 2 is in the taps)
-  constexpr int NCHK = (CR_NP + 1) / 2, NR = (NCHK + CR_NT - 1) / CR_NT;
+  // stage the window: 4 inputs per chunk (16-B loads), mixed I and Q (the gain 2 is in the taps)
+  constexpr int NCHK = (CR_NP + 3) / 4, NR = (NCHK + CR_NT - 1) / CR_NT;
   NcoTile nt{};
   if (J.nco.theta != nullptr) nt = nco_tile(J.nco, s, ws - 1);   // the pseudo-block records, once
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     const int j = t + r * CR_NT;
     if (j < NCHK) {
-      const int64_t i = ws + 2 * j;
-      float2 xv;
-      float4 cs;
-      if (i >= 1 && i + 1 < n) {
-        xv = *reinterpret_cast<const float2*>(x + i);
-        cres_nco2(J.nco, nt, s, i, &cs);
+      const int64_t i = ws + 4 * j;
+      float xv[4], c[4], sn[4];
+      if (i >= 2 && i + 3 < n && J.nco.theta != nullptr) {
+        const float4 x4 = *reinterpret_cast<const float4*>(x + i);
+        xv[0] = x4.x; xv[1] = x4.y; xv[2] = x4.z; xv[3] = x4.w;
+        nco_f32x4(J.nco, nt, i, c, sn);
       } else {
-        xv = make_float2(0.f, 0.f);
-        cs = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int e = 0; e < 2; ++e) {                       // block ends (and the carried NCO[0])
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {                           // block ends (and the carried NCO[0])
           const int64_t ie = i + e;
+          xv[e] = c[e] = sn[e] = 0.f;
           if (ie < 0 || ie >= n) continue;
-          float c, sn;
-          if (J.nco.theta) nco_at(J.nco, s, ie, &c, &sn);
-          else { c = J.nco.nco_i[(int64_t)s * J.nco.out_stride + ie]; sn = J.nco.nco_q[(int64_t)s * J.nco.out_stride + ie]; }
-          if (e == 0) { xv.x = x[ie]; cs.x = c; cs.y = sn; }
-          else { xv.y = x[ie]; cs.z = c; cs.w = sn; }
+          xv[e] = x[ie];
+          if (J.nco.theta) nco_at(J.nco, s, ie, &c[e], &sn[e]);
+          else { c[e] = J.nco.nco_i[(int64_t)s * J.nco.out_stride + ie]; sn[e] = J.nco.nco_q[(int64_t)s * J.nco.out_stride + ie]; }
         }
       }
-      *reinterpret_cast<float4*>(lds + cr_addr(2 * j)) = make_float4(xv.x * cs.x, xv.x * cs.y, xv.y * cs.z, xv.y * cs.w);
+      float* dst = lds + cr_addr(4 * j);
+      *reinterpret_cast<float4*>(dst) = make_float4(xv[0] * c[0], xv[0] * sn[0], xv[1] * c[1], xv[1] * sn[1]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(xv[2] * c[2], xv[2] * sn[2], xv[3] * c[3], xv[3] * sn[3]);
     }
   }
   __syncthreads();
@@ -1011,7 +995,7 @@ void cres_taps(const std::vector<double>& h, const std::vector<double>& g, std::
       for (int k = 0; k < CR_T; ++k) C[(size_t)rho * CR_CT + ss + k] += g[rho + CR_U * ss] * h[k];
   out->assign(CR_NTAPS, 0.f);
   auto tap = [&](int c, int u) -> float {
-    const int tt = cr_base(c) + CR_CT - u;
+    const int tt = cr_base(c) + CR_CT + CR_SH - u;
     if (tt < 0 || tt >= CR_CT) return 0.f;
     const int rho = CR_D * c - CR_U * cr_base(c);
     return (float)(2.0 * CR_U * C[(size_t)rho * CR_CT + tt]);

@@ -198,26 +198,32 @@ __device__ __forceinline__ double nco_tile_p(const NcoSrc& N, const NcoTile& T, 
 }
 
 typedef float ncof2 __attribute__((ext_vector_type(2)));
-// cos / sin (f32) of the NCO angles of outputs k and k + 1 (k >= 1) from p = phaseEst_{k-1}, _k
-__device__ __forceinline__ void nco_f32x2(const NcoSrc& N, double off, int64_t k, double p0, double p1, ncof2* c,
-                                          ncof2* sn) {
+// The reduced angle of output k (>= 1) from p = phaseEst_{k-1}: a = (w scale) (trigOffset + k)
+// + (p scale + adj) (scale a power of two in every fmPll use: the same product as the
+// reference's (th) scale, one rounding fewer), reduced by a 3-part pi/2 (exact multiples for
+// |n| < 2^29: ~40 min of a 240 kS/s stream before its last bits blur, as the reference's own
+// f64 angle does) to |y| <= pi/4 in f32, and its quadrant.
+__device__ __forceinline__ void nco_angle_at(double ws, double scale, double adj, double offk, double p, float* y,
+                                             int* q) {
 #pragma clang fp contract(off)
-  constexpr double kPio2Hi = 1.5707963267948966, kPio2Lo = 6.123233995736766e-17, k2oPi = 0.6366197723675814;
-  double y[2];
-  int q[2];
-  const double pp[2] = {p0, p1};
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const double th = N.w * ((off + (double)(k - 1 + i)) + 1.0) + pp[i];
-    const double a = sdrnco::reduce_2pi(th * N.scale + N.adj);
-    const double n = rint(a * k2oPi);
-    double yy = fma(-n, kPio2Hi, a);
-    y[i] = fma(-n, kPio2Lo, yy);
-    q[i] = (int)n & 3;
-  }
-  const ncof2 yf = ncof2{(float)y[0], (float)y[1]};
-  const ncof2 z = yf * yf;
+  constexpr double k2oPi = 0.6366197723675814;
+  constexpr double Q1 = 1.5707963705062866, Q2 = -4.3711390001862426e-08, Q3 = -2.6718907338610155e-24;
+  const double a = fma(ws, offk, fma(p, scale, adj));       // ws = w scale, offk = trigOffset + k
+  const double n = rint(a * k2oPi);
+  double r = fma(-n, Q1, a);
+  r = fma(-n, Q2, r);
+  r = fma(-n, Q3, r);
+  *y = (float)r;
+  *q = (int)(int64_t)n & 3;
+}
+__device__ __forceinline__ void nco_angle(const NcoSrc& N, double off, int64_t k, double p, float* y, int* q) {
+  nco_angle_at(N.w * N.scale, N.scale, N.adj, off + (double)(int)k, p, y, q);   // trigOffset + (k - 1) + 1
+}
+// cos / sin of two reduced angles (packed f32 Taylor polynomials to y^9 / y^10, then the quadrant)
+__device__ __forceinline__ void nco_poly2(const float (&y)[2], const int (&q)[2], float* c, float* sn) {
   auto K = [](float v) { return ncof2{v, v}; };
+  const ncof2 yf = ncof2{y[0], y[1]};
+  const ncof2 z = yf * yf;
   ncof2 ps = __builtin_elementwise_fma(K(2.7557319e-06f), z, K(-1.9841270e-04f));
   ps = __builtin_elementwise_fma(ps, z, K(8.3333333e-03f));
   ps = __builtin_elementwise_fma(ps, z, K(-1.6666667e-01f));
@@ -227,13 +233,132 @@ __device__ __forceinline__ void nco_f32x2(const NcoSrc& N, double off, int64_t k
   pc = __builtin_elementwise_fma(pc, z, K(4.1666668e-02f));
   pc = __builtin_elementwise_fma(pc, z, K(-0.5f));
   const ncof2 cv = __builtin_elementwise_fma(pc, z, K(1.0f));
-  float cs[2], ss[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const float s0 = (q[i] & 1) ? cv[i] : sv[i], c0 = (q[i] & 1) ? sv[i] : cv[i];
-    ss[i] = (q[i] == 2 || q[i] == 3) ? -s0 : s0;
-    cs[i] = (q[i] == 1 || q[i] == 2) ? -c0 : c0;
+  for (int u = 0; u < 2; ++u) {
+    const int qq = q[u];
+    const float s0 = (qq & 1) ? cv[u] : sv[u], c0 = (qq & 1) ? sv[u] : cv[u];
+    sn[u] = (qq == 2 || qq == 3) ? -s0 : s0;
+    c[u] = (qq == 1 || qq == 2) ? -c0 : c0;
   }
-  *c = ncof2{cs[0], cs[1]};
+}
+// cos / sin (f32) of the NCO of outputs k and k + 1 (k >= 1) from p = phaseEst_{k-1}, _k
+__device__ __forceinline__ void nco_f32x2(const NcoSrc& N, double off, int64_t k, double p0, double p1, ncof2* c,
+                                          ncof2* sn) {
+  float y[2], cc[2], ss[2];
+  int q[2];
+  nco_angle(N, off, k, p0, &y[0], &q[0]);
+  nco_angle(N, off, k + 1, p1, &y[1], &q[1]);
+  nco_poly2(y, q, cc, ss);
+  *c = ncof2{cc[0], cc[1]};
   *sn = ncof2{ss[0], ss[1]};
+}
+
+// cos / sin (f32) of the NCO of four consecutive outputs i .. i+3 (i >= 2 even: the phase pairs
+// are 16-B loads), every load issued before the first use and the four angle chains
+// independent.  The angle is formed as a = (w scale) (trigOffset + k) + (p scale + adj) (scale a
+// power of two in every fmPll use: the same product as the reference's (th) scale, one rounding
+// fewer) and reduced by a 3-part pi/2 (exact multiples for |n| < 2^29: ~40 min of a 240 kS/s
+// stream before its last bits blur, as the reference's own f64 angle does).
+__device__ __forceinline__ void nco_f32x4(const NcoSrc& N, const NcoTile& T, int64_t i, float (&c)[4], float (&sn)[4]) {
+#pragma clang fp contract(off)
+  typedef double d2n __attribute__((ext_vector_type(2)));
+  const double* th = T.th + i - 2;
+  const d2n t01 = *reinterpret_cast<const d2n*>(th), t23 = *reinterpret_cast<const d2n*>(th + 2),
+            t45 = *reinterpret_cast<const d2n*>(th + 4);
+  const double st[4] = {t01.y, t23.x, t23.y, t45.x};       // phaseEst_{i-1} .. phaseEst_{i+2}
+  double p[4];
+  bool lin = false;
+  double d0[4], d1[4];
+  int64_t kk[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t j = i - 1 + e;
+    const bool h = j >= T.bound;
+    const double sh = h ? T.sh[1] : T.sh[0];
+    d0[e] = h ? T.d0[1] : T.d0[0];
+    d1[e] = h ? T.d1[1] : T.d1[0];
+    kk[e] = j - (h ? T.bound : T.kb);
+    lin = lin || d0[e] != 0.0 || d1[e] != 0.0;
+    p[e] = fma(sh, sdrnco::kP1, fma(sh, sdrnco::kP2, st[e]));
+  }
+  if (lin) {
+    d2n rr[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rr[e] = *reinterpret_cast<const d2n*>(N.resp + 2 * (kk[e] + 1));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p[e] = p[e] + (rr[e].x * d0[e] + rr[e].y * d1[e]);
+  }
+  float y[4];
+  int q[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) nco_angle(N, T.off, i + e, p[e], &y[e], &q[e]);
+  nco_poly2({y[0], y[1]}, {q[0], q[1]}, &c[0], &sn[0]);
+  nco_poly2({y[2], y[3]}, {q[2], q[3]}, &c[2], &sn[2]);
+}
+
+// ---- the fused mixer's pairs (PllJob::pair), as the receiver's filters read them ----------
+// pair[k] = 2 x[k] (cos, sin)(a_k) with a_k the NCO angle of the phase the PLL kernel stored;
+// a long call's pseudo-block b is then rotated by scale (2 pi shift_b + (A^(kk+1) d_b)_phase)
+// (the chain's turns and its linear response: the same correction nco_phase_in makes to the
+// phase, moved past the cos / sin: x cos(a + r) = (x cos a) cos r - (x sin a) sin r).
+struct MixSrc {
+  const float* pair;       // pair rows: float pairs, pstride pairs apart per stream
+  int64_t pstride;
+  double scale;            // ncoScale
+  const LongBlk* blk;      // long calls: stream s's pseudo-blocks at blk + s * blk_stride
+  int64_t blk_stride, pb;
+  int nb;
+  const double* resp;      // the response table (row 0 of A^j, sdr_pll_resp_table)
+};
+struct MixTile {
+  int64_t kb, bound;       // phases j in [kb, bound): the first block, [bound, ...): the second
+  float rc[2], rs[2];      // cos / sin of scale 2 pi shift
+  float sd0[2], sd1[2];    // scale d
+  int lin[2], rot[2];
+};
+__device__ __forceinline__ MixTile mix_tile(const MixSrc& X, int s, int64_t j0) {
+  MixTile T;
+  T.kb = 0;
+  T.bound = INT64_MAX;
+  for (int h = 0; h < 2; ++h) {
+    T.rc[h] = 1.f; T.rs[h] = 0.f; T.sd0[h] = T.sd1[h] = 0.f; T.lin[h] = T.rot[h] = 0;
+  }
+  if (X.blk == nullptr) return T;
+  const int64_t b = max(j0, (int64_t)0) / X.pb;
+  T.kb = b * X.pb;
+  T.bound = T.kb + X.pb;
+  for (int h = 0; h < 2 && b + h < X.nb; ++h) {
+    const LongBlk* B = X.blk + (int64_t)s * X.blk_stride + b + h;
+    const double turns = X.scale * B->shift;                 // the rotation, in turns
+    const double f = turns - rint(turns);
+    double sv, cv;
+    sdrnco::sincos_red<false>(sdrnco::k2Pi * f, &sv, &cv);
+    T.rc[h] = (float)cv;
+    T.rs[h] = (float)sv;
+    T.sd0[h] = (float)(X.scale * B->d[0]);
+    T.sd1[h] = (float)(X.scale * B->d[1]);
+    T.lin[h] = B->d[0] != 0.0 || B->d[1] != 0.0;
+    T.rot[h] = T.lin[h] || f != 0.0;
+  }
+  return T;
+}
+// pair k (NCO index k: phase k - 1) corrected for its pseudo-block
+__device__ __forceinline__ ncof2 mix_rot(const MixSrc& X, const MixTile& T, int64_t k, ncof2 pr) {
+  const int64_t j = k - 1;
+  if (j < 0) return pr;                                      // the carried input 0: exact
+  const int h = j >= T.bound ? 1 : 0;
+  if (!T.rot[h]) return pr;
+  float c = T.rc[h], sn = T.rs[h];
+  if (T.lin[h]) {
+    const int64_t kk = j - (h ? T.bound : T.kb);
+    const double* rr = X.resp + 2 * (kk + 1);
+    const float dl = (float)rr[0] * T.sd0[h] + (float)rr[1] * T.sd1[h];   // |dl| <= 0.3 scale rad
+    const float z = dl * dl;
+    const float cd = fmaf(z, fmaf(z, fmaf(z, -1.f / 720.f, 1.f / 24.f), -0.5f), 1.f);
+    const float sd = dl * fmaf(z, fmaf(z, 1.f / 120.f, -1.f / 6.f), 1.f);
+    const float c2 = c * cd - sn * sd, s2 = sn * cd + c * sd;
+    c = c2;
+    sn = s2;
+  }
+  return ncof2{pr.x * c - pr.y * sn, pr.y * c + pr.x * sn};
 }
