@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -71,6 +72,8 @@ struct StageJob {
   int fold;              // > 1: the leader of `fold` consecutive symmetric jobs on the same input,
                          //   computed together by fold_tile (the others get no tile workgroups)
   int nco_sin;           // PRE_NCO: the quadrature NCO (sin) instead of cos
+  int mma;               // the tiles run on the matrix cores (rx_mma_kernel); this launch keeps its zf
+  int wgs;               // rx_mma_kernel: the job's workgroups (each runs every wgs-th tile)
   NcoSrc nco;            // PRE_NCO: where the NCO comes from
 };
 
@@ -96,8 +99,8 @@ struct FeState {
 struct StageJobs {
   StageJob j[RX_MAXJ];
   int njobs, nstreams;
-  int64_t tile_blocks;        // workgroups [0, tile_blocks) compute outputs
-  int zfj[RX_MAXJ], nzf;      // then nzf * nstreams workgroups compute final states
+  int64_t tile_blocks;        // tile workgroups (after the final-state ones, rx_stage_kernel)
+  int zfj[RX_MAXJ], nzf;      // nzf * nstreams workgroups compute final states (grid front)
   FeState fe;                 // then (fe.on ? nstreams : 0) workgroups finish the FE state
 };
 
@@ -295,134 +298,399 @@ __device__ __forceinline__ void fir_tile(const StageJob& J, int s, int64_t tile,
   }
 }
 
-// F symmetric 151-tap FIRs (D = 1, no pre-op) on the SAME input, together (stage A: the pilot,
-// stereo and RDS extract band-passes of the demod, model/fmMonoBlock.py:117,151 and
-// model/fmRDSblock.py:156).  Linear-phase taps (h[k] = h[150 - k], every firwin design) let
-// the three share the folded input sums:
-//   y_f[n] = sum_{k<75} h_f[k] (x[n-k] + x[n-150+k]) + h_f[75] x[n-75]
-// -- per output 75 adds shared by the F filters and 76 F multiply-adds, where the direct form
-// takes 151 F (F = 3: 303 against 453 flops per output).  One staged image for all F (the
-// direct form staged it F times).  Lane t owns outputs m0 + 16 t + r (16, as fir_tile<151, 1>,
-// whose image layout this is), two at a time: the sums (x[n-k] + x[n-150+k], x[n+1-k] +
-// x[n-149+k]) are one v_pk_add_f32 of two sample pairs, each filter's update one v_pk_fma_f32
-// with its tap broadcast from an SGPR pair.  Pair (i, i+1) of the lane's window at i even is
-// one ds_read_b64, at i odd a ds_read2_b32 (it may span the pad after a 16-sample block); the
-// unrolled k loop reads each pair once (it is reused by the 8 output pairs over 8 k steps).
-template <int F>
-__device__ __forceinline__ void fold_tile(const StageJob* Jf, int s, int64_t tile, float* lds) {
-  using S = FirShape<151, 1, 16>;
-  constexpr int T = 151, R = 16, DELTA = S::DELTA, C = (T - 1) / 2;
+// ---- D = 1 FIR tiles on a pair image (stages A, B, E) ---------------------------------------
+// A tile's TO = 2 H outputs are two halves, [m0, m0 + H) and [m0 + H, m0 + 2 H): lane t owns
+// outputs m0 + R2 t + o and m0 + H + R2 t + o (o < R2) as the two halves of ONE packed register
+// acc[o].  The LDS image is of sample PAIRS, P[v] = (x[a + v], x[a + H + v]) with a = m0 - (T-1)
+// - DELTA, so at every tap k each packed register's operand is one aligned pair:
+//   acc[o] += h[k] * P[R2 t + DELTA + o - k + T - 1]             (one v_pk_fma_f32, h broadcast)
+// and from tap k to k + 1 the operand of o is the one o - 1 had: a lane's R2 operands live in
+// registers and slide, one new pair per tap (ds_read_b64, conflict-free: the lane stride is
+// R2 + 1 pairs, a pad pair after every R2) for R2 packed FMAs.  The taps come from LDS too
+// (broadcast ds_read_b64 of two taps, one tap pair ahead) and the new pairs two taps ahead:
+// LDS reads retire in order, so no wait in the loop drains the pipe for a scalar load (r05d:
+// an s_load per tap step with an lgkmcnt(0) after it, 34 % of stage A's wave time parked, and
+// ds_read2_b32 odd pairs with 2-way bank conflicts -- both gone here).
+// FOLD: F symmetric filters on the same input at once (stage A: the pilot, stereo and RDS
+// extract band-passes of the demod, model/fmMonoBlock.py:117,151, model/fmRDSblock.py:156) on
+// the folded sums of linear-phase taps (h[k] = h[T-1-k], every firwin design):
+//   y_f[n] = sum_{k<C} h_f[k] (x[n-k] + x[n-T+1+k]) + h_f[C] x[n-C],   C = (T-1)/2
+// -- the right operands P[... + o + k] slide the other way; one v_pk_add_f32 per output pair
+// and tap, shared by the F filters (F = 3: 75 adds + 228 multiply-adds per output, not 453).
+template <int T, int R2>
+struct PairShape {
+  static constexpr int G = 4, NT = RX_NT, H = NT * R2, TO = 2 * H;
+  static constexpr int DELTA = (G - ((T - 1) % G)) % G;             // x[a] is 16-B aligned
+  static constexpr int LV = (H + T - 1 + DELTA + G - 1) / G * G;    // pairs staged
+  __device__ static constexpr int slot(int v) { return v < DELTA ? v : v + (v - DELTA) / R2; }
+  static constexpr int NSLOT = LV + (LV - DELTA) / R2 + 1;
+  static constexpr int TAPS = (2 * NSLOT + 3) / 4 * 4;              // float offset of the tap table
+  static_assert(DELTA % 2 == 0, "pad pairs split a 4-pair chunk only in halves");
+};
+
+// acc.xy += h.{lo or hi} * x.xy, the tap broadcast by op_sel from a VGPR pair
+template <bool HI>
+__device__ __forceinline__ void pk_fma_vb(f2& acc, f2 h, f2 x) {
+  if (HI) asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(h), "v"(x));
+  else asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(h), "v"(x));
+}
+
+template <int T, int R2, int F, bool FOLD>
+__device__ __forceinline__ void pair_tile(const StageJob* Jf, int s, int64_t tile, float* lds) {
+  using S = PairShape<T, R2>;
+  constexpr int H = S::H, DELTA = S::DELTA, C = (T - 1) / 2;
+  constexpr int NK = FOLD ? C + 1 : T;                 // tap steps
+  constexpr int TP = (NK + 1) / 2 * 2;                 // tap table row (even: 8-B pairs)
+  static_assert(S::TAPS + F * TP <= RX_LDS, "pair image + taps fit the stage LDS");
+  static_assert(FOLD || F == 1, "the unfolded tile runs one filter");
+  static_assert(H >= T - 1, "zi terms only in the low half");
   const StageJob& J = Jf[0];
   const int t = threadIdx.x;
   const int64_t m0 = tile * S::TO;
   const int64_t M = J.n;
-  const int64_t n_lo = m0 - (T - 1) - DELTA;
-  const int64_t mf = m0 + (int64_t)t * R;
+  const int64_t a = m0 - (T - 1) - DELTA;              // sample of P[0].x
   const float* xb = J.x + (int64_t)s * J.x_stride;
-  if (n_lo >= 0 && n_lo + S::LG <= J.n) {
-    constexpr int NCH = S::LG / S::G, NQ = (NCH + S::NT - 1) / S::NT;
-    float4 v[NQ];
+  const float* cb = J.c ? J.c + (int64_t)s * J.x_stride : nullptr;
+  const int pre = J.pre;
+  const float g = J.gain;
+  f2* P = reinterpret_cast<f2*>(lds);
+  if (a >= 0 && a + H + S::LV <= J.n) {                // interior: 16-B loads of both halves
+    constexpr int NCH = S::LV / S::G, NQ = (NCH + S::NT - 1) / S::NT;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 lo[NQ], hi[NQ], clo[NQ], chi[NQ];
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
       const int q = t + j * S::NT;
-      if (q < NCH) v[j] = reinterpret_cast<const float4*>(xb + n_lo)[q];
+      lo[j] = hi[j] = clo[j] = chi[j] = z4;
+      if (q < NCH) {
+        lo[j] = reinterpret_cast<const float4*>(xb + a)[q];
+        hi[j] = reinterpret_cast<const float4*>(xb + a + H)[q];
+        if (pre == PRE_MIX) {
+          clo[j] = reinterpret_cast<const float4*>(cb + a)[q];
+          chi[j] = reinterpret_cast<const float4*>(cb + a + H)[q];
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
       const int q = t + j * S::NT;
       if (q < NCH) {
-        const int u = q * S::G;
-        lds[S::slot(u + 0)] = v[j].x;
-        lds[S::slot(u + 1)] = v[j].y;
-        lds[S::slot(u + 2)] = v[j].z;
-        lds[S::slot(u + 3)] = v[j].w;
+        const int v = q * S::G;
+        P[S::slot(v + 0)] = f2{pre_op(pre, lo[j].x, clo[j].x, g), pre_op(pre, hi[j].x, chi[j].x, g)};
+        P[S::slot(v + 1)] = f2{pre_op(pre, lo[j].y, clo[j].y, g), pre_op(pre, hi[j].y, chi[j].y, g)};
+        P[S::slot(v + 2)] = f2{pre_op(pre, lo[j].z, clo[j].z, g), pre_op(pre, hi[j].z, chi[j].z, g)};
+        P[S::slot(v + 3)] = f2{pre_op(pre, lo[j].w, clo[j].w, g), pre_op(pre, hi[j].w, chi[j].w, g)};
       }
     }
   } else {
-    for (int u = t; u < S::LG; u += S::NT) {
-      const int64_t nn = n_lo + u;
-      lds[S::slot(u)] = (nn >= 0 && nn < J.n) ? xb[nn] : 0.f;
+    for (int v = t; v < S::LV; v += S::NT) {
+      const int64_t n0 = a + v, n1 = a + H + v;
+      f2 p{0.f, 0.f};
+      if (n0 >= 0 && n0 < J.n) p.x = pre_op(pre, xb[n0], pre == PRE_MIX ? cb[n0] : 0.f, g);
+      if (n1 >= 0 && n1 < J.n) p.y = pre_op(pre, xb[n1], pre == PRE_MIX ? cb[n1] : 0.f, g);
+      P[S::slot(v)] = p;
     }
   }
+  float* tl = lds + S::TAPS;                           // filter f's forward taps at tl + f TP
+  for (int i = t; i < F * TP; i += S::NT) {
+    const int f = i / TP, k = i - f * TP;
+    tl[i] = k < NK ? Jf[f].taps[k] : 0.f;
+  }
   __syncthreads();
-  const float* win = lds + DELTA + S::SR * t;
-  auto addr = [](int i) { return i + 2 * (i / R); };        // window index -> float offset
-  auto pair = [&](int i) -> f2 {                             // (x_i, x_{i+1}) of the lane's window
-    if (i % 2 == 0) return *reinterpret_cast<const f2*>(win + addr(i));
-    return f2{win[addr(i)], win[addr(i + 1)]};
-  };
-  ctaps2_t g2[F];
-#pragma unroll
-  for (int f = 0; f < F; ++f) g2[f] = (ctaps2_t)Jf[f].taps;  // forward taps, (h[k], h[k+1]) pairs
-  f2 acc[F][R / 2];
+  const f2* win = P + DELTA + (R2 + 1) * t;
+  auto ld = [&](int i) -> f2 { return win[i + i / R2]; };      // window pair i (compile-time i)
+  const f2* tq = reinterpret_cast<const f2*>(tl);
+  f2 acc[F][R2];
 #pragma unroll
   for (int f = 0; f < F; ++f)
 #pragma unroll
-    for (int r2 = 0; r2 < R / 2; ++r2) acc[f][r2] = f2{0.f, 0.f};
-  // output pair r2 (outputs 2 r2, 2 r2 + 1): x[n - k] is window index 150 + 2 r2 - k and
-  // x[n - 150 + k] index 2 r2 + k.  The even k first, then the odd ones: per parity the 8 left
-  // and 8 right pairs live in registers, and each step of k by 2 loads one of each (the left
-  // pair of r2 at k is that of r2 - 1 at k - 2, the right one that of r2 + 1)
-  static_for<0, 2>([&](auto PP) {
-    constexpr int par = PP;
-    f2 lw[R / 2], rw[R / 2];
-    static_for<0, R / 2>([&](auto RR) {
-      constexpr int r2 = RR;
-      lw[r2] = pair(T - 1 + 2 * r2 - par);
-      rw[r2] = pair(2 * r2 + par);
-    });
-    static_for<0, (C + 2 - par) / 2>([&](auto KI) {
-      constexpr int k = par + 2 * KI;
-      if constexpr (KI > 0) {
-#pragma unroll
-        for (int r2 = R / 2 - 1; r2 > 0; --r2) lw[r2] = lw[r2 - 1];
-        lw[0] = pair(T - 1 - k);
-        if constexpr (k < C) {
-#pragma unroll
-          for (int r2 = 0; r2 < R / 2 - 1; ++r2) rw[r2] = rw[r2 + 1];
-          rw[R / 2 - 1] = pair(R - 2 + k);
-        }
-      }
-      static_for<0, R / 2>([&](auto RR) {
-        constexpr int r2 = RR;
-        f2 sum = lw[r2];
-        if constexpr (k < C) sum = sum + rw[r2];             // v_pk_add_f32
-        static_for<0, F>([&](auto FF) {
-          constexpr int f = FF;
-          const f2a4 hp = g2[f][k / 2];                     // (h[k & ~1], h[(k & ~1) + 1])
-          pk_fma_sb<k % 2 == 1>(acc[f][r2], f2{hp.x, hp.y}, sum);
-        });
-      });
-      // one k step's loads stay with its arithmetic: hoisted, the 3 x 76 tap pairs and the
-      // window pairs outgrew the registers (183 VGPRs, 246 SGPR spills)
-      __builtin_amdgcn_sched_barrier(0);
-    });
+    for (int o = 0; o < R2; ++o) acc[f][o] = f2{0.f, 0.f};
+  f2 lw[R2], rw[R2];                                   // operands of tap k: lw[o] = pair o - k + T - 1, rw[o] = pair o + k
+  static_for<0, R2>([&](auto O) {
+    constexpr int o = O;
+    lw[o] = ld(o + T - 1);
+    if constexpr (FOLD) rw[o] = ld(o);
   });
+  constexpr int PD = 2;                                // new pairs read PD taps ahead
+  f2 ln[PD], rn[PD], tc[F], tn[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) tc[f] = tq[f * (TP / 2)];
+  static_for<1, PD>([&](auto JJ) {
+    constexpr int j = JJ;
+    if constexpr (j < NK) ln[j % PD] = ld(T - 1 - j);
+    if constexpr (FOLD && j < C) rn[j % PD] = ld(R2 - 1 + j);
+  });
+  static_for<0, NK>([&](auto KK) {
+    constexpr int k = KK;
+    if constexpr (k + PD < NK) ln[k % PD] = ld(T - 1 - (k + PD));
+    if constexpr (FOLD && k + PD < C) rn[k % PD] = ld(R2 - 1 + k + PD);
+    if constexpr (k % 2 == 0 && k + 2 < NK) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) tn[f] = tq[f * (TP / 2) + k / 2 + 1];
+    }
+    static_for<0, R2>([&](auto O) {
+      constexpr int o = O;
+      if constexpr (FOLD) {
+        f2 sum = lw[o];
+        if constexpr (k < C) sum = sum + rw[o];        // v_pk_add_f32
+#pragma unroll
+        for (int f = 0; f < F; ++f) pk_fma_vb<k % 2 == 1>(acc[f][o], tc[f], sum);
+      } else {
+        pk_fma_vb<k % 2 == 1>(acc[0][o], tc[0], lw[o]);
+      }
+    });
+    if constexpr (k + 1 < NK) {
+#pragma unroll
+      for (int o = R2 - 1; o > 0; --o) lw[o] = lw[o - 1];
+      lw[0] = ln[(k + 1) % PD];
+      if constexpr (FOLD && k + 1 < C) {
+#pragma unroll
+        for (int o = 0; o < R2 - 1; ++o) rw[o] = rw[o + 1];
+        rw[R2 - 1] = rn[(k + 1) % PD];
+      }
+      if constexpr (k % 2 == 1) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) tc[f] = tn[f];
+      }
+    }
+    // one tap step's reads stay with its arithmetic (hoisted, they outgrow the registers)
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  const int64_t nlo = m0 + (int64_t)R2 * t, nhi = nlo + H;
 #pragma unroll
   for (int f = 0; f < F; ++f) {
     const StageJob& Jj = Jf[f];
-    float o[R];
+    float ol[R2], oh[R2];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int64_t nn = mf + r;                           // lfilter zi: the block's first T - 1 outputs
+    for (int o = 0; o < R2; ++o) {
+      const int64_t nn = nlo + o;                      // lfilter zi: the block's first T - 1 outputs
       const float z = (Jj.zi != nullptr && nn < T - 1) ? (float)Jj.zi[(int64_t)s * Jj.zi_stride + nn] : 0.f;
-      o[r] = ((r & 1) ? acc[f][r / 2].y : acc[f][r / 2].x) + z;
+      ol[o] = acc[f][o].x + z;
+      oh[o] = acc[f][o].y;
     }
     float* yb = Jj.y + (int64_t)s * Jj.y_stride;
-    if (mf + R <= M) {
+    auto put = [&](float* row, int64_t n0, const float* v) {
+      if (n0 + R2 <= M) {
+        if constexpr (R2 % 4 == 0) {
 #pragma unroll
-      for (int r = 0; r < R; r += 4) *reinterpret_cast<float4*>(yb + mf + r) = make_float4(o[r], o[r + 1], o[r + 2], o[r + 3]);
-    } else {
+          for (int o = 0; o < R2; o += 4) *reinterpret_cast<float4*>(row + n0 + o) = make_float4(v[o], v[o + 1], v[o + 2], v[o + 3]);
+        } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (mf + r < M) yb[mf + r] = o[r];
-    }
-    if (Jj.yh != nullptr) {
+          for (int o = 0; o < R2; o += 2) *reinterpret_cast<float2*>(row + n0 + o) = make_float2(v[o], v[o + 1]);
+        }
+      } else {
+#pragma unroll
+        for (int o = 0; o < R2; ++o)
+          if (n0 + o < M) row[n0 + o] = v[o];
+      }
+    };
+    put(yb, nlo, ol);
+    put(yb, nhi, oh);
+    if (Jj.yh != nullptr) {                            // host rows are packed: scalar stores
       float* hb = Jj.yh + (int64_t)s * Jj.yh_stride;
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (mf + r < M) hb[mf + r] = o[r];
+      for (int o = 0; o < R2; ++o) {
+        if (nlo + o < M) hb[nlo + o] = ol[o];
+        if (nhi + o < M) hb[nhi + o] = oh[o];
+      }
     }
+  }
+}
+
+// ---- D = 1 FIRs on the matrix cores (stages A, B, E at span sizes) ------------------------
+// y[n] = sum_k h[k] x[n-k] for 256 consecutive outputs n = n0 + 16 c + b (c, b < 16) is the
+// product Y = A X of the 16 x 32 KS Toeplitz tap matrix A[b][j] = h[b + KOFF - j] (zero
+// outside 0 <= b + KOFF - j < T) and the Hankel window matrix X[j][c] = x[n0 + 16 c + j - KOFF]:
+// KS v_mfma_f32_16x16x32_f16 steps, lane l holding A[l & 15][8 (l >> 4) + 0..7] (the taps: in
+// registers for the whole launch), X[32 s + 8 (l >> 4) + 0..7][l & 15] (8 consecutive samples:
+// one ds_read_b128 of the staged window, conflict-free) and outputs n0 + 16 (l & 15) + 4 (l >> 4)
+// + 0..3 (one float4 store).  f32 accuracy from f16 operands: every x and h is split as
+// v = hi + lo / 2048 (hi = f16(v), lo = f16((v - hi) 2048): 22 significant bits) and
+//   y = sum(h_hi x_hi) + (sum(h_hi x_lo) + sum(h_lo x_hi)) / 2048
+// with f32 accumulation -- three MFMAs per step, the h_lo x_lo term (2^-22) dropped
+// (tests/test_mma_fir.py: the split form's error against f64 lfilter is the f32 direct form's).
+// F filters on the same input share the staged window and the X fragments (stage A's pilot,
+// stereo and RDS extract band-passes: F = 3).
+// Every wave works alone -- no workgroup barrier after the tap fragments are built: a wave
+// stages its own MM_WT-output window (MM_WT + 16 + 32 (KS - 1) samples, hi and lo) into its own
+// LDS slice, runs its MFMAs, stores, and moves to its next window, whose samples it loaded
+// into registers while the MFMAs ran.  Persistent: each wave owns every nw-th window of its job.
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+constexpr int MM_NB = 4;                          // 256-output column blocks per wave window
+constexpr int MM_WT = MM_NB * 256;                // outputs per wave window
+constexpr float MM_LO = 2048.f;                   // the lo parts' scale
+constexpr int MM_MIN_WIN = 32;                    // a row of fewer windows stays on the VALU tiles
+
+template <int T>
+struct MmaShape {
+  static constexpr int KS = (16 + T - 1 + 31) / 32;                  // K steps of 32
+  static constexpr int KOFF = (T - 1 + 7) / 8 * 8;                   // window start: 16-B aligned
+  static constexpr int LU = MM_WT + 16 + 32 * (KS - 1);              // staged samples per window
+  static constexpr int NCH = LU / 4, NQ = (NCH + 63) / 64;           // 16-B chunks, per lane
+  static_assert(KOFF >= T - 1 && KOFF <= 32 * KS - 16, "every tap inside the K steps");
+  static_assert(LU % 8 == 0, "16-B fragments");
+};
+constexpr int MM_LU_MAX = MmaShape<151>::LU;
+constexpr int MM_TAPS_MAX = 3 * 151;
+template <int FMAX> constexpr int mm_waves_per_cu() { return FMAX == 1 ? 12 : 8; }   // the VGPR limit
+
+struct MmHL { _Float16 hi, lo; };
+__device__ __forceinline__ MmHL mm_split(float v) {
+  const _Float16 h = (_Float16)v;
+  return MmHL{h, (_Float16)((v - (float)h) * MM_LO)};
+}
+// four samples at once: v_cvt_pk_f16_f32 pairs, the residuals as packed f32 ops
+__device__ __forceinline__ void mm_split4(float4 x, h4v* hi, h4v* lo) {
+  const f2 a{x.x, x.y}, c{x.z, x.w};
+  const h2v ha = __builtin_convertvector(a, h2v), hc = __builtin_convertvector(c, h2v);
+  const f2 ra = (a - __builtin_convertvector(ha, f2)) * MM_LO, rc = (c - __builtin_convertvector(hc, f2)) * MM_LO;
+  const h2v la = __builtin_convertvector(ra, h2v), lc = __builtin_convertvector(rc, h2v);
+  *hi = h4v{ha.x, ha.y, hc.x, hc.y};
+  *lo = h4v{la.x, la.y, lc.x, lc.y};
+}
+
+// A buffer descriptor over bytes [p, p + bytes) from wave-uniform values (readfirstlane: the
+// compiler cannot prove a wave-id-derived address uniform and would wrap every access in a
+// waterfall loop).  Raw buffer accesses outside it read 0 / are dropped by the hardware.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mm_rsrc(const void* p, int64_t bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo), 0, nb, 0x00020000);
+}
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+// wave w of job group Jf: windows gw, gw + nw, ... of the job's (stream, window) list.  Every
+// global access is a raw buffer access (the range check zero-fills samples outside the row and
+// drops stores past its end: no edge paths) and unconditional, so the compiler's vmcnt waits
+// count exactly; the loads of window i + 2 go out after window i's stores, and window i + 1's
+// staging waits for its own loads only -- never for a store.
+template <int T, int F>
+__device__ __forceinline__ void mma_run(const StageJob* Jf, int S, int64_t gw, int64_t nw, _Float16* img,
+                                        const float* tap_s) {
+  using Sh = MmaShape<T>;
+  constexpr int KS = Sh::KS, KOFF = Sh::KOFF, LU = Sh::LU, NCH = Sh::NCH, NQ = Sh::NQ;
+  static_assert(F * T <= MM_TAPS_MAX && LU <= MM_LU_MAX, "the window fits the kernel's LDS");
+  static_assert(NQ >= 2 && 1024 * (NQ - 2) < 4096, "chunk offsets: immediates up to NQ - 2");
+  const StageJob& J = Jf[0];
+  const int l = threadIdx.x & 63;
+  const int b = l & 15, g = l >> 4;
+  const int64_t wins = (J.n + MM_WT - 1) / MM_WT;   // per stream
+  const int64_t total = wins * S;
+  const int pre = J.pre;
+  _Float16* xh = img;
+  _Float16* xl = img + LU;
+  // the tap fragments: lane l holds A[b = l & 15][j = 32 st + 8 (l >> 4) + e] = h[b + KOFF - j]
+  h8v ah[F][KS], al[F][KS];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int st = 0; st < KS; ++st)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = b + KOFF - (32 * st + 8 * g + e);
+        const MmHL p = mm_split((k >= 0 && k < T) ? tap_s[f * T + k] : 0.f);
+        ah[f][st][e] = p.hi;
+        al[f][st][e] = p.lo;
+      }
+  // window i's samples: 16-B chunks l + 64 j of x[m0 - KOFF ...], at byte offset
+  // 4 (m0 - KOFF) + 16 l + 1 024 j of the stream's row (negative: before the row, read as 0)
+  constexpr int PFD = F == 1 ? 1 : 2;                // windows in flight (F = 1: four waves per SIMD cover it)
+  u4v v[PFD][NQ];
+  auto load = [&](int64_t i, u4v* vv) {
+    const int s = (int)(i / wins);
+    const int64_t m0 = (i - s * wins) * MM_WT;
+    const __amdgpu_buffer_rsrc_t r = mm_rsrc(J.x + (int64_t)s * J.x_stride, J.n * 4);
+    const int o = (int)(4 * (m0 - KOFF)) + 16 * l;
+#pragma unroll
+    for (int j = 0; j < NQ - 1; ++j) vv[j] = __builtin_amdgcn_raw_buffer_load_b128(r, o + 1024 * j, 0, 0);
+    vv[NQ - 1] = __builtin_amdgcn_raw_buffer_load_b128(r, o + 1024 * (NQ - 1), 0, 0);
+  };
+#pragma unroll
+  for (int d = 0; d < PFD; ++d) load(gw + d * nw, v[d]);   // (past the job's end: loads of 0 bytes' worth, unused)
+  for (int64_t i = gw; i < total; i += nw) {
+    const int s = (int)(i / wins);
+    const int64_t m0 = (i - s * wins) * MM_WT;
+    // stage: the wave's own LDS slice (its previous window's fragment reads retired in order)
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const int q = l + j * 64;
+      if (q < NCH) {
+        float4 x = __builtin_bit_cast(float4, v[0][j]);
+        if (pre == PRE_SQUARE) x = make_float4(x.x * x.x, x.y * x.y, x.z * x.z, x.w * x.w);
+        h4v hv, lv;
+        mm_split4(x, &hv, &lv);
+        *reinterpret_cast<h4v*>(xh + 4 * q) = hv;
+        *reinterpret_cast<h4v*>(xl + 4 * q) = lv;
+      }
+    }
+#pragma unroll
+    for (int d = 0; d + 1 < PFD; ++d)
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) v[d][j] = v[d + 1][j];
+    // the column blocks' K steps as one unrolled sequence, the X fragments of step q + 1 read
+    // while step q's MFMAs run
+    constexpr int NSTEP = MM_NB * KS;
+    auto frag = [&](int q, h8v* bh, h8v* bl) {
+      const int u = 256 * (q / KS) + 16 * b + 8 * g + 32 * (q % KS);
+      *bh = *reinterpret_cast<const h8v*>(xh + u);
+      *bl = *reinterpret_cast<const h8v*>(xl + u);
+    };
+    h8v fh[2], fl[2];
+    f4v acc_h[F], acc_c[F];
+    const bool head = m0 < T - 1;                    // the block's first T - 1 outputs: + lfilter zi
+    __amdgpu_buffer_rsrc_t ry[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) ry[f] = mm_rsrc(Jf[f].y + (int64_t)s * Jf[f].y_stride + m0, (J.n - m0) * 4);
+    frag(0, &fh[0], &fl[0]);
+    static_for<0, NSTEP>([&](auto Q) {
+      constexpr int q = Q, st = q % KS, c = q / KS;
+      if constexpr (q + 1 < NSTEP) frag(q + 1, &fh[(q + 1) % 2], &fl[(q + 1) % 2]);
+      if constexpr (st == 0) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) acc_h[f] = acc_c[f] = f4v{0.f, 0.f, 0.f, 0.f};
+      }
+      const h8v bh = fh[q % 2], bl = fl[q % 2];
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        acc_h[f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[f][st], bh, acc_h[f], 0, 0, 0);
+        acc_c[f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[f][st], bl, acc_c[f], 0, 0, 0);
+        acc_c[f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[f][st], bh, acc_c[f], 0, 0, 0);
+      }
+      if constexpr (st == KS - 1) {
+        const int ol = 256 * c + 16 * b + 4 * g;     // this lane's 4 outputs: m0 + ol ...
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          const StageJob& Jj = Jf[f];
+          float4 o = make_float4(fmaf(acc_c[f][0], 1.f / MM_LO, acc_h[f][0]), fmaf(acc_c[f][1], 1.f / MM_LO, acc_h[f][1]),
+                                 fmaf(acc_c[f][2], 1.f / MM_LO, acc_h[f][2]), fmaf(acc_c[f][3], 1.f / MM_LO, acc_h[f][3]));
+          if (head && Jj.zi != nullptr) {            // uniform: the stream's first window only
+            const double* zi = Jj.zi + (int64_t)s * Jj.zi_stride;
+            const int64_t n0 = m0 + ol;
+            if (n0 + 0 < T - 1) o.x += (float)zi[n0 + 0];
+            if (n0 + 1 < T - 1) o.y += (float)zi[n0 + 1];
+            if (n0 + 2 < T - 1) o.z += (float)zi[n0 + 2];
+            if (n0 + 3 < T - 1) o.w += (float)zi[n0 + 3];
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, o), ry[f], 4 * ol, 0, 0);
+          if (Jj.yh != nullptr) {                    // host rows (per-call runs): plain stores
+            float* hb = Jj.yh + (int64_t)s * Jj.yh_stride;
+            const int64_t n0 = m0 + ol;
+            const float ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n0 + r < J.n) hb[n0 + r] = ov[r];
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    const int64_t nf = i + PFD * nw;                 // after this window's stores: see above
+    if (nf < total) load(nf, v[PFD - 1]);
   }
 }
 
@@ -618,13 +886,16 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
   static_assert(!NCO || T > 0, "PRE_NCO jobs run on the compile-time tiles");
   static_assert(!FOLD || (T == 151 && !NCO), "fold groups: 151 taps, no NCO jobs");
   __shared__ __attribute__((aligned(16))) float lds[RX_LDS];
-  const int64_t b = blockIdx.x;
-  if (b >= P.tile_blocks) {
-    const int64_t zb = b - P.tile_blocks;
-    if (zb < (int64_t)P.nzf * P.nstreams) zf_block<NCO>(P, zb, lds);
-    else fe_state_block(P.fe, (int)(zb - (int64_t)P.nzf * P.nstreams), lds);
+  // the final-state workgroups first: each is a short serial f64 pass, dispatched ahead of the
+  // tiles it would otherwise trail at the end of the launch
+  const int64_t nzb = (int64_t)P.nzf * P.nstreams, nfront = nzb + (P.fe.on ? P.nstreams : 0);
+  if ((int64_t)blockIdx.x < nfront) {
+    const int64_t zb = blockIdx.x;
+    if (zb < nzb) zf_block<NCO>(P, zb, lds);
+    else fe_state_block(P.fe, (int)(zb - nzb), lds);
     return;
   }
+  const int64_t b = blockIdx.x - nfront;
   int q = 0;
   for (int i = 1; i < P.njobs; ++i)
     if (b >= P.j[i].b0) q = i;
@@ -637,13 +908,19 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
     return;
   }
   if constexpr (FOLD) {
-    if (J.fold == 3) { fold_tile<3>(&J, s, tile, lds); return; }
-    if (J.fold == 2) { fold_tile<2>(&J, s, tile, lds); return; }
+    if (J.fold == 3) { pair_tile<151, 8, 3, true>(&J, s, tile, lds); return; }
+    if (J.fold == 2) { pair_tile<151, 8, 2, true>(&J, s, tile, lds); return; }
   }
   if constexpr (T > 0) {
     if (J.D == 1) {
-      if (J.small) fir_tile<T, 1, 4, NCO>(J, s, tile, lds);
-      else fir_tile<T, 1, 16, NCO>(J, s, tile, lds);
+      if (NCO && J.pre == PRE_NCO) {                 // the mixers forming their NCO
+        if (J.small) fir_tile<T, 1, 4, NCO>(J, s, tile, lds);
+        else fir_tile<T, 1, 16, NCO>(J, s, tile, lds);
+      } else if (J.small) {
+        pair_tile<T, 2, 1, false>(&J, s, tile, lds);
+      } else {
+        pair_tile<T, 8, 1, false>(&J, s, tile, lds);
+      }
       return;
     }
     if (J.D == 5) { fir_tile<T, 5, 4, NCO>(J, s, tile, lds); return; }
@@ -651,8 +928,46 @@ __global__ __launch_bounds__(RX_NT) void rx_stage_kernel(StageJobs P) {
   fir_tile_any(J, s, tile, lds);
 }
 
+// The matrix-core FIR launch of one tap class and group width: job q (a group of F = fold
+// filters on one input) owns workgroups [b0, b0 + wgs), i.e. waves 4 b0 ... 4 (b0 + wgs) - 1,
+// each running every (4 wgs)-th window of the job's streams x windows (mma_run).
+template <int T, int FMAX>
+__global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(mm_waves_per_cu<FMAX>() / 4)))
+void rx_mma_kernel(StageJobs P) {
+  __shared__ __attribute__((aligned(16))) _Float16 img[4][2 * MmaShape<T>::LU];
+  __shared__ float tap_s[FMAX * T];
+  const int64_t b = blockIdx.x;
+  int q = 0;
+  for (int i = 1; i < P.njobs; ++i)
+    if (b >= P.j[i].b0) q = i;
+  const StageJob& J = P.j[q];
+  const int F = J.fold;
+  for (int i = threadIdx.x; i < F * T; i += RX_NT) tap_s[i] = P.j[q + i / T].taps[i % T];
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  const int64_t gw = (b - J.b0) * 4 + w, nw = (int64_t)J.wgs * 4;
+  if constexpr (FMAX == 1) {
+    mma_run<T, 1>(&J, P.nstreams, gw, nw, img[w], tap_s);
+  } else {
+    if (F == 3) mma_run<T, 3>(&J, P.nstreams, gw, nw, img[w], tap_s);
+    else mma_run<T, 2>(&J, P.nstreams, gw, nw, img[w], tap_s);
+  }
+}
+
+// The matrix-core path (SDR_RX_MMA=0 in the environment: the VALU pair tiles throughout)
+bool mma_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SDR_RX_MMA");
+    return e == nullptr || std::strcmp(e, "0") != 0;
+  }();
+  return on;
+}
+
 // outputs per tile of a job in a launch of tap class `key` (as rx_stage_kernel<key> picks the tile)
 int64_t tile_outputs(const StageJob& j, int key) {
+  static_assert(PairShape<151, 2>::TO == FirShape<151, 1, 4>::TO && PairShape<151, 8>::TO == FirShape<151, 1>::TO &&
+                PairShape<101, 2>::TO == FirShape<101, 1, 4>::TO && PairShape<101, 8>::TO == FirShape<101, 1>::TO,
+                "pair tiles and the mixers' fir tiles cover the same outputs");
   if (j.kind == JK_FIR && key == 151 && j.D == 1 && j.small) return FirShape<151, 1, 4>::TO;
   if (j.kind == JK_FIR && key == 101 && j.D == 1 && j.small) return FirShape<101, 1, 4>::TO;
   if (j.kind == JK_FIR && key == 151 && j.D == 1) return FirShape<151, 1>::TO;
@@ -665,6 +980,71 @@ int64_t tile_outputs(const StageJob& j, int key) {
 // Launch the jobs of one stage, one launch per tap-count class.
 hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const FeState* fe = nullptr) {
   auto cls = [](const StageJob& j) { return (j.kind == JK_FIR && (j.T == 101 || j.T == 151)) ? j.T : 0; };
+  // matrix-core FIR launches first: D = 1 filters of 101 / 151 taps on 16-B aligned rows of at
+  // least MM_MIN_WIN windows per stream (spans; per-block calls keep the VALU tiles' finer
+  // grain) -- decided per job from its length alone, so a stream's outputs do not depend on how
+  // many streams share the launch.  Their final states stay with the VALU launch below (tiles = 0).
+  auto al16 = [](const void* p, int64_t stride) { return p != nullptr && ((uintptr_t)p % 16) == 0 && stride % 4 == 0; };
+  auto mmable = [&](const StageJob& j, int key) {
+    return j.kind == JK_FIR && j.D == 1 && j.T == key && (j.pre == PRE_NONE || j.pre == PRE_SQUARE) &&
+           al16(j.x, j.x_stride) && al16(j.y, j.y_stride) && j.n >= (int64_t)MM_MIN_WIN * MM_WT &&
+           j.n % 4 == 0 && j.n < (int64_t)1 << 28;      // (buffer ranges: 32-bit byte offsets)
+  };
+  for (StageJob& j : jobs) j.mma = 0;
+  for (int key : {151, 101})
+    for (int wide : {1, 0}) {                        // groups of 2-3 filters / single filters
+      if (!mma_enabled()) break;
+      StageJobs Q{};
+      Q.nstreams = S;
+      std::vector<size_t> members;
+      for (size_t ji = 0; ji < jobs.size(); ++ji) {
+        if (!mmable(jobs[ji], key) || jobs[ji].mma) continue;
+        int g = 1;                                   // jobs on the same input: one group (<= 3)
+        while (jobs[ji].pre == PRE_NONE && g < 3 && ji + g < jobs.size() && mmable(jobs[ji + g], key) &&
+               jobs[ji + g].pre == PRE_NONE && jobs[ji + g].x == jobs[ji].x && jobs[ji + g].x_stride == jobs[ji].x_stride &&
+               jobs[ji + g].n == jobs[ji].n)
+          ++g;
+        if ((g > 1) != (wide == 1) || Q.njobs + g > RX_MAXJ) {
+          ji += g - 1;
+          continue;
+        }
+        for (int m = 0; m < g; ++m) {
+          StageJob j = jobs[ji + m];
+          j.fold = m == 0 ? g : 0;
+          j.zf = nullptr;
+          j.wgs = 0;
+          Q.j[Q.njobs++] = j;
+          members.push_back(ji + m);
+        }
+        ji += g - 1;
+      }
+      if (Q.njobs == 0) continue;
+      // persistent waves: mm_waves_per_cu per CU over the launch, shared by the groups in
+      // proportion to their windows (every group at least one workgroup)
+      const int64_t waves = 256 * (wide ? mm_waves_per_cu<3>() : mm_waves_per_cu<1>());
+      int64_t wins = 0;
+      for (int i = 0; i < Q.njobs; ++i)
+        if (Q.j[i].fold > 0) wins += (Q.j[i].n + MM_WT - 1) / MM_WT * S;
+      const int64_t per = std::max<int64_t>(1, (wins + waves - 1) / waves);     // windows per wave
+      int64_t blocks = 0;
+      for (int i = 0; i < Q.njobs; ++i) {
+        StageJob& j = Q.j[i];
+        j.b0 = blocks;
+        if (j.fold > 0) {
+          const int64_t jw = (j.n + MM_WT - 1) / MM_WT * S;
+          j.wgs = (int)std::max<int64_t>(1, (jw + 4 * per - 1) / (4 * per));
+          blocks += j.wgs;
+        }
+      }
+      Q.tile_blocks = blocks;
+      if (key == 151 && wide) hipLaunchKernelGGL((rx_mma_kernel<151, 3>), dim3((unsigned)blocks), dim3(RX_NT), 0, st, Q);
+      else if (key == 151) hipLaunchKernelGGL((rx_mma_kernel<151, 1>), dim3((unsigned)blocks), dim3(RX_NT), 0, st, Q);
+      else if (wide) hipLaunchKernelGGL((rx_mma_kernel<101, 3>), dim3((unsigned)blocks), dim3(RX_NT), 0, st, Q);
+      else hipLaunchKernelGGL((rx_mma_kernel<101, 1>), dim3((unsigned)blocks), dim3(RX_NT), 0, st, Q);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      for (size_t m : members) jobs[m].mma = 1;
+    }
   bool fe_done = fe == nullptr || !fe->on;
   for (int key : {151, 101, 0}) {
     StageJobs P{};
@@ -675,14 +1055,14 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
     // in 1 024-output tiles (4 per lane): latency-bound launches get 4x the waves
     int64_t big = 0;
     for (const StageJob& j : jobs)
-      if (cls(j) == key) {
+      if (cls(j) == key && !j.mma) {
         const int64_t nout = j.kind == JK_RESAMPLE ? (j.n * j.U + j.D - 1) / j.D : (j.n + j.D - 1) / j.D;
         big += (nout + 1023) / 1024 * S;
       }
     const bool small = key > 0 && big < 10 * 256;
     // symmetric 151-tap D = 1 jobs on one input, consecutive in the list: folded together (fold_tile)
     auto foldable = [&](const StageJob& a) {
-      return key == 151 && !small && a.kind == JK_FIR && a.D == 1 && a.pre == PRE_NONE && a.T == 151 && a.sym;
+      return key == 151 && !small && !a.mma && a.kind == JK_FIR && a.D == 1 && a.pre == PRE_NONE && a.T == 151 && a.sym;
     };
     int follow = 0;                                  // jobs left in the current fold group
     for (size_t ji = 0; ji < jobs.size(); ++ji) {
@@ -703,7 +1083,7 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
       const bool follower = follow > 0 && j.fold == 0;
       if (follow > 0) --follow;
       const int64_t to = tile_outputs(j, key);
-      j.tiles = follower ? 0 : (int)std::max<int64_t>((nout + to - 1) / to, 0);
+      j.tiles = (follower || j.mma) ? 0 : (int)std::max<int64_t>((nout + to - 1) / to, 0);
       j.b0 = blocks;
       blocks += (int64_t)j.tiles * S;
       if (j.zf != nullptr && j.T > 1) P.zfj[P.nzf++] = P.njobs;
