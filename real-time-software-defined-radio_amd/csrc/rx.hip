@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "sdr_ctx.h"
@@ -536,7 +537,7 @@ struct MmaShape {
 };
 constexpr int MM_LU_MAX = MmaShape<151>::LU;
 constexpr int MM_TAPS_MAX = 3 * 151;
-template <int FMAX> constexpr int mm_waves_per_cu() { return FMAX == 1 ? 12 : 8; }   // the VGPR limit
+template <int FMAX> constexpr int mm_waves_per_cu() { return FMAX == 1 ? 16 : 8; }   // the VGPR limit
 
 struct MmHL { _Float16 hi, lo; };
 __device__ __forceinline__ MmHL mm_split(float v) {
@@ -944,13 +945,179 @@ void rx_mma_kernel(StageJobs P) {
   const int F = J.fold;
   for (int i = threadIdx.x; i < F * T; i += RX_NT) tap_s[i] = P.j[q + i / T].taps[i % T];
   __syncthreads();
-  const int w = threadIdx.x >> 6;
+  // the wave id, provably uniform (readfirstlane): everything derived from it -- stream, window,
+  // row addresses, pseudo-block records -- stays in scalar registers
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int64_t gw = (b - J.b0) * 4 + w, nw = (int64_t)J.wgs * 4;
   if constexpr (FMAX == 1) {
     mma_run<T, 1>(&J, P.nstreams, gw, nw, img[w], tap_s);
   } else {
     if (F == 3) mma_run<T, 3>(&J, P.nstreams, gw, nw, img[w], tap_s);
     else mma_run<T, 2>(&J, P.nstreams, gw, nw, img[w], tap_s);
+  }
+}
+
+// ---- stage C's stereo mixer + LPF + [::5] + L/R combiner on the matrix cores (spans) -------
+// y[m] = sum_k h[k] u[5 m - k], u[i] = (x[i] nco[i]) g (model/fmMonoBlock.py:155-162, the NCO
+// formed from the pilot PLL's phases, sdr_nco.h): the 16 outputs m = m0 + 16 c + b of column c
+// of a 256-output window are Y = A X with A[b][j] = h[5 b + 151 - j] (zero outside the taps)
+// and X[j][c] = u[5 m0 + 80 c + j - 151], j < 256 -- the Hankel form of the composite kernel
+// (columns 80 inputs apart, odd window starts: each chunk's four phases are two aligned
+// pairs), one channel; A's 8 K steps built once per workgroup into LDS.  The epilogue is the
+// combiner (fmMonoBlock.py:166-170): L = (mono + y) / 2, R = (mono - y) / 2.
+constexpr int SM_KS = 8, SM_KOFF = 151, SM_D = 5;
+constexpr int SM_LU = 80 * 15 + 32 * SM_KS;         // 1 456 inputs staged per window
+constexpr int SM_NG = SM_LU / 4, SM_NQ = (SM_NG + 63) / 64;
+constexpr int SM_WPE = 3;                           // waves per SIMD (registers)
+constexpr int SM_WGS = SM_WPE * 256;                // persistent workgroups
+static_assert(SM_D * 15 + SM_KOFF < 32 * SM_KS && SM_KOFF >= 150 && SM_KOFF % 2 == 1, "stereo LPF window");
+
+__global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(SM_WPE))) void rx_stereomm_kernel(StageJobs P, int wgs) {
+  const StageJob& J = P.j[0];                        // (in the kernel arguments: no private copy)
+  const int S = P.nstreams;
+  __shared__ __attribute__((aligned(16))) _Float16 img[4][2 * SM_LU];   // per wave: hi, lo
+  __shared__ __attribute__((aligned(16))) h8v afr[2][SM_KS][64];         // A fragments: hi, lo
+  constexpr int T = 151;
+  for (int idx = threadIdx.x; idx < SM_KS * 64; idx += RX_NT) {
+    const int st = idx >> 6, ln = idx & 63, bb = ln & 15, gg = ln >> 4;
+    h8v hi, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = SM_D * bb + SM_KOFF - (32 * st + 8 * gg + e);
+      const MmHL p = mm_split((k >= 0 && k < T) ? J.taps[k] : 0.f);
+      hi[e] = p.hi;
+      lo[e] = p.lo;
+    }
+    afr[0][st][ln] = hi;
+    afr[1][st][ln] = lo;
+  }
+  __syncthreads();
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: see rx_mma_kernel
+  const int l = threadIdx.x & 63, b = l & 15, g = l >> 4;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + w, nw = (int64_t)wgs * 4;
+  _Float16* xh = img[w];
+  _Float16* xl = xh + SM_LU;
+  const int64_t n = J.n, M = (J.n + SM_D - 1) / SM_D;
+  const int64_t wins = (M + 255) / 256;              // per stream
+  const int64_t total = wins * S;
+  const float gain = J.gain;
+  // A window's geometry and pseudo-block records; every window (row ends included: mix_eval)
+  // takes the same branch-free path.  The chunks' loads run PD chunks ahead of their arithmetic
+  // through the window seams: the last PD chunks of a window issue the next window's first ones
+  // (its records were read a window earlier), so a wave's stream of chunks never waits for a
+  // load it issued in its own window.
+  static_assert((SM_D * 256 - SM_KOFF) % 4 == 1 && SM_KOFF % 4 == 3, "chunks start at 1 mod 4 (mix_load)");
+  struct Win { int s; int64_t m0, a; const float* x; NcoTile nt; bool lin; };
+  auto winfo = [&](int64_t i, Win* v) {
+    v->s = (int)(i / wins);
+    const int64_t W = i - (int64_t)v->s * wins;
+    v->m0 = 256 * W;
+    v->a = SM_D * v->m0 - SM_KOFF;                   // input of element 0
+    v->x = J.x + (int64_t)v->s * J.x_stride;
+    v->nt = nco_tile(J.nco, v->s, max<int64_t>(v->a, 1) - 1);
+    v->lin = nco_tile_lin(v->nt);
+  };
+  constexpr int PD = 2;
+  static_assert(SM_NQ % PD == 0, "ring slots line up across windows");
+  MixLd gb[PD];
+  auto ldg = [&](const Win& v, int j, MixLd* gg) {
+    mix_load(J.nco, v.nt, v.x, v.a + 4 * min(l + 64 * j, SM_NG - 1), v.lin, gg);
+  };
+  Win cur{}, nxt{};
+  if (gw < total) {
+    winfo(gw, &cur);
+    static_for<0, PD>([&](auto D) { ldg(cur, D, &gb[D]); });
+  }
+  for (int64_t i = gw; i < total; i += nw) {
+    const bool more = i + nw < total;
+    if (more) winfo(i + nw, &nxt);
+    const int s = cur.s;
+    const int64_t m0 = cur.m0, a = cur.a;
+    {
+      const NcoWin nwin = nco_win(J.nco, cur.nt, a);
+      const bool lin = cur.lin;
+      const float c0 = J.nco.nco_i[(int64_t)s * J.nco.out_stride];   // the carried NCO[0]
+      static_for<0, SM_NQ>([&](auto JJ) {
+        constexpr int j = JJ;
+        const int q = min(l + 64 * j, SM_NG - 1);
+        const MixLd gc = gb[j % PD];
+        if constexpr (j + PD < SM_NQ) ldg(cur, j + PD, &gb[j % PD]);
+        else ldg(more ? nxt : cur, j + PD - SM_NQ, &gb[j % PD]);
+        float xv[4], c[4], sn[4];
+        mix_eval(cur.nt, nwin, a + 4 * q, n, gc, lin, c0, 0.f, xv, c, sn);
+        h4v hv, lv;
+        mm_split4(make_float4(pre_op(PRE_NCO, xv[0], c[0], gain), pre_op(PRE_NCO, xv[1], c[1], gain),
+                              pre_op(PRE_NCO, xv[2], c[2], gain), pre_op(PRE_NCO, xv[3], c[3], gain)), &hv, &lv);
+        *reinterpret_cast<h4v*>(xh + 4 * q) = hv;
+        *reinterpret_cast<h4v*>(xl + 4 * q) = lv;
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+    f4v acc_h = f4v{0.f, 0.f, 0.f, 0.f}, acc_c = acc_h;
+    struct Fr { h8v xh, xl, ah, al; };
+    Fr fr[2];
+    auto frag = [&](int st, Fr* d) {
+      const int u = 80 * b + 32 * st + 8 * g;
+      d->xh = *reinterpret_cast<const h8v*>(xh + u);
+      d->xl = *reinterpret_cast<const h8v*>(xl + u);
+      d->ah = afr[0][st][l];
+      d->al = afr[1][st][l];
+    };
+    frag(0, &fr[0]);
+    static_for<0, SM_KS>([&](auto ST) {
+      constexpr int st = ST;
+      if constexpr (st + 1 < SM_KS) frag(st + 1, &fr[(st + 1) % 2]);
+      const Fr& f = fr[st % 2];
+      acc_h = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.ah, f.xh, acc_h, 0, 0, 0);
+      acc_c = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.ah, f.xl, acc_c, 0, 0, 0);
+      acc_c = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.al, f.xh, acc_c, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    // outputs m0 + 16 b + 4 g + r: the stereo LPF, and the combiner's L and R
+    const int64_t n0 = m0 + 16 * b + 4 * g;
+    float y[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      y[r] = fmaf(acc_c[r], 1.f / MM_LO, acc_h[r]);
+      const int64_t nn = SM_D * (n0 + r);             // lfilter zi: the block's first outputs
+      if (m0 == 0 && J.zi != nullptr && nn < T - 1) y[r] += (float)J.zi[(int64_t)s * J.zi_stride + nn];
+    }
+    const float* mb = J.mono + (int64_t)s * J.y_stride;
+    float* yb = J.y + (int64_t)s * J.y_stride;
+    float* lb = J.left + (int64_t)s * J.y_stride;
+    float* rb = J.right + (int64_t)s * J.y_stride;
+    if (n0 + 4 <= M) {
+      const float4 mv = *reinterpret_cast<const float4*>(mb + n0);
+      const float mm[4] = {mv.x, mv.y, mv.z, mv.w};
+      float lv[4], rv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        lv[r] = (mm[r] + y[r]) * 0.5f;
+        rv[r] = (mm[r] - y[r]) * 0.5f;
+      }
+      *reinterpret_cast<float4*>(yb + n0) = make_float4(y[0], y[1], y[2], y[3]);
+      *reinterpret_cast<float4*>(lb + n0) = make_float4(lv[0], lv[1], lv[2], lv[3]);
+      *reinterpret_cast<float4*>(rb + n0) = make_float4(rv[0], rv[1], rv[2], rv[3]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n0 + r < M) {
+          yb[n0 + r] = y[r];
+          lb[n0 + r] = (mb[n0 + r] + y[r]) * 0.5f;
+          rb[n0 + r] = (mb[n0 + r] - y[r]) * 0.5f;
+        }
+    }
+    if (J.yh != nullptr || J.lh != nullptr || J.rh != nullptr) {   // host rows (per-call runs)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n0 + r < M) {
+          const float mm = mb[n0 + r];
+          if (J.yh) J.yh[(int64_t)s * J.yh_stride + n0 + r] = y[r];
+          if (J.lh) J.lh[(int64_t)s * J.yh_stride + n0 + r] = (mm + y[r]) * 0.5f;
+          if (J.rh) J.rh[(int64_t)s * J.yh_stride + n0 + r] = (mm - y[r]) * 0.5f;
+        }
+    }
+    cur = nxt;
   }
 }
 
@@ -991,6 +1158,24 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
            j.n % 4 == 0 && j.n < (int64_t)1 << 28;      // (buffer ranges: 32-bit byte offsets)
   };
   for (StageJob& j : jobs) j.mma = 0;
+  // stage C's stereo mixer + LPF + combiner (rx_stereomm_kernel)
+  for (StageJob& j : jobs) {
+    if (!(mma_enabled() && j.kind == JK_FIR && j.pre == PRE_NCO && !j.nco_sin && j.D == SM_D && j.T == 151 &&
+          j.mono != nullptr && j.left != nullptr && j.right != nullptr && j.nco.theta != nullptr && al16(j.y, j.y_stride) &&
+          al16(j.mono, j.y_stride) && al16(j.left, j.y_stride) && al16(j.right, j.y_stride) &&
+          j.n >= (int64_t)MM_MIN_WIN * MM_WT && j.n < (int64_t)1 << 28 && j.n % 4 == 0))   // (n = 0 mod 4: mix_load)
+      continue;
+    const int64_t wins = (j.n / SM_D + 256) / 256 * S;
+    const int wgs = (int)std::min<int64_t>(SM_WGS, (wins + 3) / 4);
+    StageJobs Q{};
+    Q.j[0] = j;
+    Q.njobs = 1;
+    Q.nstreams = S;
+    hipLaunchKernelGGL(rx_stereomm_kernel, dim3((unsigned)wgs), dim3(RX_NT), 0, st, Q, wgs);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    j.mma = 1;
+  }
   for (int key : {151, 101})
     for (int wide : {1, 0}) {                        // groups of 2-3 filters / single filters
       if (!mma_enabled()) break;
@@ -1364,6 +1549,200 @@ __global__ __launch_bounds__(CR_NT) void rx_cres_kernel(CresJob J) {
   }
 }
 
+// ---- the composite RDS filter on the matrix cores (spans) --------------------------------
+// Per window of 16 groups L (304 outputs m = m0 + 19 L + c): Y_ch[c][L] = sum_j A[c][j]
+// X_ch[j][L], A[c][j] = the composite tap of phase c at window pair j + 1 (tap(c, j + 1) of
+// cres_taps: 19 rows in two 16-row tiles), X_ch[j][L] = mixed_ch[I0 + 80 L - 159 + j], j < 256
+// (8 K steps) -- the Hankel form of mma_run with columns 80 inputs apart (fragment reads at
+// 160 L + 64 s + 16 g bytes: conflict-free); the I and Q channels share A.  A's fragments
+// (the 13 K steps that hold taps) are built once per workgroup into LDS and read per step.
+// The mixed inputs are formed where they are staged, from the RDS PLL's phases (sdr_nco.h),
+// four inputs i .. i+3 per lane and chunk with i odd (the window starts at an odd input) so
+// that their four phases are two aligned 16-B loads; every chunk's loads go out three chunks
+// ahead of its arithmetic.  Waves work alone and persist; one wave's staging (VALU: the NCO)
+// runs beside another's MFMAs.  Workgroups [0, S) write the streams' final states.
+constexpr int CM_RT = 2, CM_KS = 8, CM_KOFF = CR_CT + CR_SH - 1;   // 159: odd window starts
+constexpr int CM_LU = CR_D * 15 + 32 * CM_KS;       // 1 456 inputs staged per window
+constexpr int CM_NG = CM_LU / 4, CM_NQ = (CM_NG + 63) / 64;
+constexpr int CM_WO = 16 * CR_U;                   // 304 outputs per window
+constexpr int CM_WI = 16 * CR_D;                   // 1 280 inputs per window
+constexpr int CM_AROWS = 16 * CM_RT, CM_ACOLS = 32 * CM_KS;
+constexpr int CM_WGS = 2 * 256;                    // persistent workgroups (2 per CU: LDS)
+static_assert(CM_KOFF % 2 == 1 && CM_WI % 4 == 0, "odd window starts: chunk phases are aligned pairs");
+static_assert(cr_base(CR_U - 1) + CR_CT + CR_SH - 1 < CM_ACOLS && CR_U <= CM_AROWS, "every composite tap inside A");
+// the K steps holding row tile rt's taps: phase c's at j in [base_c + SH, base_c + CT + SH - 1]
+__host__ __device__ constexpr int cm_st0(int rt) { return (cr_base(16 * rt) + CR_SH) / 32; }
+__host__ __device__ constexpr int cm_st1(int rt) {
+  return (cr_base(rt == 0 ? 15 : CR_U - 1) + CR_CT + CR_SH - 1) / 32 + 1;
+}
+__host__ __device__ constexpr int cm_fi(int rt, int st) { return (rt == 0 ? 0 : cm_st1(0) - cm_st0(0)) + st - cm_st0(rt); }
+constexpr int CM_NF = cm_st1(0) - cm_st0(0) + cm_st1(1) - cm_st0(1);
+static_assert(cm_st1(1) <= CM_KS && CM_NF == 13, "row tiles' K steps");
+
+__global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(2))) void rx_cresmm_kernel(CresJob J,
+                                                                                               const float* amat, int wgs) {
+  __shared__ __attribute__((aligned(16))) _Float16 img[4][4 * CM_LU];   // per wave: I hi, I lo, Q hi, Q lo
+  __shared__ __attribute__((aligned(16))) h8v afr[2][CM_NF][64];         // A fragments: hi, lo
+  const int S = J.nstreams;
+  if ((int)blockIdx.x < S) {
+    cres_zf_block(J, blockIdx.x, reinterpret_cast<float*>(&img[0][0]));
+    return;
+  }
+  for (int idx = threadIdx.x; idx < CM_NF * 64; idx += RX_NT) {
+    const int fi = idx >> 6, ln = idx & 63;
+    const int rt = fi < cm_st1(0) - cm_st0(0) ? 0 : 1;
+    const int st = fi - (rt ? cm_st1(0) - cm_st0(0) : 0) + cm_st0(rt);
+    const float* ar = amat + (16 * rt + (ln & 15)) * CM_ACOLS + 32 * st + 8 * (ln >> 4);
+    h8v hi, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const MmHL p = mm_split(ar[e]);
+      hi[e] = p.hi;
+      lo[e] = p.lo;
+    }
+    afr[0][fi][ln] = hi;
+    afr[1][fi][ln] = lo;
+  }
+  __syncthreads();
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: see rx_mma_kernel
+  const int l = threadIdx.x & 63, b = l & 15, g = l >> 4;
+  const int64_t gw = ((int64_t)blockIdx.x - S) * 4 + w, nw = (int64_t)wgs * 4;
+  _Float16* Ih = img[w];
+  _Float16* Il = Ih + CM_LU;
+  _Float16* Qh = Il + CM_LU;
+  _Float16* Ql = Qh + CM_LU;
+  const int64_t n = J.n, R = J.R;
+  const int64_t wins = (R + CM_WO - 1) / CM_WO;     // per stream
+  const int64_t total = wins * S;
+  // A window's geometry and pseudo-block records (the RDS loop's blocks carry a linear
+  // response: its pre-roll stops short of LONG_ACCEPT, pll.hip warm_len); one branch-free path
+  // for every window, the chunks' loads PD chunks ahead through the seams (rx_stereomm_kernel)
+  static_assert((CM_WI - CM_KOFF) % 4 == 1 && CM_KOFF % 4 == 3, "chunks start at 1 mod 4 (mix_load)");
+  struct Win { int s; int64_t W, m0, a; const float* x; NcoTile nt; };
+  auto winfo = [&](int64_t i, Win* v) {
+    v->s = (int)(i / wins);
+    v->W = i - (int64_t)v->s * wins;
+    v->m0 = CM_WO * v->W;
+    v->a = CM_WI * v->W - CM_KOFF;                   // input of element 0
+    v->x = J.x + (int64_t)v->s * J.x_stride;
+    v->nt = nco_tile(J.nco, v->s, max<int64_t>(v->a, 1) - 1);
+  };
+  constexpr int PD = 2;
+  static_assert(CM_NQ % PD == 0, "ring slots line up across windows");
+  MixLd gb[PD];
+  auto ldg = [&](const Win& v, int j, MixLd* gg) {
+    mix_load(J.nco, v.nt, v.x, v.a + 4 * min(l + 64 * j, CM_NG - 1), true, gg);
+  };
+  Win cur{}, nxt{};
+  if (gw < total) {
+    winfo(gw, &cur);
+    static_for<0, PD>([&](auto D) { ldg(cur, D, &gb[D]); });
+  }
+  for (int64_t i = gw; i < total; i += nw) {
+    const bool more = i + nw < total;
+    if (more) winfo(i + nw, &nxt);
+    const int s = cur.s;
+    const int64_t W = cur.W, m0 = cur.m0, a = cur.a;
+    {
+      const NcoWin nwin = nco_win(J.nco, cur.nt, a);
+      const bool lin = nco_tile_lin(cur.nt);
+      const float c0 = J.nco.nco_i[(int64_t)s * J.nco.out_stride], s0 = J.nco.nco_q[(int64_t)s * J.nco.out_stride];
+      static_for<0, CM_NQ>([&](auto JJ) {
+        constexpr int j = JJ;
+        const int q = min(l + 64 * j, CM_NG - 1);
+        const MixLd gc = gb[j % PD];
+        if constexpr (j + PD < CM_NQ) ldg(cur, j + PD, &gb[j % PD]);
+        else ldg(more ? nxt : cur, j + PD - CM_NQ, &gb[j % PD]);
+        float xv[4], c[4], sn[4];
+        mix_eval(cur.nt, nwin, a + 4 * q, n, gc, lin, c0, s0, xv, c, sn);
+        h4v hv, lv;
+        mm_split4(make_float4(xv[0] * c[0], xv[1] * c[1], xv[2] * c[2], xv[3] * c[3]), &hv, &lv);
+        *reinterpret_cast<h4v*>(Ih + 4 * q) = hv;
+        *reinterpret_cast<h4v*>(Il + 4 * q) = lv;
+        mm_split4(make_float4(xv[0] * sn[0], xv[1] * sn[1], xv[2] * sn[2], xv[3] * sn[3]), &hv, &lv);
+        *reinterpret_cast<h4v*>(Qh + 4 * q) = hv;
+        *reinterpret_cast<h4v*>(Ql + 4 * q) = lv;
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+    // the K steps, fragments of step st + 1 read while step st's MFMAs run
+    f4v aIh[CM_RT], aIc[CM_RT], aQh[CM_RT], aQc[CM_RT];
+#pragma unroll
+    for (int rt = 0; rt < CM_RT; ++rt) aIh[rt] = aIc[rt] = aQh[rt] = aQc[rt] = f4v{0.f, 0.f, 0.f, 0.f};
+    struct Fr { h8v x[4], a[CM_RT][2]; };
+    Fr fr[2];
+    auto frag = [&](auto ST, Fr* d) {
+      constexpr int st = ST;
+      const int u = CR_D * b + 32 * st + 8 * g;
+      d->x[0] = *reinterpret_cast<const h8v*>(Ih + u);
+      d->x[1] = *reinterpret_cast<const h8v*>(Il + u);
+      d->x[2] = *reinterpret_cast<const h8v*>(Qh + u);
+      d->x[3] = *reinterpret_cast<const h8v*>(Ql + u);
+      static_for<0, CM_RT>([&](auto RT) {
+        constexpr int rt = RT;
+        if constexpr (st >= cm_st0(rt) && st < cm_st1(rt)) {
+          d->a[rt][0] = afr[0][cm_fi(rt, st)][l];
+          d->a[rt][1] = afr[1][cm_fi(rt, st)][l];
+        }
+      });
+    };
+    frag(std::integral_constant<int, 0>{}, &fr[0]);
+    static_for<0, CM_KS>([&](auto ST) {
+      constexpr int st = ST;
+      if constexpr (st + 1 < CM_KS) frag(std::integral_constant<int, st + 1>{}, &fr[(st + 1) % 2]);
+      const Fr& f = fr[st % 2];
+      static_for<0, CM_RT>([&](auto RT) {
+        constexpr int rt = RT;
+        if constexpr (st >= cm_st0(rt) && st < cm_st1(rt)) {
+          const h8v ah = f.a[rt][0], al = f.a[rt][1];
+          aIh[rt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, f.x[0], aIh[rt], 0, 0, 0);
+          aIc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, f.x[1], aIc[rt], 0, 0, 0);
+          aIc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, f.x[0], aIc[rt], 0, 0, 0);
+          aQh[rt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, f.x[2], aQh[rt], 0, 0, 0);
+          aQc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, f.x[3], aQc[rt], 0, 0, 0);
+          aQc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, f.x[2], aQc[rt], 0, 0, 0);
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    // outputs: lane (b, g) holds phases c = 16 rt + 4 g + r of group L = b
+    const bool head = W == 0;                        // the stream's first window: the zi terms
+#pragma unroll
+    for (int rt = 0; rt < CM_RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = 16 * rt + 4 * g + r;
+        const int64_t m = m0 + CR_U * b + c;
+        if (c >= CR_U || m >= R) continue;
+        float yi = fmaf(aIc[rt][r], 1.f / MM_LO, aIh[rt][r]), yq = fmaf(aQc[rt][r], 1.f / MM_LO, aQh[rt][r]);
+        const int64_t i0 = (CR_D * m) / CR_U;
+        if (head && (i0 < CR_CT - 1 || CR_D * m < CR_T - 1)) {
+          // block head: the LPF's zi (in lpf[i < 150]) and the anti-image zi (in a[q < 150])
+          const int rho = (int)(CR_D * m - (int64_t)CR_U * i0);
+          double ci = 0.0, cq = 0.0;
+          for (int ss = 0; rho + CR_U * ss <= CR_T - 1; ++ss) {
+            const int64_t li = i0 - ss;
+            if (li >= 0 && li < CR_T - 1) {
+              ci = fma(J.g64[rho + CR_U * ss], J.zi_l[0][(int64_t)s * J.zs + li], ci);
+              cq = fma(J.g64[rho + CR_U * ss], J.zi_l[1][(int64_t)s * J.zs + li], cq);
+            }
+          }
+          if (CR_D * m < CR_T - 1) {
+            ci += J.zi_a[0][(int64_t)s * J.zs + CR_D * m];
+            cq += J.zi_a[1][(int64_t)s * J.zs + CR_D * m];
+          }
+          yi += (float)(CR_U * ci);
+          yq += (float)(CR_U * cq);
+        }
+        J.y[0][(int64_t)s * J.y_stride + m] = yi;
+        J.y[1][(int64_t)s * J.y_stride + m] = yq;
+        if (J.yh[0]) J.yh[0][(int64_t)s * J.yh_stride + m] = yi;
+        if (J.yh[1]) J.yh[1][(int64_t)s * J.yh_stride + m] = yq;
+      }
+    cur = nxt;
+  }
+}
+
 // the composite taps (host, f64 then f32) in the kernel's order; empty unless both filters
 // have CR_T taps
 void cres_taps(const std::vector<double>& h, const std::vector<double>& g, std::vector<float>* out) {
@@ -1391,6 +1770,10 @@ void cres_taps(const std::vector<double>& h, const std::vector<double>& g, std::
       }
     }
   }
+  // then the dense A of rx_cresmm_kernel: A[c][j] = tap(c, j + 1), rows 19 .. 31 zero
+  out->resize(CR_NTAPS + CM_AROWS * CM_ACOLS, 0.f);
+  for (int c = 0; c < CR_U; ++c)
+    for (int j = 0; j < CM_ACOLS; ++j) (*out)[CR_NTAPS + c * CM_ACOLS + j] = tap(c, j + 1);
 }
 
 // state-bank slots (f64 lfilter states, T-1 per stream each)
@@ -1968,7 +2351,15 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       J.nstreams = S;
       const int64_t grid = (int64_t)J.tiles * S + S;
       if (grid > 0x7fffffff || r->zlen[Z_ANTI_I] != J.zs) return fail(SDR_EINVAL, "sdr_rx: composite RDS geometry");
-      hipLaunchKernelGGL(rx_cres_kernel, dim3((unsigned)grid), dim3(CR_NT), 0, st, J);
+      // spans: the matrix-core form (per job length, as launch_stage decides: a stream's outputs
+      // do not depend on how many streams share the launch)
+      if (mma_enabled() && M >= (int64_t)MM_MIN_WIN * MM_WT && M % 4 == 0 && J.nco.theta != nullptr) {
+        const int64_t wins = ceil_div(r->R, CM_WO) * S;
+        const int wgs = (int)std::min<int64_t>(CM_WGS, ceil_div(wins, 4));
+        hipLaunchKernelGGL(rx_cresmm_kernel, dim3((unsigned)(S + wgs)), dim3(RX_NT), 0, st, J, r->ctaps + CR_NTAPS, wgs);
+      } else {
+        hipLaunchKernelGGL(rx_cres_kernel, dim3((unsigned)grid), dim3(CR_NT), 0, st, J);
+      }
       HIP_TRY(hipGetLastError());
     } else {
       // stage D: rational resamplers (fmRDSblock.py:184-199)

@@ -296,6 +296,159 @@ __device__ __forceinline__ void nco_f32x4(const NcoSrc& N, const NcoTile& T, int
   nco_poly2({y[2], y[3]}, {q[2], q[3]}, &c[2], &sn[2]);
 }
 
+// nco_f32x4 in two halves, for consumers that software-pipeline their loads (rx.hip's matrix-
+// core mixers): nco4_load issues every load of inputs i .. i+3 (i >= 1 odd) -- the phase pairs
+// and, when the tile's pseudo-blocks carry a linear response (lin: uniform), the response rows
+// -- and nco4_eval forms the four cos / sin with nco_f32x4's arithmetic exactly.
+struct Nco4Ld {
+  typedef double d2n __attribute__((ext_vector_type(2)));
+  d2n t01, t23;
+  d2n rr[4];
+};
+__device__ __forceinline__ bool nco_tile_lin(const NcoTile& T) {
+  return T.d0[0] != 0.0 || T.d1[0] != 0.0 || T.d0[1] != 0.0 || T.d1[1] != 0.0;
+}
+// (i odd: the four phases phaseEst_{i-1} .. phaseEst_{i+2} are two aligned pairs, t01 and t23)
+__device__ __forceinline__ void nco4_load(const NcoSrc& N, const NcoTile& T, int64_t i, bool lin, Nco4Ld* L) {
+  typedef Nco4Ld::d2n d2n;
+  const double* th = T.th + i - 1;
+  L->t01 = *reinterpret_cast<const d2n*>(th);
+  L->t23 = *reinterpret_cast<const d2n*>(th + 2);
+  if (lin) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t j = i - 1 + e;
+      const int64_t k0 = j - (j >= T.bound ? T.bound : T.kb);
+      const int64_t kk = k0 > 0 ? k0 : (int64_t)0;                // (>= 0: clamped rows)
+      L->rr[e] = *reinterpret_cast<const d2n*>(N.resp + 2 * (kk + 1));
+    }
+  }
+}
+__device__ __forceinline__ void nco4_eval(const NcoSrc& N, const NcoTile& T, int64_t i, const Nco4Ld& L, bool lin,
+                                          float (&c)[4], float (&sn)[4]) {
+#pragma clang fp contract(off)
+  const double st[4] = {L.t01.x, L.t01.y, L.t23.x, L.t23.y};   // phaseEst_{i-1} .. phaseEst_{i+2}
+  double p[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t j = i - 1 + e;
+    const bool h = j >= T.bound;
+    const double sh = h ? T.sh[1] : T.sh[0];
+    p[e] = fma(sh, sdrnco::kP1, fma(sh, sdrnco::kP2, st[e]));
+    if (lin) {
+      const double d0 = h ? T.d0[1] : T.d0[0], d1 = h ? T.d1[1] : T.d1[0];
+      if (d0 != 0.0 || d1 != 0.0) p[e] = p[e] + (L.rr[e].x * d0 + L.rr[e].y * d1);
+    }
+  }
+  float y[4];
+  int q[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) nco_angle(N, T.off, i + e, p[e], &y[e], &q[e]);
+  nco_poly2({y[0], y[1]}, {q[0], q[1]}, &c[0], &sn[0]);
+  nco_poly2({y[2], y[3]}, {q[2], q[3]}, &c[2], &sn[2]);
+}
+
+// The matrix-core mixers' angle, per window (rx.hip rx_stereomm_kernel / rx_cresmm_kernel):
+// a_k = ws (off + k) + (phaseEst_{k-1}) scale + adj with phaseEst = stored + 2 pi shift (+ the
+// linear response) is formed as
+//   a_k = base_h + ws (k - kw) + stored scale (+ scale (rr . d)),
+//   base_h = [ws (off + kw) mod 2 pi] + adj + 2 pi frac(scale shift_h)
+// -- the large product ws (off + kw) reduced ONCE per window in double-double (its rounding
+// error kept, then a 3-part 2 pi), the chain's whole turns folded in exactly (scale shift is a
+// multiple of 1/2 for every fmPll scale), so each sample needs one fma for its phase and a
+// 2-part pi/2 reduction of |a| < ~1e4: 8 f64 operations instead of 14, and no larger angle
+// error than the reference's own f64 th (it is smaller: the reference rounds ws (off + k) at
+// full magnitude).  The f32 polynomials are nco_poly2's.
+struct NcoWin {
+  double base[2];          // per pseudo-block half h (as NcoTile)
+  double sd0[2], sd1[2];   // scale d, per half (the linear response)
+  double ws, scale;
+  int64_t kw;              // the reference sample
+};
+__device__ __forceinline__ NcoWin nco_win(const NcoSrc& N, const NcoTile& T, int64_t kw) {
+#pragma clang fp contract(off)
+  NcoWin W;
+  W.ws = N.w * N.scale;
+  W.scale = N.scale;
+  W.kw = kw;
+  const double X = T.off + (double)kw;               // integer-valued: exact
+  const double hi = W.ws * X, lo = fma(W.ws, X, -hi);
+  const double n = rint(hi * sdrnco::kInv2Pi);
+  double r = fma(-n, sdrnco::kP1, hi);
+  r = fma(-n, sdrnco::kP2, r);
+  r = fma(-n, sdrnco::kP3, r);
+  r = (r + lo) + N.adj;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const double f = N.scale * T.sh[h];
+    W.base[h] = r + (f - rint(f)) * sdrnco::k2Pi;
+    W.sd0[h] = N.scale * T.d0[h];
+    W.sd1[h] = N.scale * T.d1[h];
+  }
+  return W;
+}
+// cos / sin (f32) of outputs i .. i+3 (i odd: L from nco4_load) from the window's angle base
+__device__ __forceinline__ void nco4_eval_w(const NcoTile& T, const NcoWin& W, int64_t i, const Nco4Ld& L, bool lin,
+                                            float (&c)[4], float (&sn)[4]) {
+#pragma clang fp contract(off)
+  constexpr double k2oPi = 0.6366197723675814;
+  constexpr double Q1 = 1.5707963705062866, Q2 = -4.3711390001862426e-08;   // 2-part pi/2 (|n| < 2^29)
+  const double st[4] = {L.t01.x, L.t01.y, L.t23.x, L.t23.y};   // phaseEst_{i-1} .. phaseEst_{i+2} (stored)
+  const double dk = (double)(int)(i - W.kw);
+  double tb0 = fma(W.ws, dk, W.base[0]), tb1 = fma(W.ws, dk, W.base[1]);
+  float y[4];
+  int q[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t j = i - 1 + e;
+    const bool h = j >= T.bound;
+    if (e > 0) {                                      // the next output: + ws
+      tb0 = tb0 + W.ws;
+      tb1 = tb1 + W.ws;
+    }
+    double a = fma(st[e], W.scale, h ? tb1 : tb0);
+    if (lin) a = a + (L.rr[e].x * (h ? W.sd0[1] : W.sd0[0]) + L.rr[e].y * (h ? W.sd1[1] : W.sd1[0]));
+    const double n = rint(a * k2oPi);
+    double r = fma(-n, Q1, a);
+    r = fma(-n, Q2, r);
+    y[e] = (float)r;
+    q[e] = (int)n & 3;
+  }
+  nco_poly2({y[0], y[1]}, {q[0], q[1]}, &c[0], &sn[0]);
+  nco_poly2({y[2], y[3]}, {q[2], q[3]}, &c[2], &sn[2]);
+}
+
+// A matrix-core mixer's chunk: inputs i0 .. i0+3 (i0 = 1 mod 4 -- so no chunk straddles the
+// row's end (n = 0 mod 4) except the last, i0 = n - 3, and none its start except i0 = -3, whose
+// only input in the row is x[0] with the carried NCO[0]).  Loads are clamped into the rows
+// (x[n], read by the last chunk, is row padding: receiver rows are >= n + 1 long) and the
+// response rows always read: branch-free, unconditional loads that the compiler counts exactly.
+struct MixLd {
+  float4 x;
+  Nco4Ld t;
+};
+// (lin: whether to read the response rows -- true always for the RDS loop, whose blocks all
+// carry one; the pilot loop's rarely do, and a uniform branch then costs little)
+__device__ __forceinline__ void mix_load(const NcoSrc& N, const NcoTile& T, const float* xr, int64_t i0, bool lin,
+                                         MixLd* L) {
+  __builtin_memcpy(&L->x, xr + (i0 > 0 ? i0 : (int64_t)0), sizeof(float4));   // (4-B aligned)
+  nco4_load(N, T, i0 > 1 ? i0 : (int64_t)1, lin, &L->t);
+}
+// the chunk's inputs (0 outside [0, n)) and cos / sin (NCO[0]: the carried c0 / s0)
+__device__ __forceinline__ void mix_eval(const NcoTile& T, const NcoWin& W, int64_t i0, int64_t n, const MixLd& L,
+                                         bool lin, float c0, float s0, float (&xv)[4], float (&c)[4], float (&sn)[4]) {
+  nco4_eval_w(T, W, i0, L.t, lin, c, sn);
+  // per chunk, not per sample: i0 = -3 (only x[0], with NCO[0]), i0 = n - 3 (the last three),
+  // wholly outside the row, or interior
+  const bool head = i0 == -3, tail = i0 == n - 3, out = (i0 < 0 && !head) || i0 >= n;
+  xv[0] = (head || out) ? 0.f : L.x.x;
+  xv[1] = (head || out) ? 0.f : L.x.y;
+  xv[2] = (head || out) ? 0.f : L.x.z;
+  xv[3] = head ? L.x.x : ((tail || out) ? 0.f : L.x.w);
+  c[3] = head ? c0 : c[3];
+  sn[3] = head ? s0 : sn[3];
+}
+
 // ---- the fused mixer's pairs (PllJob::pair), as the receiver's filters read them ----------
 // pair[k] = 2 x[k] (cos, sin)(a_k) with a_k the NCO angle of the phase the PLL kernel stored;
 // a long call's pseudo-block b is then rotated by scale (2 pi shift_b + (A^(kk+1) d_b)_phase)
