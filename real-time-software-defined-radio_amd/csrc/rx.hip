@@ -937,7 +937,16 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(mm_waves_
 void rx_mma_kernel(StageJobs P) {
   __shared__ __attribute__((aligned(16))) _Float16 img[4][2 * MmaShape<T>::LU];
   __shared__ float tap_s[FMAX * T];
-  const int64_t b = blockIdx.x;
+  // the final-state workgroups first (the jobs' zf, and the FE state when the launch carries
+  // it): they run beside the persistent waves instead of in a launch of their own
+  const int64_t nzb = (int64_t)P.nzf * P.nstreams, nfront = nzb + (P.fe.on ? P.nstreams : 0);
+  if ((int64_t)blockIdx.x < nfront) {
+    float* lf = reinterpret_cast<float*>(&img[0][0]);
+    if ((int64_t)blockIdx.x < nzb) zf_block<false>(P, blockIdx.x, lf);
+    else fe_state_block(P.fe, (int)(blockIdx.x - nzb), lf);
+    return;
+  }
+  const int64_t b = blockIdx.x - nfront;
   int q = 0;
   for (int i = 1; i < P.njobs; ++i)
     if (b >= P.j[i].b0) q = i;
@@ -957,26 +966,39 @@ void rx_mma_kernel(StageJobs P) {
   }
 }
 
-// ---- stage C's stereo mixer + LPF + [::5] + L/R combiner on the matrix cores (spans) -------
-// y[m] = sum_k h[k] u[5 m - k], u[i] = (x[i] nco[i]) g (model/fmMonoBlock.py:155-162, the NCO
-// formed from the pilot PLL's phases, sdr_nco.h): the 16 outputs m = m0 + 16 c + b of column c
-// of a 256-output window are Y = A X with A[b][j] = h[5 b + 151 - j] (zero outside the taps)
-// and X[j][c] = u[5 m0 + 80 c + j - 151], j < 256 -- the Hankel form of the composite kernel
-// (columns 80 inputs apart, odd window starts: each chunk's four phases are two aligned
-// pairs), one channel; A's 8 K steps built once per workgroup into LDS.  The epilogue is the
-// combiner (fmMonoBlock.py:166-170): L = (mono + y) / 2, R = (mono - y) / 2.
+// ---- decimate-by-5 LPFs on the matrix cores (spans): stage C's stereo mixer + LPF + L/R
+// combiner (MIX) and stage A's mono audio LPF ------------------------------------------------
+// y[m] = sum_k h[k] u[5 m - k] with u = x (mono, model/fmMonoBlock.py:101-109) or u[i] = (x[i]
+// nco[i]) g (stereo, :155-162, the NCO formed from the pilot PLL's phases, sdr_nco.h): the 16
+// outputs m = m0 + 16 c + b of column c of a 256-output window are Y = A X with A[b][j] =
+// h[5 b + 151 - j] (zero outside the taps) and X[j][c] = u[5 m0 + 80 c + j - 151], j < 256 --
+// the Hankel form of the composite kernel (columns 80 inputs apart; odd window starts: each
+// chunk's four phases are two aligned pairs), one channel; A's 8 K steps built once per
+// workgroup into LDS.  MIX's epilogue is the combiner (:166-170): L = (mono + y) / 2,
+// R = (mono - y) / 2; every global access of the loop is unconditional (buffer loads / stores
+// with the range check at the row ends), so the compiler's vmcnt waits count exactly and the
+// next window's prefetched chunks are never waited for early.
 constexpr int SM_KS = 8, SM_KOFF = 151, SM_D = 5;
 constexpr int SM_LU = 80 * 15 + 32 * SM_KS;         // 1 456 inputs staged per window
 constexpr int SM_NG = SM_LU / 4, SM_NQ = (SM_NG + 63) / 64;
-constexpr int SM_WPE = 3;                           // waves per SIMD (registers)
-constexpr int SM_WGS = SM_WPE * 256;                // persistent workgroups
-static_assert(SM_D * 15 + SM_KOFF < 32 * SM_KS && SM_KOFF >= 150 && SM_KOFF % 2 == 1, "stereo LPF window");
+template <bool MIX> constexpr int sm_wpe() { return MIX ? 2 : 4; }   // waves per SIMD (registers; LDS: 4 x 39.7 KB)
+static_assert(SM_D * 15 + SM_KOFF < 32 * SM_KS && SM_KOFF >= 150 && SM_KOFF % 2 == 1, "LPF window");
 
-__global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(SM_WPE))) void rx_stereomm_kernel(StageJobs P, int wgs) {
+template <bool MIX>
+__global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(sm_wpe<MIX>()))) void rx_decmm_kernel(StageJobs P,
+                                                                                                             int wgs) {
   const StageJob& J = P.j[0];                        // (in the kernel arguments: no private copy)
   const int S = P.nstreams;
   __shared__ __attribute__((aligned(16))) _Float16 img[4][2 * SM_LU];   // per wave: hi, lo
   __shared__ __attribute__((aligned(16))) h8v afr[2][SM_KS][64];         // A fragments: hi, lo
+  const int nfront = P.nzf * S + (P.fe.on ? S : 0);
+  if ((int)blockIdx.x < nfront) {                    // final states first (as rx_mma_kernel)
+    float* lf = reinterpret_cast<float*>(&img[0][0]);
+    if ((int)blockIdx.x < P.nzf * S) zf_block<MIX>(P, blockIdx.x, lf);
+    else fe_state_block(P.fe, (int)blockIdx.x - P.nzf * S, lf);
+    return;
+  }
+  const int bx = (int)blockIdx.x - nfront;
   constexpr int T = 151;
   for (int idx = threadIdx.x; idx < SM_KS * 64; idx += RX_NT) {
     const int st = idx >> 6, ln = idx & 63, bb = ln & 15, gg = ln >> 4;
@@ -994,18 +1016,17 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(SM_WPE)))
   __syncthreads();
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // uniform: see rx_mma_kernel
   const int l = threadIdx.x & 63, b = l & 15, g = l >> 4;
-  const int64_t gw = (int64_t)blockIdx.x * 4 + w, nw = (int64_t)wgs * 4;
+  const int64_t gw = (int64_t)bx * 4 + w, nw = (int64_t)wgs * 4;
   _Float16* xh = img[w];
   _Float16* xl = xh + SM_LU;
   const int64_t n = J.n, M = (J.n + SM_D - 1) / SM_D;
   const int64_t wins = (M + 255) / 256;              // per stream
   const int64_t total = wins * S;
   const float gain = J.gain;
-  // A window's geometry and pseudo-block records; every window (row ends included: mix_eval)
-  // takes the same branch-free path.  The chunks' loads run PD chunks ahead of their arithmetic
-  // through the window seams: the last PD chunks of a window issue the next window's first ones
-  // (its records were read a window earlier), so a wave's stream of chunks never waits for a
-  // load it issued in its own window.
+  // A window's geometry (and, MIX, pseudo-block records); every window (row ends included:
+  // mix_eval) takes the same branch-free path.  The chunks' loads run PD chunks ahead of their
+  // arithmetic through the window seams: the last PD chunks of a window issue the next
+  // window's first ones (its records were read a window earlier).
   static_assert((SM_D * 256 - SM_KOFF) % 4 == 1 && SM_KOFF % 4 == 3, "chunks start at 1 mod 4 (mix_load)");
   struct Win { int s; int64_t m0, a; const float* x; NcoTile nt; bool lin; };
   auto winfo = [&](int64_t i, Win* v) {
@@ -1014,14 +1035,18 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(SM_WPE)))
     v->m0 = 256 * W;
     v->a = SM_D * v->m0 - SM_KOFF;                   // input of element 0
     v->x = J.x + (int64_t)v->s * J.x_stride;
-    v->nt = nco_tile(J.nco, v->s, max<int64_t>(v->a, 1) - 1);
-    v->lin = nco_tile_lin(v->nt);
+    if constexpr (MIX) {
+      v->nt = nco_tile(J.nco, v->s, max<int64_t>(v->a, 1) - 1);
+      v->lin = nco_tile_lin(v->nt);
+    }
   };
   constexpr int PD = 2;
   static_assert(SM_NQ % PD == 0, "ring slots line up across windows");
   MixLd gb[PD];
   auto ldg = [&](const Win& v, int j, MixLd* gg) {
-    mix_load(J.nco, v.nt, v.x, v.a + 4 * min(l + 64 * j, SM_NG - 1), v.lin, gg);
+    const int64_t i0 = v.a + 4 * min(l + 64 * j, SM_NG - 1);
+    if constexpr (MIX) mix_load(J.nco, v.nt, v.x, i0, v.lin, gg);
+    else __builtin_memcpy(&gg->x, v.x + (i0 > 0 ? i0 : (int64_t)0), sizeof(float4));
   };
   Win cur{}, nxt{};
   if (gw < total) {
@@ -1033,21 +1058,43 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(SM_WPE)))
     if (more) winfo(i + nw, &nxt);
     const int s = cur.s;
     const int64_t m0 = cur.m0, a = cur.a;
+    const int64_t n0 = m0 + 16 * b + 4 * g;          // this lane's 4 outputs
+    // (MIX) the combiner's mono inputs, loaded before this window's prefetches: waiting for
+    // them later never waits for those
+    f4v mv = f4v{0.f, 0.f, 0.f, 0.f};
+    if constexpr (MIX) {
+      const __amdgpu_buffer_rsrc_t rm = mm_rsrc(J.mono + (int64_t)s * J.y_stride + m0, (M - m0) * 4);
+      mv = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rm, (int)(4 * (n0 - m0)), 0, 0));
+    }
     {
-      const NcoWin nwin = nco_win(J.nco, cur.nt, a);
-      const bool lin = cur.lin;
-      const float c0 = J.nco.nco_i[(int64_t)s * J.nco.out_stride];   // the carried NCO[0]
+      NcoWin nwin{};
+      float c0 = 0.f;
+      if constexpr (MIX) {
+        nwin = nco_win(J.nco, cur.nt, a);
+        c0 = J.nco.nco_i[(int64_t)s * J.nco.out_stride];   // the carried NCO[0]
+      }
       static_for<0, SM_NQ>([&](auto JJ) {
         constexpr int j = JJ;
         const int q = min(l + 64 * j, SM_NG - 1);
         const MixLd gc = gb[j % PD];
         if constexpr (j + PD < SM_NQ) ldg(cur, j + PD, &gb[j % PD]);
         else ldg(more ? nxt : cur, j + PD - SM_NQ, &gb[j % PD]);
-        float xv[4], c[4], sn[4];
-        mix_eval(cur.nt, nwin, a + 4 * q, n, gc, lin, c0, 0.f, xv, c, sn);
+        const int64_t i0 = a + 4 * q;
+        float u[4];
+        if constexpr (MIX) {
+          float xv[4], c[4], sn[4];
+          mix_eval(cur.nt, nwin, i0, n, gc, cur.lin, c0, 0.f, xv, c, sn);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) u[e] = pre_op(PRE_NCO, xv[e], c[e], gain);
+        } else {                                     // (the edges as mix_eval)
+          const bool head = i0 == -3, tail = i0 == n - 3, out = (i0 < 0 && !head) || i0 >= n;
+          u[0] = (head || out) ? 0.f : gc.x.x;
+          u[1] = (head || out) ? 0.f : gc.x.y;
+          u[2] = (head || out) ? 0.f : gc.x.z;
+          u[3] = head ? gc.x.x : ((tail || out) ? 0.f : gc.x.w);
+        }
         h4v hv, lv;
-        mm_split4(make_float4(pre_op(PRE_NCO, xv[0], c[0], gain), pre_op(PRE_NCO, xv[1], c[1], gain),
-                              pre_op(PRE_NCO, xv[2], c[2], gain), pre_op(PRE_NCO, xv[3], c[3], gain)), &hv, &lv);
+        mm_split4(make_float4(u[0], u[1], u[2], u[3]), &hv, &lv);
         *reinterpret_cast<h4v*>(xh + 4 * q) = hv;
         *reinterpret_cast<h4v*>(xl + 4 * q) = lv;
         __builtin_amdgcn_sched_barrier(0);
@@ -1057,9 +1104,9 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(SM_WPE)))
     struct Fr { h8v xh, xl, ah, al; };
     Fr fr[2];
     auto frag = [&](int st, Fr* d) {
-      const int u = 80 * b + 32 * st + 8 * g;
-      d->xh = *reinterpret_cast<const h8v*>(xh + u);
-      d->xl = *reinterpret_cast<const h8v*>(xl + u);
+      const int uu = 80 * b + 32 * st + 8 * g;
+      d->xh = *reinterpret_cast<const h8v*>(xh + uu);
+      d->xl = *reinterpret_cast<const h8v*>(xl + uu);
       d->ah = afr[0][st][l];
       d->al = afr[1][st][l];
     };
@@ -1073,48 +1120,38 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(SM_WPE)))
       acc_c = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.al, f.xh, acc_c, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     });
-    // outputs m0 + 16 b + 4 g + r: the stereo LPF, and the combiner's L and R
-    const int64_t n0 = m0 + 16 * b + 4 * g;
-    float y[4];
+    // outputs n0 .. n0 + 3: the LPF (and, MIX, the combiner's L and R)
+    f4v y;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      y[r] = fmaf(acc_c[r], 1.f / MM_LO, acc_h[r]);
-      const int64_t nn = SM_D * (n0 + r);             // lfilter zi: the block's first outputs
-      if (m0 == 0 && J.zi != nullptr && nn < T - 1) y[r] += (float)J.zi[(int64_t)s * J.zi_stride + nn];
-    }
-    const float* mb = J.mono + (int64_t)s * J.y_stride;
-    float* yb = J.y + (int64_t)s * J.y_stride;
-    float* lb = J.left + (int64_t)s * J.y_stride;
-    float* rb = J.right + (int64_t)s * J.y_stride;
-    if (n0 + 4 <= M) {
-      const float4 mv = *reinterpret_cast<const float4*>(mb + n0);
-      const float mm[4] = {mv.x, mv.y, mv.z, mv.w};
-      float lv[4], rv[4];
+    for (int r = 0; r < 4; ++r) y[r] = fmaf(acc_c[r], 1.f / MM_LO, acc_h[r]);
+    if (m0 == 0 && J.zi != nullptr) {                // lfilter zi: the stream's first outputs
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        lv[r] = (mm[r] + y[r]) * 0.5f;
-        rv[r] = (mm[r] - y[r]) * 0.5f;
+        const int64_t nn = SM_D * (n0 + r);
+        if (nn < T - 1) y[r] += (float)J.zi[(int64_t)s * J.zi_stride + nn];
       }
-      *reinterpret_cast<float4*>(yb + n0) = make_float4(y[0], y[1], y[2], y[3]);
-      *reinterpret_cast<float4*>(lb + n0) = make_float4(lv[0], lv[1], lv[2], lv[3]);
-      *reinterpret_cast<float4*>(rb + n0) = make_float4(rv[0], rv[1], rv[2], rv[3]);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (n0 + r < M) {
-          yb[n0 + r] = y[r];
-          lb[n0 + r] = (mb[n0 + r] + y[r]) * 0.5f;
-          rb[n0 + r] = (mb[n0 + r] - y[r]) * 0.5f;
-        }
     }
-    if (J.yh != nullptr || J.lh != nullptr || J.rh != nullptr) {   // host rows (per-call runs)
+    const int ob = (int)(4 * (n0 - m0));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, y),
+                                           mm_rsrc(J.y + (int64_t)s * J.y_stride + m0, (M - m0) * 4), ob, 0, 0);
+    f4v lv, rv;
+    if constexpr (MIX) {
+      lv = (mv + y) * 0.5f;
+      rv = (mv - y) * 0.5f;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, lv),
+                                             mm_rsrc(J.left + (int64_t)s * J.y_stride + m0, (M - m0) * 4), ob, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, rv),
+                                             mm_rsrc(J.right + (int64_t)s * J.y_stride + m0, (M - m0) * 4), ob, 0, 0);
+    }
+    if (J.yh != nullptr || (MIX && (J.lh != nullptr || J.rh != nullptr))) {   // host rows (per-call runs)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (n0 + r < M) {
-          const float mm = mb[n0 + r];
           if (J.yh) J.yh[(int64_t)s * J.yh_stride + n0 + r] = y[r];
-          if (J.lh) J.lh[(int64_t)s * J.yh_stride + n0 + r] = (mm + y[r]) * 0.5f;
-          if (J.rh) J.rh[(int64_t)s * J.yh_stride + n0 + r] = (mm - y[r]) * 0.5f;
+          if constexpr (MIX) {
+            if (J.lh) J.lh[(int64_t)s * J.yh_stride + n0 + r] = lv[r];
+            if (J.rh) J.rh[(int64_t)s * J.yh_stride + n0 + r] = rv[r];
+          }
         }
     }
     cur = nxt;
@@ -1158,23 +1195,35 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
            j.n % 4 == 0 && j.n < (int64_t)1 << 28;      // (buffer ranges: 32-bit byte offsets)
   };
   for (StageJob& j : jobs) j.mma = 0;
-  // stage C's stereo mixer + LPF + combiner (rx_stereomm_kernel)
+  bool fe_done = fe == nullptr || !fe->on;
+  // the decimate-by-5 LPFs: stage C's stereo mixer + LPF + combiner, stage A's mono LPF
+  // (rx_decmm_kernel; zf and the FE state ride on the launch)
   for (StageJob& j : jobs) {
-    if (!(mma_enabled() && j.kind == JK_FIR && j.pre == PRE_NCO && !j.nco_sin && j.D == SM_D && j.T == 151 &&
-          j.mono != nullptr && j.left != nullptr && j.right != nullptr && j.nco.theta != nullptr && al16(j.y, j.y_stride) &&
-          al16(j.mono, j.y_stride) && al16(j.left, j.y_stride) && al16(j.right, j.y_stride) &&
-          j.n >= (int64_t)MM_MIN_WIN * MM_WT && j.n < (int64_t)1 << 28 && j.n % 4 == 0))   // (n = 0 mod 4: mix_load)
-      continue;
+    const bool mix = j.pre == PRE_NCO && !j.nco_sin && j.mono != nullptr && j.left != nullptr && j.right != nullptr &&
+                     j.nco.theta != nullptr && al16(j.mono, j.y_stride) && al16(j.left, j.y_stride) &&
+                     al16(j.right, j.y_stride);
+    const bool mono = j.pre == PRE_NONE && j.mono == nullptr;
+    if (!(mma_enabled() && j.kind == JK_FIR && j.D == SM_D && j.T == 151 && (mix || mono) && al16(j.y, j.y_stride) &&
+          j.x != nullptr && j.n >= (int64_t)MM_MIN_WIN * MM_WT && j.n < (int64_t)1 << 28 && j.n % 4 == 0))
+      continue;                                      // (n = 0 mod 4: the chunks' edges, mix_load)
     const int64_t wins = (j.n / SM_D + 256) / 256 * S;
-    const int wgs = (int)std::min<int64_t>(SM_WGS, (wins + 3) / 4);
+    const int wgs = (int)std::min<int64_t>((mix ? sm_wpe<true>() : sm_wpe<false>()) * 256, (wins + 3) / 4);
     StageJobs Q{};
     Q.j[0] = j;
     Q.njobs = 1;
     Q.nstreams = S;
-    hipLaunchKernelGGL(rx_stereomm_kernel, dim3((unsigned)wgs), dim3(RX_NT), 0, st, Q, wgs);
+    if (j.zf != nullptr && j.T > 1) Q.zfj[Q.nzf++] = 0;
+    if (!fe_done) {
+      Q.fe = *fe;
+      fe_done = true;
+    }
+    const unsigned grid = (unsigned)(wgs + Q.nzf * S + (Q.fe.on ? S : 0));
+    if (mix) hipLaunchKernelGGL(rx_decmm_kernel<true>, dim3(grid), dim3(RX_NT), 0, st, Q, wgs);
+    else hipLaunchKernelGGL(rx_decmm_kernel<false>, dim3(grid), dim3(RX_NT), 0, st, Q, wgs);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     j.mma = 1;
+    j.zf = nullptr;                                  // (written by that launch)
   }
   for (int key : {151, 101})
     for (int wide : {1, 0}) {                        // groups of 2-3 filters / single filters
@@ -1196,8 +1245,8 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
         for (int m = 0; m < g; ++m) {
           StageJob j = jobs[ji + m];
           j.fold = m == 0 ? g : 0;
-          j.zf = nullptr;
           j.wgs = 0;
+          if (j.zf != nullptr && j.T > 1) Q.zfj[Q.nzf++] = Q.njobs;
           Q.j[Q.njobs++] = j;
           members.push_back(ji + m);
         }
@@ -1222,15 +1271,22 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
         }
       }
       Q.tile_blocks = blocks;
-      if (key == 151 && wide) hipLaunchKernelGGL((rx_mma_kernel<151, 3>), dim3((unsigned)blocks), dim3(RX_NT), 0, st, Q);
-      else if (key == 151) hipLaunchKernelGGL((rx_mma_kernel<151, 1>), dim3((unsigned)blocks), dim3(RX_NT), 0, st, Q);
-      else if (wide) hipLaunchKernelGGL((rx_mma_kernel<101, 3>), dim3((unsigned)blocks), dim3(RX_NT), 0, st, Q);
-      else hipLaunchKernelGGL((rx_mma_kernel<101, 1>), dim3((unsigned)blocks), dim3(RX_NT), 0, st, Q);
+      if (!fe_done) {                                // the FE state rides on the first launch
+        Q.fe = *fe;
+        fe_done = true;
+      }
+      const int64_t grid = blocks + (int64_t)Q.nzf * S + (Q.fe.on ? S : 0);
+      if (key == 151 && wide) hipLaunchKernelGGL((rx_mma_kernel<151, 3>), dim3((unsigned)grid), dim3(RX_NT), 0, st, Q);
+      else if (key == 151) hipLaunchKernelGGL((rx_mma_kernel<151, 1>), dim3((unsigned)grid), dim3(RX_NT), 0, st, Q);
+      else if (wide) hipLaunchKernelGGL((rx_mma_kernel<101, 3>), dim3((unsigned)grid), dim3(RX_NT), 0, st, Q);
+      else hipLaunchKernelGGL((rx_mma_kernel<101, 1>), dim3((unsigned)grid), dim3(RX_NT), 0, st, Q);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
-      for (size_t m : members) jobs[m].mma = 1;
+      for (size_t m : members) {
+        jobs[m].mma = 1;
+        jobs[m].zf = nullptr;                        // (written by that launch)
+      }
     }
-  bool fe_done = fe == nullptr || !fe->on;
   for (int key : {151, 101, 0}) {
     StageJobs P{};
     P.nstreams = S;
@@ -1616,7 +1672,7 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(2))) void
   const int64_t total = wins * S;
   // A window's geometry and pseudo-block records (the RDS loop's blocks carry a linear
   // response: its pre-roll stops short of LONG_ACCEPT, pll.hip warm_len); one branch-free path
-  // for every window, the chunks' loads PD chunks ahead through the seams (rx_stereomm_kernel)
+  // for every window, the chunks' loads PD chunks ahead through the seams (rx_decmm_kernel)
   static_assert((CM_WI - CM_KOFF) % 4 == 1 && CM_KOFF % 4 == 3, "chunks start at 1 mod 4 (mix_load)");
   struct Win { int s; int64_t W, m0, a; const float* x; NcoTile nt; };
   auto winfo = [&](int64_t i, Win* v) {
