@@ -972,7 +972,9 @@ def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, arg
         "dominant_stage": {"stage": dom, "ms": stage_ms[dom],
                            "bound": ("PLL: pseudo-blocks solved in parallel from warm-up guesses and chained "
                                      "(f64, csrc/pll.hip long calls)") if dom == "pll" else
-                           ("HBM: IQ in, demod out" if dom == "fe" else "FP32 VALU: FIR multiply-adds")},
+                           ("HBM: IQ in, demod out" if dom == "fe" else
+                            "FIR multiply-adds (span rows on the matrix cores, f16 hi/lo; per-block rows on the "
+                            "FP32 VALU)")},
         "pll_solver": pll,
     }
     # per-stage achieved FP32 TFLOP/s (2 flops per multiply-add) against VALU_PEAK_TFLOPS, and the
@@ -991,7 +993,10 @@ def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, arg
         out["roofline"] = {"bound": "valu", "achieved": round(per_gpu_tflops, 3), "peak": VALU_PEAK_TFLOPS,
                            "unit": "TFLOP/s", "frac": round(per_gpu_tflops / VALU_PEAK_TFLOPS, 4), "traffic": None,
                            "flops_per_sample": round(fps, 2),
-                           "note": "FIR flops of the whole chain per input sample x samples / wall time per GPU"}
+                           "note": ("f32-equivalent FIR flops of the whole chain per input sample x samples / wall time "
+                                    "per GPU, against the FP32 VALU peak the direct form would be capped at; span "
+                                    "rows run their filters on the matrix cores (f16 hi/lo splits, 3 MFMA products "
+                                    "per multiply-add), so frac > 1 is possible; pll_roofline bounds the PLL")}
     if cpu and args is not None:
         out["cpu_baseline"] = ref_rx_baseline(args, cpu_rows, B, u8, stereo, rds, rf_taps)
     return out

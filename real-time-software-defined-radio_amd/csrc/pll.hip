@@ -1856,7 +1856,7 @@ void sdr_pll_resp_table(const PllCfg& c, int64_t n, std::vector<double>* out) {
   int nb;
   if (!sdr_pll_long_geom(n, &pb, &nb)) return;
   const M2 A = loop_matrix(c);
-  out->resize(2 * (size_t)(pb + 1));
+  out->resize(2 * (size_t)(pb + 1 + 4));
   double r0 = 1.0, r1 = 0.0;                        // row 0 of A^j, j = 0, 1, ...
   for (int64_t j = 0; j <= pb; ++j) {
     (*out)[2 * j] = r0;
@@ -1864,6 +1864,12 @@ void sdr_pll_resp_table(const PllCfg& c, int64_t n, std::vector<double>* out) {
     const double n0 = r0 * A.a + r1 * A.c, n1 = r0 * A.b + r1 * A.d;
     r0 = n0;
     r1 = n1;
+  }
+  // rows pb + 1 .. pb + 4 repeat rows 1 .. 4: a consumer reading four consecutive steps' rows
+  // from one pseudo-block's base (sdr_nco.h nco4_load) reads the next block's first rows there
+  for (int64_t t = 1; t <= 4; ++t) {
+    (*out)[2 * (pb + t)] = (*out)[2 * t];
+    (*out)[2 * (pb + t) + 1] = (*out)[2 * t + 1];
   }
 }
 

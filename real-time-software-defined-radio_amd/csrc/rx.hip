@@ -537,7 +537,7 @@ struct MmaShape {
 };
 constexpr int MM_LU_MAX = MmaShape<151>::LU;
 constexpr int MM_TAPS_MAX = 3 * 151;
-template <int FMAX> constexpr int mm_waves_per_cu() { return FMAX == 1 ? 16 : 8; }   // the VGPR limit
+template <int FMAX> constexpr int mm_waves_per_cu() { return FMAX == 1 ? 12 : 8; }   // the VGPR limit
 
 struct MmHL { _Float16 hi, lo; };
 __device__ __forceinline__ MmHL mm_split(float v) {
@@ -600,7 +600,7 @@ __device__ __forceinline__ void mma_run(const StageJob* Jf, int S, int64_t gw, i
       }
   // window i's samples: 16-B chunks l + 64 j of x[m0 - KOFF ...], at byte offset
   // 4 (m0 - KOFF) + 16 l + 1 024 j of the stream's row (negative: before the row, read as 0)
-  constexpr int PFD = F == 1 ? 1 : 2;                // windows in flight (F = 1: four waves per SIMD cover it)
+  constexpr int PFD = 2;                             // windows in flight
   u4v v[PFD][NQ];
   auto load = [&](int64_t i, u4v* vv) {
     const int s = (int)(i / wins);

@@ -315,13 +315,15 @@ __device__ __forceinline__ void nco4_load(const NcoSrc& N, const NcoTile& T, int
   L->t01 = *reinterpret_cast<const d2n*>(th);
   L->t23 = *reinterpret_cast<const d2n*>(th + 2);
   if (lin) {
+    // the four steps' rows are consecutive from the chunk's first step's block base: a chunk
+    // that crosses into the next pseudo-block reads that block's first rows from the table's
+    // four repeated rows (sdr_pll_resp_table) -- one address, four immediate offsets
+    const int64_t j0 = i - 1;
+    const int64_t k0 = j0 - (j0 >= T.bound ? T.bound : T.kb);
+    const int64_t kk = k0 > 0 ? k0 : (int64_t)0;                  // (>= 0: clamped rows)
+    const d2n* rr = reinterpret_cast<const d2n*>(N.resp) + (kk + 1);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int64_t j = i - 1 + e;
-      const int64_t k0 = j - (j >= T.bound ? T.bound : T.kb);
-      const int64_t kk = k0 > 0 ? k0 : (int64_t)0;                // (>= 0: clamped rows)
-      L->rr[e] = *reinterpret_cast<const d2n*>(N.resp + 2 * (kk + 1));
-    }
+    for (int e = 0; e < 4; ++e) L->rr[e] = rr[e];
   }
 }
 __device__ __forceinline__ void nco4_eval(const NcoSrc& N, const NcoTile& T, int64_t i, const Nco4Ld& L, bool lin,

@@ -5,6 +5,8 @@ pseudo-blocks solved from warm-up guesses and chained).  Compared with the oracl
 restatement of model/fmPll.py:4-46 over chained blocks, and the solver counters
 (sdr_pll_stats) asserted, so a solve that silently fell back to the sequential kernel fails
 here.  Run on an MI355X: pytest -m gpu."""
+import time
+
 import numpy as np
 import pytest
 
@@ -27,12 +29,15 @@ def fresh_counters(gpu_ctx):
     gpu_ctx.pll_stats(reset=True)
 
 
-def chained(sdr, oracle, x, blocks, freq, scale, adj=0.0, bw=0.01):
+def chained(sdr, oracle, x, blocks, freq, scale, adj=0.0, bw=0.01, times=None):
     st = [0.0, 0.0, 1.0, 0.0, 1.0, 0.0]
     sr = list(st)
     err = 0.0
     for a, b in blocks:
+        t0 = time.perf_counter()
         nco, ncoq, st = sdr.fmPll(x[a:b], freq, FS, st, scale, adj, bw)
+        if times is not None:
+            times.append(time.perf_counter() - t0)
         nr, nqr, sr = oracle.fm_pll(x[a:b].astype(np.float64), freq, FS, sr, scale, adj, bw)
         err = max(err, maxabs(nco[1:], nr[1:]), maxabs(ncoq[1:], nqr[1:]))
         assert maxabs(st, sr) < 1e-6, (a, b)
@@ -133,10 +138,14 @@ def test_pll_long_call_unlocked(sdr, gpu_ctx, oracle, offset, noise):
     :4-46) over three chained calls, and the counters must show the non-trivial paths ran."""
     n = 4 * 16384 + 5
     x = pilot(3 * n, 19e3 + offset, seed=int(offset), noise=noise)
-    err = chained(sdr, oracle, x, [(0, n), (n, 2 * n), (2 * n, 3 * n)], 19e3, 2.0)
+    times = []
+    err = chained(sdr, oracle, x, [(0, n), (n, 2 * n), (2 * n, 3 * n)], 19e3, 2.0, times=times)
     assert err < NCO_TOL
     s = gpu_ctx.pll_stats()
-    print(f"offset {offset} noise {noise} solver counters:", s)
+    # the unlocked call's cost, host-to-host (the pseudo-blocks the chain hands to the one-thread
+    # tail run serially, ~30 ns a step: the whole call fully serial would be ~2 ms of loop)
+    print(f"offset {offset} noise {noise} call ms {[round(t * 1e3, 2) for t in times]} solver counters:", s)
     nb = long_blocks(n)
     assert s["recurrences"] == 3 * nb, s
     assert s["long_stops"] + s["long_tail"] + s["sequential"] + s["spec_r1"] + s["spec_r2"] > 0, s
+    assert max(times[1:]) < 0.25, times
