@@ -191,6 +191,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDR_FE_MFMA_
 #pragma unroll
     for (int dg = 0; dg < 3; ++dg) afr[ks][dg] = i4v{w[dg][0], w[dg][1], w[dg][2], w[dg][3]};
   }
+  // the fragments' loads retired here, in the compiler's view: otherwise its wait for them is
+  // merged into the tile loop's top from the entry path and retires the image prefetch (and the
+  // previous tile's stores) at every tile, before the MFMAs instead of after them
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg) asm volatile("" : : "v"(afr[ks][dg]));
   // audio taps reversed (g[j] = h[150 - j]), tap pairs as SGPR operands (scalar loads at
   // compile-time offsets, as rx.hip's fir_tile)
   const cfp4 gr = (cfp4)p.argev;
@@ -560,6 +567,13 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
 #pragma unroll
     for (int dg = 0; dg < 3; ++dg) afr[ks][dg] = i4v{w[dg][0], w[dg][1], w[dg][2], w[dg][3]};
   }
+  // the fragments' loads retired here, in the compiler's view: otherwise its wait for them is
+  // merged into the tile loop's top from the entry path and retires the image prefetch (and the
+  // previous tile's stores) at every tile, before the MFMAs instead of after them
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int dg = 0; dg < 3; ++dg) asm volatile("" : : "v"(afr[ks][dg]));
 
   f4v stg[NL];
   const unsigned voff = 16u * lane;
@@ -584,8 +598,14 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
     *reinterpret_cast<uint2*>(&img[0][8 * c]) = make_uint2(i_lo, i_hi);
     *reinterpret_cast<uint2*>(&img[1][8 * c]) = make_uint2(q_lo, q_hi);
   };
+  // st1: the previous epilogue issued exactly one VMEM op (its demod store) after this
+  // image's loads -- vmcnt counts loads and stores in issue order, so vmcnt(1) retires the
+  // loads and leaves that store in flight; anything else (a tile at a stream's edge: zi loads,
+  // last_phi, the wrap-count atomic, partial stores) waits for everything
+  bool st1 = false;
   auto store_image = [&](bool halo) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (__builtin_amdgcn_readfirstlane((int)st1)) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int cf = halo ? HC : 0;
     if (halo && lane < 2 * HC) {
       const int ch = lane / HC, k = lane - ch * HC;
@@ -722,11 +742,13 @@ __global__ __launch_bounds__(64) void fe_mfma_demod_kernel(MfmaDemod p) {
       }
     }
     // the stream's wrap count leaves with its last tile of this run
-    if (keep && (!more || s_nx != s) && p.wraps != nullptr) {
+    const bool wr = keep && (!more || s_nx != s) && p.wraps != nullptr;
+    if (wr) {
       const int w = wave_sum_i(wsum);
       if (lane == 0 && w != 0) atomicAdd(p.wraps + s, w);
       wsum = 0;
     }
+    st1 = keep && p.vec_out && t > 0 && (int64_t)TO * t + TO < p.M && !wr;
     if (more) {
       s = s_nx;
       t = t_nx;
