@@ -36,7 +36,7 @@ for k in sorted(b, key=lambda k: -sum(dur.get(k, [0]))):
     if k not in dur or "rocclr" in k:
         continue
     us = sum(dur[k]) / len(dur[k])
-    v = b[k].get("SQ_ACTIVE_INST_VALU", 0) * 4 / (us * 2400 * 1024)
+    v = b[k].get("SQ_ACTIVE_INST_VALU", a[k].get("SQ_ACTIVE_INST_VALU", 0)) * 4 / (us * 2400 * 1024)   # (either pass)
     l = b[k].get("SQ_LDS_IDX_ACTIVE", 0) / (us * 2400 * 256)
     w = a[k].get("SQ_WAVES", 1)
     print(f"| `{short(k)}` | {us:.1f} | {v:.2f} | {l:.2f} | {a[k].get('SQ_INSTS_VALU', 0) / w:.0f} | {w:.0f} |")
