@@ -480,7 +480,7 @@ static_assert(SPEC_NMAX == 16384 + 1, "LDS sizing");
 #define SDR_SPEC_N256 10240
 #endif
 constexpr int SPEC_N256 = SDR_SPEC_N256;     // longest call the 256-thread solve takes (512 above; A/B builds: -DSDR_SPEC_N256=)
-constexpr int SPEC_LDS = 32 * 513;           // padded transposed bytes: 512 chunks of <= 32 steps (or 256 of <= 40)
+constexpr int SPEC_LDS = 32 * 516;           // padded transposed bytes: 512 chunks of <= 32 steps (or 256 of <= 40)
 constexpr int SB = 8;                        // steps per batch of LDS reads in the step loops
 
 // ---- long calls: pseudo-block bookkeeping (device scratch P.work; LongBlk / LongHdr in
@@ -546,10 +546,19 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // (jb = floor(phaseEst_1 / 2pi)).  tb: per wave, SB steps x 64 chunks of phases on their
   // way to coalesced theta stores (stride TBS = 4 mod 32 doubles: both its write and its
   // transposed read are conflict-free); the chunk scans' scratch (yb) shares its space.
-  constexpr int CSTR = SPEC_T + 1, NW = SPEC_T / 64, TBS = 68;
+  // CSTR = 4 mod 256 bytes: the staging's byte writes (consecutive lanes on consecutive rows)
+  // fall in consecutive banks -- SPEC_T + 1 put every 4 lanes in one bank; the padding column
+  // SPEC_T stays
+  constexpr int CSTR = SPEC_T + 4, NW = SPEC_T / 64, TBS = 68;
+  static_assert(CSTR * (SPEC_T == 512 ? 32 : 40) <= SPEC_LDS, "rows fit");
   static_assert(NW * SB * TBS >= 2 * SPEC_T, "yb fits in tb");
   __shared__ int8_t code[SPEC_LDS];
-  __shared__ int8_t mrel[SPEC_LDS];
+  // the integers m_k chunk-major (a thread's own steps contiguous): MSTR an odd number of dwords,
+  // so the 64 lanes' per-step byte accesses fall in 64 different banks (step-major put four
+  // lanes in every dword)
+  constexpr int MSTR = SPEC_T == 512 ? 36 : 44;
+  static_assert(MSTR >= (SPEC_T == 512 ? 32 : 40) && (MSTR / 4) % 2 == 1 && MSTR % 4 == 0, "m_k rows");
+  __shared__ int8_t mrel[SPEC_T * MSTR];
   __shared__ double tb[NW * SB * TBS];
   __shared__ d2v wsum[NW];
   __shared__ Mat2 qp[10];
@@ -878,7 +887,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
           const bool act = F || i < len;
           bad |= act && cd[u] == 0;                // a 0 / NaN input: the general form's case
           const double f = __builtin_amdgcn_fract(t);
-          if (act) mrel[i * CSTR + tid] = floor_byte(t, f);
+          if (act) mrel[tid * MSTR + i] = floor_byte(t, f);
           const double S = p + V;
           const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
           if constexpr (F) {
@@ -995,7 +1004,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
 #pragma unroll
             for (int v = 0; v < SB / 2; ++v) {
               cd[v] = code[(i0 + u + v) * CSTR + tid];
-              mm[v] = mrel[(i0 + u + v) * CSTR + tid];
+              mm[v] = mrel[tid * MSTR + i0 + u + v];
             }
           }
           const int i = i0 + u;
@@ -1020,7 +1029,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
             mlo = min(mlo, own ? fb : 0x3f800000u);
             mhi = max(mhi, own ? fb : 0u);
           }
-          if (act) mrel[i * CSTR + tid] = r;
+          if (act) mrel[tid * MSTR + i] = r;
           tw[u * TBS + lane] = thval(p, k0 + i);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
