@@ -554,9 +554,13 @@ def compact_line(result: dict) -> dict:
     if "c5" in result:
         r = result["c5"]
         pl = r.get("pll_solver") or {}
-        c5 = _pick(r, ("value", "ms_per_step", "stage_ms", "stage_tflops"))
+        c5 = _pick(r, ("value", "ms_per_step", "stage_ms"))
         c5["pll"] = {k: pl.get(k) for k in ("recurrences", "spec_r0", "sequential", "long_stops", "long_tail")}
-        c5["frac"] = (r.get("roofline") or {}).get("frac")
+        rl = r.get("roofline") or {}
+        c5["roofline"] = {"stage": rl.get("kernel_stage"), "bound": rl.get("bound"), "frac": rl.get("frac")}
+        sr = (r.get("stage_roofline") or {}).get("stages") or {}
+        c5["stage_roofline"] = {k: [v.get("bound"), v.get("frac")] for k, v in sr.items()}
+        c5["pll_roofline"] = (r.get("pll_roofline") or {}).get("frac")
         c5["cpu"] = cpu_v(r)
         out["c5"] = c5
     return out
@@ -837,27 +841,22 @@ F64_WAVE_INSTR_PEAK = 256 * 4 * 2.4e9 / 4
 
 
 def pll_roofline(stage_ms_pll, S, K, B, steps_per_span, path=None):
-    """The PLL stage against the f64 VALU issue rate, from committed SQ counts of its kernels
-    (tools/pmc_pll.py over rocprofv3 --pmc passes of the same configuration) and the stage time
-    measured in this run.  None when no counts for this configuration are committed."""
-    path = path or os.path.join(ROOT, "profiles", "r04", "pll_pmc.json")
+    """The PLL stage against the f64 VALU issue rate, from the committed SQ counts of its kernels
+    (tools/pmc_c5.py over rocprofv3 --pmc passes of the same configuration: pll_spec_kernel +
+    pll_long_fix_kernel) and the stage time measured in this run.  None when no counts for this
+    configuration are committed."""
+    path = path or C5_PMC
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if t.get("config", {}).get("streams") != S or t.get("config", {}).get("span") != K:
+    cfg = t.get("config", {})
+    if cfg.get("streams") != S or cfg.get("span") != K or cfg.get("block_complex") != B:
         return None
-    f64 = valu = 0.0
-    names = []
-    for k, c in t["kernels"].items():
-        if not ("pll_spec" in k or "pll_long" in k):
-            continue
-        names.append(k)
-        f64 += sum(c.get(n, 0.0) for n in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
-                                             "SQ_INSTS_VALU_TRANS_F64"))
-        valu += c.get("SQ_INSTS_VALU", 0.0)
-    if not names or stage_ms_pll <= 0:
+    c = t.get("stages", {}).get("pll") or {}
+    f64, valu = c.get("f64_wave_instr", 0.0), c.get("valu_wave_instr", 0.0)
+    if not f64 or stage_ms_pll <= 0:
         return None
     rate = f64 / (stage_ms_pll * 1e-3)
     return {"bound": "f64 VALU issue", "achieved": round(rate / 1e9, 2), "peak": round(F64_WAVE_INSTR_PEAK / 1e9, 1),
@@ -865,8 +864,66 @@ def pll_roofline(stage_ms_pll, S, K, B, steps_per_span, path=None):
             "f64_wave_instr_per_span": f64, "valu_wave_instr_per_span": valu,
             "f64_lane_ops_per_step": round(64 * f64 / steps_per_span, 2),
             "valu_lane_ops_per_step": round(64 * valu / steps_per_span, 2),
-            "kernels": names, "stage_ms": stage_ms_pll,
-            "source": os.path.relpath(path, ROOT) + " (SQ counts per dispatch) + this run's PLL stage time"}
+            "kernels": c.get("kernels"), "stage_ms": stage_ms_pll,
+            "source": os.path.relpath(path, ROOT) + " (SQ counts per span call) + this run's PLL stage time"}
+
+
+MFMA_F16_PEAK_TFLOPS = 2500.0    # dense f16 / bf16 matrix-core peak (MI355X_MICROARCH.md; not the 2:1-sparse figure)
+MFMA_I8_PEAK_TOPS = 5000.0       # dense int8 matrix-core peak: 2x the f16 rate per clock (MI355X_MICROARCH.md)
+C5_PMC = os.path.join(ROOT, "profiles", "r06", "c5_pmc.json")
+
+
+def c5_stage_roofline(stage_ms, S, K, B, path=C5_PMC):
+    """Each C5 span stage against the ceilings it can hit: HBM bytes / s vs 8 TB/s, executed
+    matrix-core ops / s vs the dense f16 (2.5 PF) or int8 (5 POPS) peak, f64 VALU wave-
+    instructions / s vs the f64 issue rate -- from committed per-stage counts of the same
+    configuration (tools/pmc_c5.py over rocprofv3 --pmc passes of `bench.py --workload c5`) and
+    THIS run's per-stage times (solo).  `bound` is the ceiling the stage comes closest to and
+    `frac` its fraction.  None when no counts for this configuration are committed."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    cfg = t.get("config", {})
+    if cfg.get("streams") != S or cfg.get("span") != K or cfg.get("block_complex") != B:
+        return None
+    out = {}
+    for st, c in t["stages"].items():
+        ms = stage_ms.get(st, 0.0)
+        if ms <= 0:
+            continue
+        sec = ms * 1e-3
+        e = {"ms": ms}
+        if "hbm_read_bytes" in c and "hbm_write_bytes" in c:
+            gbs = (c["hbm_read_bytes"] + c["hbm_write_bytes"]) / sec / 1e9
+            e["hbm"] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        if c.get("mfma_ops_f16"):
+            tf = c["mfma_ops_f16"] / sec / 1e12
+            e["mfma_f16"] = {"achieved_tflops": round(tf, 1), "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4)}
+        if c.get("mfma_ops_i8"):
+            to = c["mfma_ops_i8"] / sec / 1e12
+            e["mfma_i8"] = {"achieved_tops": round(to, 1), "frac": round(to / MFMA_I8_PEAK_TOPS, 4)}
+        if c.get("f64_wave_instr"):
+            g = c["f64_wave_instr"] / sec
+            e["f64_issue"] = {"achieved_g_wave_instr_s": round(g / 1e9, 1), "frac": round(g / F64_WAVE_INSTR_PEAK, 4)}
+        lim = {k: v["frac"] for k, v in e.items() if isinstance(v, dict)}
+        if lim:
+            e["bound"] = max(lim, key=lim.get)
+            e["frac"] = lim[e["bound"]]
+        out[st] = e
+    return {"stages": out, "source": os.path.relpath(path, ROOT) + " (per-stage counts per span call) + this run's "
+                                                                    "stage times"}
+
+
+def c5_stage_bytes(stage, path=C5_PMC):
+    """HBM bytes (read + write, PMC) of one C5 stage per span call, or None"""
+    try:
+        with open(path) as f:
+            c = json.load(f)["stages"][stage]
+        return c["hbm_read_bytes"] + c["hbm_write_bytes"]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def chain_flops_per_sample(rf_taps=151, taps=151, audio_decim=5, up=19, down=80):
@@ -989,14 +1046,23 @@ def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, arg
     if pr is not None:
         out["pll_roofline"] = pr
     if fps is not None:
-        per_gpu_tflops = fps * S * n * steps / elapsed / 1e12
-        out["roofline"] = {"bound": "valu", "achieved": round(per_gpu_tflops, 3), "peak": VALU_PEAK_TFLOPS,
-                           "unit": "TFLOP/s", "frac": round(per_gpu_tflops / VALU_PEAK_TFLOPS, 4), "traffic": None,
-                           "flops_per_sample": round(fps, 2),
-                           "note": ("f32-equivalent FIR flops of the whole chain per input sample x samples / wall time "
-                                    "per GPU, against the FP32 VALU peak the direct form would be capped at; span "
-                                    "rows run their filters on the matrix cores (f16 hi/lo splits, 3 MFMA products "
-                                    "per multiply-add), so frac > 1 is possible; pll_roofline bounds the PLL")}
+        # the chain's f32-equivalent FIR rate (2 flops per useful multiply-add, whatever unit runs it):
+        # a throughput figure, not a roofline fraction (the span filters run on the matrix cores)
+        out["chain_f32eq_tflops"] = round(fps * S * n * steps / elapsed / 1e12, 3)
+    sr = c5_stage_roofline(stage_ms, S, K, B) if (stereo and rds and u8) else None
+    if sr is not None:
+        out["stage_roofline"] = sr
+        # the line's roofline: the dominant stage's own, against the ceiling it comes closest to
+        d = sr["stages"].get(dom)
+        if d is not None and "bound" in d:
+            unit = {"hbm": "GB/s", "mfma_f16": "TFLOP/s", "mfma_i8": "TOP/s", "f64_issue": "G f64 wave-instr/s"}[d["bound"]]
+            ach = next(v for k, v in d[d["bound"]].items() if k.startswith("achieved"))
+            peak = {"hbm": HBM_PEAK_GBS, "mfma_f16": MFMA_F16_PEAK_TFLOPS, "mfma_i8": MFMA_I8_PEAK_TOPS,
+                    "f64_issue": round(F64_WAVE_INSTR_PEAK / 1e9, 1)}[d["bound"]]
+            out["roofline"] = {"bound": d["bound"], "kernel_stage": dom, "achieved": ach, "peak": peak, "unit": unit,
+                               "frac": d["frac"], "traffic": c5_stage_bytes(dom),
+                               "note": ("the dominant stage's own ceiling (stage_roofline); traffic: its HBM bytes per "
+                                        "span call (PMC)")}
     if cpu and args is not None:
         out["cpu_baseline"] = ref_rx_baseline(args, cpu_rows, B, u8, stereo, rds, rf_taps)
     return out

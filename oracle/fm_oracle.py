@@ -178,9 +178,18 @@ def rds_coeffs(taps=151):
 
 
 def mono_stereo_blocks(iq, block_complex, rf_taps=151, audio_taps=151, stereo=True, nblocks=None,
-                       demod_fn=fm_demod_arctan, pll_fn=fm_pll):
+                       demod_fn=fm_demod_arctan, pll_fn=fm_pll, alt_in=None, alt_from=0):
     """Restatement of the model/fmMonoBlock.py:80-173 loop (fmPll unpack fixed, intended
-    combiner).  iq: interleaved float32.  Returns a list of per-block dicts."""
+    combiner).  iq: interleaved float32.  Returns a list of per-block dicts.
+
+    alt_in (test infrastructure for the device's own PLL inputs): a function k -> block k's
+    pilot-BPF row to run a SECOND fmPll on (state carried from the stream start like the first)
+    and the same mixer / LPF / combiner statements after it, with their own filter states; block
+    k's dict then holds r["alt"] = {"nco", "stereo", "left", "right"}.  The PLL and everything
+    after it depend on the PLL input only, so this chain is the reference's on that input.  Its
+    downstream statements run from block alt_from - 1 on (zero filter state there: an FIR's zf
+    depends only on its last taps - 1 inputs, so blocks >= alt_from are exact); the second PLL
+    runs on every block (its state)."""
     rf_b, au_b = mono_coeffs(rf_taps, audio_taps)
     pil_b, ext_b, st_b = stereo_coeffs(151)
     B = 2 * block_complex
@@ -188,8 +197,22 @@ def mono_stereo_blocks(iq, block_complex, rf_taps=151, audio_taps=151, stereo=Tr
     zi_q = np.zeros(rf_taps - 1)
     phase = 0.0
     au_zi = np.zeros(audio_taps - 1)
-    rec_zi, ext_zi, st_zi = np.zeros(150), np.zeros(150), np.zeros(150)
+    rec_zi, ext_zi = np.zeros(150), np.zeros(150)
     pll_state = [0.0, 0.0, 1.0, 0.0, 1.0, 0.0]
+    chains = [{"pll": pll_state, "st_zi": np.zeros(150)}]
+    if alt_in is not None:
+        chains.append({"pll": list(pll_state), "st_zi": np.zeros(150)})
+
+    def stereo_tail(r, c, x):
+        nco, _, c["pll"] = pll_fn(x, 19e3, 240e3, list(c["pll"]), 2)
+        o = {"nco": nco}
+        if c is chains[0] or k >= alt_from - 1:
+            mixed = np.multiply(nco[0:len(r["bpf_extraction"])], r["bpf_extraction"]) * 2
+            s_f, c["st_zi"] = lfilter_fir(st_b, mixed, c["st_zi"])
+            o["stereo"] = s_f[::5].copy()
+            o["left"] = (r["audio"] + o["stereo"]) / 2
+            o["right"] = (r["audio"] - o["stereo"]) / 2
+        return o
     out = []
     k = 0
     while (k + 1) * B < len(iq) and (nblocks is None or k < nblocks):   # strict "<" as :80
@@ -204,14 +227,10 @@ def mono_stereo_blocks(iq, block_complex, rf_taps=151, audio_taps=151, stereo=Tr
         r["phase"] = phase
         if stereo:
             r["bpf_recovery"], rec_zi = lfilter_fir(pil_b, r["demod"], rec_zi)
-            nco, _, pll_state = pll_fn(r["bpf_recovery"], 19e3, 240e3, list(pll_state), 2)
-            r["nco"] = nco
             r["bpf_extraction"], ext_zi = lfilter_fir(ext_b, r["demod"], ext_zi)
-            mixed = np.multiply(nco[0:len(r["bpf_extraction"])], r["bpf_extraction"]) * 2
-            s_f, st_zi = lfilter_fir(st_b, mixed, st_zi)
-            r["stereo"] = s_f[::5].copy()
-            r["left"] = (r["audio"] + r["stereo"]) / 2
-            r["right"] = (r["audio"] - r["stereo"]) / 2
+            r.update(stereo_tail(r, chains[0], r["bpf_recovery"]))
+            if alt_in is not None:
+                r["alt"] = stereo_tail(r, chains[1], np.asarray(alt_in(k), dtype=np.float64))
         out.append(r)
         k += 1
     return out
@@ -274,18 +293,39 @@ def mode1_stereo_blocks(iq, block_complex=153_600, rf_taps=151, nblocks=None):
     return out
 
 
-def rds_blocks(iq_u8, block_values=307200, taps=151, nblocks=None, demod_fn=fm_demod_arctan, pll_fn=fm_pll):
+def rds_blocks(iq_u8, block_values=307200, taps=151, nblocks=None, demod_fn=fm_demod_arctan, pll_fn=fm_pll,
+               alt_in=None, alt_from=0):
     """Restatement of model/fmRDSblock.py:127-204 (signal path up to the RRC filter).
-    iq_u8: interleaved uint8, normalised (x-128)/128 as :59."""
+    iq_u8: interleaved uint8, normalised (x-128)/128 as :59.  alt_in / alt_from: a second
+    fmPll on the rows alt_in(k) (the device's own pre-PLL rows) and the mixer -> LPF ->
+    resampler -> RRC statements after it, as mono_stereo_blocks' (r["alt"])."""
     iq = (np.asarray(iq_u8, dtype=np.float64) - 128.0) / 128.0
     rf_b, _ = mono_coeffs(taps, 151)
     co = rds_coeffs(taps)
     z = lambda: np.zeros(taps - 1)  # noqa: E731
     zi_i, zi_q, phase = z(), z(), 0.0
-    ex_zi, sq_zi, li_zi, lq_zi, ai_zi, aq_zi = z(), z(), z(), z(), z(), z()
-    ri_zi, rq_zi = np.zeros(150), np.zeros(150)
+    ex_zi, sq_zi = z(), z()
     pll_state = [0.0, 0.0, 1.0, 0.0, 1.0, 0.0]
     phase_adj = math.pi / 3.3 - math.pi / 1.5
+
+    def chain():
+        return {"pll": list(pll_state), "li": z(), "lq": z(), "ai": z(), "aq": z(), "ri": np.zeros(150),
+                "rq": np.zeros(150)}
+    chains = [chain()] + ([chain()] if alt_in is not None else [])
+
+    def rds_tail(r, c, x):
+        nco_i, nco_q, c["pll"] = pll_fn(x, 114000, 240000, list(c["pll"]), ncoScale=0.5,
+                                        phaseAdjust=phase_adj, normBandwidth=0.001)
+        o = {"nco_i": nco_i, "nco_q": nco_q}
+        if c is chains[0] or k >= alt_from - 1:
+            n = len(r["extract"])
+            o["lpf_i"], c["li"] = lfilter_fir(co["lpf"], np.multiply(r["extract"], nco_i[0:n]) * 2, c["li"])
+            o["lpf_q"], c["lq"] = lfilter_fir(co["lpf"], np.multiply(r["extract"], nco_q[0:n]) * 2, c["lq"])
+            o["resample_i"], c["ai"] = resample(o["lpf_i"], co["anti_img"], c["ai"], 19, 80)
+            o["resample_q"], c["aq"] = resample(o["lpf_q"], co["anti_img"], c["aq"], 19, 80)
+            o["rrc_i"], c["ri"] = lfilter_fir(co["rrc"], o["resample_i"], c["ri"])
+            o["rrc_q"], c["rq"] = lfilter_fir(co["rrc"], o["resample_q"], c["rq"])
+        return o
     out = []
     k = 0
     while (k + 1) * block_values < len(iq) and (nblocks is None or k < nblocks):   # :127
@@ -296,16 +336,9 @@ def rds_blocks(iq_u8, block_values=307200, taps=151, nblocks=None, demod_fn=fm_d
         r["demod"], phase = demod_fn(i_f[::10].copy(), q_f[::10].copy(), phase)
         r["extract"], ex_zi = lfilter_fir(co["extract"], r["demod"], ex_zi)
         r["pre_pll"], sq_zi = lfilter_fir(co["square"], np.square(r["extract"]), sq_zi)
-        nco_i, nco_q, pll_state = pll_fn(r["pre_pll"], 114000, 240000, list(pll_state), ncoScale=0.5,
-                                         phaseAdjust=phase_adj, normBandwidth=0.001)
-        r["nco_i"], r["nco_q"] = nco_i, nco_q
-        n = len(r["extract"])
-        r["lpf_i"], li_zi = lfilter_fir(co["lpf"], np.multiply(r["extract"], nco_i[0:n]) * 2, li_zi)
-        r["lpf_q"], lq_zi = lfilter_fir(co["lpf"], np.multiply(r["extract"], nco_q[0:n]) * 2, lq_zi)
-        r["resample_i"], ai_zi = resample(r["lpf_i"], co["anti_img"], ai_zi, 19, 80)
-        r["resample_q"], aq_zi = resample(r["lpf_q"], co["anti_img"], aq_zi, 19, 80)
-        r["rrc_i"], ri_zi = lfilter_fir(co["rrc"], r["resample_i"], ri_zi)
-        r["rrc_q"], rq_zi = lfilter_fir(co["rrc"], r["resample_q"], rq_zi)
+        r.update(rds_tail(r, chains[0], r["pre_pll"]))
+        if alt_in is not None:
+            r["alt"] = rds_tail(r, chains[1], np.asarray(alt_in(k), dtype=np.float64))
         out.append(r)
         k += 1
     return out

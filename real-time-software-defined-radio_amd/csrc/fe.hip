@@ -553,10 +553,7 @@ __global__ __launch_bounds__(64) void fe_ring_kernel(FeParams p, TapsF32 taps, R
   // FUSED, r04b: 16 audio blocks (48 VGPRs of queue, 20 of them AGPRs) hold a whole run of the
   // 128-block step (13.4 blocks per wave), so no flush goes out mid-run beside the read stream
   // (12: one at block 12 of every wave at once); A/B 0.738 -> 0.747 of HBM on one box
-#ifndef SDR_RING_QN
-#define SDR_RING_QN 16
-#endif
-  constexpr int QN = FUSED ? SDR_RING_QN : 36;
+  constexpr int QN = FUSED ? 16 : 36;             // (fixed constants)
   OutQ3<QN> oq;
   int qn = 0, qs = 0;
   int64_t q0 = 0;                                  // FE: first tile; FUSED: first audio block

@@ -455,31 +455,22 @@ __global__ __launch_bounds__(128) void pll_chunk_kernel(PllJobs P) {
 // literal general step (fI, fQ from the caller's state), as in the loop kernels.  A completed
 // recurrence is marked by c[0] = +inf (c[0] is the literal sample's slot: the loop kernels
 // never read it, and the prep kernel rewrites it every call).
-#ifndef SDR_SPEC_W
-#define SDR_SPEC_W 32
-#endif
-// warm-up samples before each chunk (A/B builds: -DSDR_SPEC_W=).  r04: 32 -- the guess runs
+// warm-up samples before each chunk (a fixed constant; r03-r05 A/B builds measured it).  r04: 32 -- the guess runs
 // the true step from the measured phase, and in the per-block solve of one recurrence (C4, a
 // 256-thread workgroup: one wave per SIMD, no other wave to hide the f64 latency behind) the
 // 128-step warm-up was 40 % of the kernel (spec_prof: 22 k of 52 k cycles).  r03, per-block solves at 64
 // streams x 2 PLLs (profiles/r03/iter/specw_*): 256 -> 86 us, 128 -> 73 us, 64 -> 66 us per
 // block, every recurrence in round 0 at each, the offset sweep (tests/test_offsets.py) too;
 // 128 keeps a margin for inputs noisier than the synthetic ones
-constexpr int SPEC_W = SDR_SPEC_W;
-#ifndef SDR_SPEC_W_LONG
-#define SDR_SPEC_W_LONG 16
-#endif
+constexpr int SPEC_W = 32;
 // ... in a long call's pseudo-block: its start is a converged guess or the chained state and
 // its drift is measured, so the guess needs little settling (r03 A/B on the S8 K256 span: 0,
 // 16, 32 and 64 steps all solve every pseudo-block in round 0; 16 is the fastest)
-constexpr int SPEC_W_LONG = SDR_SPEC_W_LONG;
+constexpr int SPEC_W_LONG = 16;
 constexpr int SPEC_IT = 3;           // solve / check rounds before the sequential kernel takes over
 constexpr int SPEC_NMAX = SDR_PLL_BLOCK_MAX; // samples per call (the sign codes of steps 1.. in LDS: 16 KiB)
 static_assert(SPEC_NMAX == 16384 + 1, "LDS sizing");
-#ifndef SDR_SPEC_N256
-#define SDR_SPEC_N256 10240
-#endif
-constexpr int SPEC_N256 = SDR_SPEC_N256;     // longest call the 256-thread solve takes (512 above; A/B builds: -DSDR_SPEC_N256=)
+constexpr int SPEC_N256 = 10240;             // longest call the 256-thread solve takes (512 above; fixed, r04 A/B)
 constexpr int SPEC_LDS = 32 * 516;           // padded transposed bytes: 512 chunks of <= 32 steps (or 256 of <= 40)
 constexpr int SB = 8;                        // steps per batch of LDS reads in the step loops
 

@@ -1158,15 +1158,6 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(sm_wpe<MI
   }
 }
 
-// The matrix-core path (SDR_RX_MMA=0 in the environment: the VALU pair tiles throughout)
-bool mma_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("SDR_RX_MMA");
-    return e == nullptr || std::strcmp(e, "0") != 0;
-  }();
-  return on;
-}
-
 // outputs per tile of a job in a launch of tap class `key` (as rx_stage_kernel<key> picks the tile)
 int64_t tile_outputs(const StageJob& j, int key) {
   static_assert(PairShape<151, 2>::TO == FirShape<151, 1, 4>::TO && PairShape<151, 8>::TO == FirShape<151, 1>::TO &&
@@ -1203,7 +1194,7 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
                      j.nco.theta != nullptr && al16(j.mono, j.y_stride) && al16(j.left, j.y_stride) &&
                      al16(j.right, j.y_stride);
     const bool mono = j.pre == PRE_NONE && j.mono == nullptr;
-    if (!(mma_enabled() && j.kind == JK_FIR && j.D == SM_D && j.T == 151 && (mix || mono) && al16(j.y, j.y_stride) &&
+    if (!(j.kind == JK_FIR && j.D == SM_D && j.T == 151 && (mix || mono) && al16(j.y, j.y_stride) &&
           j.x != nullptr && j.n >= (int64_t)MM_MIN_WIN * MM_WT && j.n < (int64_t)1 << 28 && j.n % 4 == 0))
       continue;                                      // (n = 0 mod 4: the chunks' edges, mix_load)
     const int64_t wins = (j.n / SM_D + 256) / 256 * S;
@@ -1227,7 +1218,6 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
   }
   for (int key : {151, 101})
     for (int wide : {1, 0}) {                        // groups of 2-3 filters / single filters
-      if (!mma_enabled()) break;
       StageJobs Q{};
       Q.nstreams = S;
       std::vector<size_t> members;
@@ -2409,7 +2399,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       if (grid > 0x7fffffff || r->zlen[Z_ANTI_I] != J.zs) return fail(SDR_EINVAL, "sdr_rx: composite RDS geometry");
       // spans: the matrix-core form (per job length, as launch_stage decides: a stream's outputs
       // do not depend on how many streams share the launch)
-      if (mma_enabled() && M >= (int64_t)MM_MIN_WIN * MM_WT && M % 4 == 0 && J.nco.theta != nullptr) {
+      if (M >= (int64_t)MM_MIN_WIN * MM_WT && M % 4 == 0 && J.nco.theta != nullptr) {
         const int64_t wins = ceil_div(r->R, CM_WO) * S;
         const int wgs = (int)std::min<int64_t>(CM_WGS, ceil_div(wins, 4));
         hipLaunchKernelGGL(rx_cresmm_kernel, dim3((unsigned)(S + wgs)), dim3(RX_NT), 0, st, J, r->ctaps + CR_NTAPS, wgs);

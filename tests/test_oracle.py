@@ -54,6 +54,28 @@ def test_rds_chain_matches_golden(oracle, golden):
             assert maxabs(r[key], g[key][k]) < 1e-9 * scale, (key, k)
 
 
+def test_oracle_alt_chain_is_the_chain(oracle, golden):
+    """The second fmPll + downstream chain the span tests run on the device's loop inputs
+    (alt_in / alt_from, tests/test_span.py): fed the oracle's own inputs, it reproduces the main
+    chain -- the PLL bit for bit, every downstream row from block alt_from on (its filters start
+    one block early from zero state) to rounding."""
+    g = golden("mono_t151.npz")
+    iq = golden("mono_t101.npz")["iq"]
+    B = int(g["block"][0])
+    base = oracle.mono_stereo_blocks(iq, B)
+    out = oracle.mono_stereo_blocks(iq, B, alt_in=lambda k: base[k]["bpf_recovery"], alt_from=2)
+    assert np.array_equal(out[0]["alt"]["nco"], out[0]["nco"]) and "stereo" not in out[0]["alt"]
+    for k in (2,):
+        for key in ("nco", "stereo", "left", "right"):
+            assert maxabs(out[k]["alt"][key], out[k][key]) < TIGHT, (key, k)
+    r = golden("rds_u8.npz")
+    rb = oracle.rds_blocks(r["iq"], 307200)
+    ro = oracle.rds_blocks(r["iq"], 307200, alt_in=lambda k: rb[k]["pre_pll"], alt_from=1)
+    for k in range(len(ro)):
+        for key in ("nco_i", "nco_q", "lpf_i", "lpf_q", "resample_i", "resample_q", "rrc_i", "rrc_q"):
+            assert maxabs(ro[k]["alt"][key], ro[k][key]) < TIGHT, (key, k)
+
+
 def test_mono_basic_matches_golden(oracle, golden):
     g = golden("basic_t101.npz")
     audio, wav = oracle.mono_basic(g["iq"], rf_taps=101)

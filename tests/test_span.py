@@ -27,17 +27,39 @@ SPAN_REL = {"demod": 2e-6, "audio": 2e-6, "stereo": 2e-6, "left": 2e-6, "right":
             "rrc_i": 4e-6, "rrc_q": 3e-5}
 
 
-# A PLL's phase detector takes the sign of its input (model/fmPll.py), so where the span and the
-# block loop round an input sample to opposite sides of zero (a sample within ~1e-9 of 0: rare,
-# but 7.8 M samples per recurrence make it a matter of seeds and filter arithmetic) the two loops
-# legitimately part for a while.  Blocks within FLIP_SPAN after such a sign flip of a loop's
-# input compare that loop's outputs at FLIP_REL; every other block at SPAN_REL.
-FLIP_SPAN, FLIP_REL, FLIP_MAX = 3, 5e-2, 3
+# A PLL's phase detector takes the sign of its input (model/fmPll.py:24-27), so where two correct
+# computations of a loop's input (the span and the per-block VALU loop; f32 and the oracle's f64)
+# round a sample within the rounding of zero to opposite sides, the two loops legitimately part for
+# a while (a ~4e-3 NCO transient that decays within a block; an RDS I / Q row's window is taken
+# relative to the I / Q pair's peak).  Such a FLIP is counted only where
+# every sign-mismatched sample lies within FLIP_NEAR of zero (relative to the row's peak: the
+# input rows' own tolerance) -- a wrong-sign sample any larger fails the test -- and at most
+# FLIP_MAX per stream and comparison.  Blocks within FLIP_SPAN after a flip compare that loop's
+# outputs at FLIP_REL (~2.5x the largest window measured, 5.9e-3), every other block at the tight
+# tolerances.  The oracle checks do not rely on this: they also run the oracle's fmPll on the
+# device's OWN loop inputs (identical signs, so no flip can occur) and the oracle's mixers and
+# filters after it, and compare every block at the tight tolerances (_check_oracle_block).
+FLIP_SPAN, FLIP_REL, FLIP_MAX = 3, 1.5e-2, 3
+FLIP_NEAR = {"bpf_recovery": 2e-6, "pre_pll": 5e-6}
 FLIP_DEPS = {"bpf_recovery": ("nco", "stereo", "left", "right"),
              "pre_pll": ("nco_i", "nco_q", "lpf_i", "lpf_q", "resample_i", "resample_q", "rrc_i", "rrc_q")}
+# the device's NCO rows against the oracle's fmPll run on the device's own loop inputs
+NCO_REPLAY = 1e-7
 
 
-def _transient_blocks(row, tables, blocks, max_flips=None):
+def _flips(src, got, want):
+    """True when `got` and `want` (one block of the loop input src) differ in sign anywhere;
+    asserts that every such sample lies within FLIP_NEAR of zero"""
+    bad = np.sign(got) != np.sign(want)
+    if not np.any(bad):
+        return False
+    peak = max(float(np.max(np.abs(want))), 1e-3)
+    far = float(np.max(np.abs(np.asarray(want, dtype=np.float64)[bad]))) / peak
+    assert far <= FLIP_NEAR[src], (src, "a wrong-sign sample far from zero", far)
+    return True
+
+
+def _transient_blocks(row, tables, blocks, max_flips=FLIP_MAX):
     """{block k: the outputs inside a FLIP_SPAN window after a sign flip of their loop's input}
     between a span (row(src, k, n) = block k's n samples of output src) and per-block tables
     (tables[src][k][src]: the block loop's or the oracle's loop input), over `blocks` in order"""
@@ -46,13 +68,27 @@ def _transient_blocks(row, tables, blocks, max_flips=None):
     for k in blocks:
         for src in FLIP_DEPS:
             want = tables[src][k][src]
-            if np.any(np.sign(row(src, k, len(want))) != np.sign(want)):
+            if _flips(src, row(src, k, len(want)), want):
                 last[src] = k
                 flips.append((src, k))
         out[k] = {nm for src, deps in FLIP_DEPS.items() if k - last[src] <= FLIP_SPAN for nm in deps}
     print("loop-input sign flips against the block tables (source, block):", flips)
-    assert max_flips is None or len(flips) <= max_flips, flips
+    assert len(flips) <= max_flips, flips
     return out
+
+
+def _oracle_blocks(oracle, iq_u8, nblk, rec, pre, alt_from=0):
+    """The oracle's block loops (model/fmMonoBlock.py:80-173, model/fmRDSblock.py:127-204; fmPll
+    by its C restatement, bit-identical to the Python one) over a u8 stream's first nblk
+    blocks, each block also with r["alt"]: the oracle's fmPll run on the device's own loop
+    inputs (rec(k): its bpf_recovery row, pre(k): its pre_pll row, block k) and the oracle's
+    mixer / LPF / resampler / RRC / combiner after it"""
+    f = (iq_u8.astype(np.float64) - 128.0) / 128.0
+    mono = oracle.mono_stereo_blocks(f, B5, rf_taps=151, audio_taps=151, nblocks=nblk, pll_fn=oracle.fm_pll_c,
+                                     alt_in=rec, alt_from=alt_from)
+    rds = oracle.rds_blocks(iq_u8, 2 * B5, taps=151, nblocks=nblk, pll_fn=oracle.fm_pll_c, alt_in=pre,
+                            alt_from=alt_from)
+    return mono, rds
 
 
 def _concat_blocks(rows, name):
@@ -114,15 +150,17 @@ def test_span_receiver_equals_block_loop_and_oracle(sdr, gpu_ctx, oracle):
     # the span's carried states continue the block loop's
     for a, b in zip(span_rx.state(), per_rx.state()):
         assert maxabs(a, b) < 1e-6
-    # against the oracle (stream 0, every block)
-    f = (iq[0].astype(np.float64) - 128.0) / 128.0
-    mono = oracle.mono_stereo_blocks(f, B5, rf_taps=151, audio_taps=151, nblocks=nblk)
-    rds = oracle.rds_blocks(iq[0], 2 * B5, taps=151, nblocks=nblk)
+    # against the oracle (stream 0, every block; the loops also on the span's own inputs)
+    M = B5 // 10
+    dev = lambda src: lambda k: span_row(0)(src, k, M)   # noqa: E731
+    mono, rds = _oracle_blocks(oracle, iq[0], nblk, dev("bpf_recovery"), dev("pre_pll"))
     trans = _transient_blocks(span_row(0), {"bpf_recovery": mono, "pre_pll": rds}, range(nblk))
+    errs = {}
     for k in range(nblk):
         sp, kk = divmod(k, K)
         g = got[sp]
-        _check_oracle_block(g, lambda key: g[key][0], kk, mono[k], rds[k], trans[k], (k,))
+        _check_oracle_block(lambda key: g[key][0], kk, mono[k], rds[k], trans[k], (k,), errs)
+    _print_errs(errs)
 
 
 def test_span_bench_shape_matches_block_loop_and_oracle(sdr, gpu_ctx, oracle):
@@ -132,8 +170,8 @@ def test_span_bench_shape_matches_block_loop_and_oracle(sdr, gpu_ctx, oracle):
     Checked against (a) the per-block receiver over all 512 blocks (the reference's block
     loop) at SPAN_REL, and (b) the oracle (model/fmMonoBlock.py:80-173,
     model/fmRDSblock.py:127-204, run over all 512 blocks with the C restatement of fmPll,
-    bit-identical to the Python one) on the first two and last two blocks of each span; the
-    solver counters of the locked span: every pseudo-block solved in parallel in round 0, no
+    bit-identical to the Python one) on every block, its loops also run on the span's own
+    inputs (_check_oracle_block); the solver counters of the locked span: every pseudo-block solved in parallel in round 0, no
     chain stop, no sequential tail."""
     K, spans = 256, 2
     nblk = K * spans
@@ -155,8 +193,6 @@ def test_span_bench_shape_matches_block_loop_and_oracle(sdr, gpu_ctx, oracle):
     per_rx = sdr.Receiver(1, B5, **kw)
     M = B5 // 10
     peak, worst, loose = {}, {}, {}
-    keep = {0, 1, K - 2, K - 1}
-    per_keep = {}
     last_flip = {src: -10 ** 9 for src in FLIP_DEPS}
     flips = []
     for k in range(nblk):
@@ -171,8 +207,7 @@ def test_span_bench_shape_matches_block_loop_and_oracle(sdr, gpu_ctx, oracle):
             blk[name] = (g, w)
             peak[name] = max(peak.get(name, 0.0), float(np.max(np.abs(w))))
         for src in FLIP_DEPS:
-            g, w = blk[src]
-            if np.any(np.sign(g) != np.sign(w)):
+            if _flips(src, *blk[src]):
                 last_flip[src] = k
                 flips.append((src, k))
         for name in NAMES:
@@ -180,8 +215,6 @@ def test_span_bench_shape_matches_block_loop_and_oracle(sdr, gpu_ctx, oracle):
             transient = any(name in deps and k - last_flip[src] <= FLIP_SPAN for src, deps in FLIP_DEPS.items())
             tgt = loose if transient else worst
             tgt[name] = max(tgt.get(name, 0.0), maxabs(g, w))
-        if kk in keep:
-            per_keep[k] = {name: p[name][0] for name in NAMES}
     rel = {name: worst.get(name, 0.0) / max(peak[name], 1e-3) for name in NAMES}
     print("bench-shape span vs block loop, max error relative to peak:", {k: f"{v:.1e}" for k, v in rel.items()})
     print("loop-input sign flips (source, block):", flips, "; their windows:",
@@ -192,47 +225,107 @@ def test_span_bench_shape_matches_block_loop_and_oracle(sdr, gpu_ctx, oracle):
         assert loose.get(name, 0.0) / max(peak[name], 1e-3) < FLIP_REL, (name, loose[name])
     for a, b in zip(span_rx.state(), per_rx.state()):
         assert maxabs(a, b) < 1e-6
-    # (b) the oracle on the first two and last two blocks of each span
-    f = (iq[0].astype(np.float64) - 128.0) / 128.0
-    mono = oracle.mono_stereo_blocks(f, B5, rf_taps=151, audio_taps=151, nblocks=nblk, pll_fn=oracle.fm_pll_c)
-    rds = oracle.rds_blocks(iq[0], 2 * B5, taps=151, nblocks=nblk, pll_fn=oracle.fm_pll_c)
-    A = len(mono[0]["audio"])
+    del per_rx
 
+    # (b) the oracle on every block of both spans, its loops also run on the span's own inputs
     def span_row(src, k, n):
         sp, kk = divmod(k, K)
         return got[sp][src][0][kk * n:(kk + 1) * n]
+    dev = lambda src: lambda k: span_row(src, k, M)    # noqa: E731
+    mono, rds = _oracle_blocks(oracle, iq[0], nblk, dev("bpf_recovery"), dev("pre_pll"))
     trans = _transient_blocks(span_row, {"bpf_recovery": mono, "pre_pll": rds}, range(nblk))
-    for k in sorted(per_keep):
+    errs = {}
+    for k in range(nblk):
         sp, kk = divmod(k, K)
         g = got[sp]
-        _check_oracle_block(g, lambda key: g[key][0], kk, mono[k], rds[k], trans[k], (k,))
+        _check_oracle_block(lambda key: g[key][0], kk, mono[k], rds[k], trans[k], (k,), errs)
+    _print_errs(errs)
 
 
-def _check_oracle_block(g, row, kk, mono_k, rds_k, trans, tag):
-    """block kk of a span's outputs (row(key): the span row) against the oracle's block; the
-    outputs in `trans` (a loop-input sign-flip window) at FLIP_REL of their peak"""
+def _check_oracle_block(row, kk, mono_k, rds_k, trans, tag, errs):
+    """block kk of a span's outputs (row(key): the span row) against the oracle's block:
+      (a) every output upstream of the PLLs (demod, audio, the loops' inputs bpf_recovery /
+          pre_pll, bpf_extraction, extract) against the oracle's own rows;
+      (b) the NCO rows against the oracle's fmPll run on the device's own loop inputs
+          (mono_k["alt"], rds_k["alt"]: same signs, so no flip) at NCO_REPLAY;
+      (c) everything downstream of the PLLs against the oracle's mixers and filters after that
+          NCO, at the tight tolerances;
+      (d) end to end against the oracle's own chain: the outputs in `trans` (a loop-input sign-
+          flip window) at FLIP_REL of their peak, the others as (b) / (c).
+    errs: the worst error per (check, output), updated"""
     A, M = len(mono_k["audio"]), len(mono_k["nco"]) - 1
 
-    def flip_ok(gv, want):
-        return maxabs(gv, want) / max(float(np.max(np.abs(want))), 1e-3) < FLIP_REL
-    for key in ("audio", "stereo", "left", "right"):
-        gv, want = row(key)[kk * A:(kk + 1) * A], mono_k[key]
-        if key in trans:
-            assert flip_ok(gv, want), (key,) + tag
-        else:
-            assert rms(gv, want) < AUDIO_RMS and maxabs(gv, want) < AUDIO_MAX, (key, rms(gv, want)) + tag
-    gv = row("nco")[kk * M:kk * M + M + 1]
-    assert flip_ok(gv, mono_k["nco"]) if "nco" in trans else maxabs(gv, mono_k["nco"]) < 3e-7, tag
-    for key, (tmax, trms) in RDS_TOL.items():
-        want = rds_k[key]
+    def note(key, v):
+        errs[key] = max(errs.get(key, 0.0), v)
+
+    def seg(key, want):
         n = len(want) - 1 if key in NCO_NAMES else len(want)
         gv = row(key)[kk * n:kk * n + len(want)]
+        assert gv.shape == want.shape, (key,) + tag
+        return gv
+
+    def audio_ok(key, gv, want, chk):
+        r, m = rms(gv, want), maxabs(gv, want)
+        note((chk, key), m)
+        assert r < AUDIO_RMS and m < AUDIO_MAX, (chk, key, r, m) + tag
+
+    def rds_ok(key, gv, want, chk):
+        tmax, trms = RDS_TOL[key]
         scale = max(float(np.max(np.abs(want))), 1e-3)
         em, er = maxabs(gv, want) / scale, rms(gv, want) / scale
+        note((chk, key), em)
+        assert em < tmax and er < trms, (chk, key, em, er) + tag
+
+    def flip_ok(key, gv, want):
+        # an RDS I or Q row relative to the pair's peak (one complex signal: the loop's transient
+        # moves both by about the same amount, and Q is small next to I once locked)
+        pair = {"_i": "_q", "_q": "_i"}.get(key[-2:])
+        peak = float(np.max(np.abs(want)))
+        if pair is not None:
+            peak = max(peak, float(np.max(np.abs(rds_k[key[:-2] + pair]))))
+        e = maxabs(gv, want) / max(peak, 1e-3)
+        note(("flip", key), e)
+        assert e < FLIP_REL, ("flip window", key, e) + tag
+    # (a) upstream of the loops
+    for key in ("demod", "audio"):
+        audio_ok(key, seg(key, mono_k[key]), mono_k[key], "a")
+    for key, tol in (("bpf_recovery", 2e-6), ("bpf_extraction", 4e-6)):      # relative to the peak
+        want = mono_k[key]
+        m = maxabs(seg(key, want), want) / max(float(np.max(np.abs(want))), 1e-3)
+        note(("a", key), m)
+        assert m < tol, ("a", key, m) + tag
+    for key in ("extract", "pre_pll"):
+        rds_ok(key, seg(key, rds_k[key]), rds_k[key], "a")
+    # (b) the loops on the device's own inputs, (c) what follows them
+    for key, alt in (("nco", mono_k["alt"]), ("nco_i", rds_k["alt"]), ("nco_q", rds_k["alt"])):
+        m = maxabs(seg(key, alt[key]), alt[key])
+        note(("b", key), m)
+        assert m < NCO_REPLAY, ("b", key, m) + tag
+    for key in ("stereo", "left", "right"):
+        audio_ok(key, seg(key, mono_k["alt"][key]), mono_k["alt"][key], "c")
+    for key in ("lpf_i", "lpf_q", "resample_i", "resample_q", "rrc_i", "rrc_q"):
+        rds_ok(key, seg(key, rds_k["alt"][key]), rds_k["alt"][key], "c")
+    # (d) end to end
+    for key in ("stereo", "left", "right"):
+        want = mono_k[key]
+        flip_ok(key, seg(key, want), want) if key in trans else audio_ok(key, seg(key, want), want, "d")
+    for key in ("nco", "nco_i", "nco_q"):
+        want = (mono_k if key == "nco" else rds_k)[key]
         if key in trans:
-            assert em < FLIP_REL, (key, em) + tag
+            flip_ok(key, seg(key, want), want)
         else:
-            assert em < tmax and er < trms, (key, em, er) + tag
+            m = maxabs(seg(key, want), want)
+            note(("d", key), m)
+            assert m < NCO_REPLAY, ("d", key, m) + tag
+    for key in ("lpf_i", "lpf_q", "resample_i", "resample_q", "rrc_i", "rrc_q"):
+        want = rds_k[key]
+        flip_ok(key, seg(key, want), want) if key in trans else rds_ok(key, seg(key, want), want, "d")
+
+
+def _print_errs(errs):
+    print("span vs oracle, worst error per (check, output) -- a: upstream, b: NCO on the device's loop "
+          "inputs, c: downstream of that NCO, d: end to end, flip: sign-flip windows:",
+          {f"{c}:{k}": f"{v:.1e}" for (c, k), v in sorted(errs.items())})
 
 
 def test_span_c5_timed_shape_eight_streams(sdr, gpu_ctx, oracle):
@@ -247,8 +340,9 @@ def test_span_c5_timed_shape_eight_streams(sdr, gpu_ctx, oracle):
           materialises every intermediate, bit for bit, for every output both produce (the
           streams of a job table are independent; the NCO formed in the mixers is the NCO row);
       (b) streams 0 and 7 against the oracle (model/fmMonoBlock.py:80-173,
-          model/fmRDSblock.py:127-204 with the C restatement of fmPll) on the first two and
-          last two blocks of the second span, the intermediates from the 1-stream receiver;
+          model/fmRDSblock.py:127-204 with the C restatement of fmPll) on every block of the
+          second span, the intermediates from the 1-stream receiver, the oracle's loops also
+          run on the receiver's own loop inputs (_check_oracle_block);
       (c) the solver counters: 16 x 275 recurrences per span, no sequential tail; the locked
           span all in round 0, no chain stop."""
     from importlib import import_module
@@ -282,30 +376,34 @@ def test_span_c5_timed_shape_eight_streams(sdr, gpu_ctx, oracle):
     rx.close()
     # (a) every stream against a 1-stream receiver over the same two spans, every output kept
     one = sdr.Receiver(1, n, **kw)
-    full = {}
+    full, first = {}, {}
     for s in range(S):
         one.reset()
         for sp in range(spans):
             one.process_dev(d.ptr + s * row_bytes + sp * 2 * n, n)
+            if sp == 0 and s in (0, S - 1):          # the first span's loop inputs (the replayed loops' state)
+                first[s] = {src: one.output(src)[0].copy() for src in FLIP_DEPS}
         for name in lean:
             assert np.array_equal(one.output(name)[0], got[name][s]), (name, s)
         if s in (0, S - 1):
             full[s] = {name: one.output(name)[0] for name in NAMES}
     one.close()
     d.free()
-    # (b) streams 0 and 7 against the oracle on the second span's first two and last two blocks
+    # (b) streams 0 and 7 against the oracle on every block of the second span, the loops also on
+    # the receiver's own inputs (from the stream start: the loops' state)
+    M = B5 // 10
     for s in (0, S - 1):
         g = full[s]
-        iq = win(s)
-        mono = oracle.mono_stereo_blocks((iq.astype(np.float64) - 128.0) / 128.0, B5, rf_taps=151, audio_taps=151,
-                                         nblocks=spans * K, pll_fn=oracle.fm_pll_c)
-        rds = oracle.rds_blocks(iq, 2 * B5, taps=151, nblocks=spans * K, pll_fn=oracle.fm_pll_c)
-        # (the sign-flip windows over the second span, whose outputs the receiver holds)
-        trans = _transient_blocks(lambda src, k, n: g[src][(k - K) * n:(k - K + 1) * n],
-                                  {"bpf_recovery": mono, "pre_pll": rds}, range(K, spans * K))
-        for kk in (0, 1, K - 2, K - 1):
+        rows = lambda src: lambda k: (first[s] if k < K else g)[src][(k % K) * M:(k % K + 1) * M]   # noqa: E731
+        mono, rds = _oracle_blocks(oracle, win(s), spans * K, rows("bpf_recovery"), rows("pre_pll"), alt_from=K)
+        # (the sign-flip windows over both spans: the first span's inputs are held too)
+        trans = _transient_blocks(lambda src, k, n: rows(src)(k), {"bpf_recovery": mono, "pre_pll": rds},
+                                  range(spans * K))
+        errs = {}
+        for kk in range(K):
             k = K + kk
-            _check_oracle_block(g, lambda key: g[key], kk, mono[k], rds[k], trans[k], (s, k))
+            _check_oracle_block(lambda key: g[key], kk, mono[k], rds[k], trans[k], (s, k), errs)
+        _print_errs(errs)
         del mono, rds
 
 

@@ -1,5 +1,5 @@
 """Diagnostic: where the RDS NCO of the block receiver departs from the oracle (one u8 stream,
-3 blocks), with the PLL solver counters; run under SDR_PLL_SPLIT=0 / default for an A/B."""
+3 blocks), with the PLL solver counters (the r04 split A/B switch it was run under is removed)."""
 import os, sys
 import numpy as np
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
