@@ -473,6 +473,10 @@ static_assert(SPEC_NMAX == 16384 + 1, "LDS sizing");
 constexpr int SPEC_N256 = 10240;             // longest call the 256-thread solve takes (512 above; fixed, r04 A/B)
 constexpr int SPEC_LDS = 32 * 516;           // padded transposed bytes: 512 chunks of <= 32 steps (or 256 of <= 40)
 constexpr int SB = 8;                        // steps per batch of LDS reads in the step loops
+// The solve's matrix-power table (qtab_host): per chunk length L = SB, 2 SB, .., QT_NL SB
+// (SPEC_T = 256 takes up to SPEC_N256 steps: L <= 40), QT_N 2x2 matrices of Q = A^L --
+// Q^e for e = 0 .. 64, then Q^(64 w) for w = 0 .. 7 (the waves of a 512-thread solve)
+constexpr int QT_N = 65 + 8, QT_NL = 5;
 
 // ---- long calls: pseudo-block bookkeeping (device scratch P.work; LongBlk / LongHdr in
 // sdr_nco.h, which the receiver's mixers read too) ---------------------------------------
@@ -552,7 +556,6 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   __shared__ int8_t mrel[SPEC_T * MSTR];
   __shared__ double tb[NW * SB * TBS];
   __shared__ d2v wsum[NW];
-  __shared__ Mat2 qp[10];
   __shared__ double x1s[2];
   __shared__ float mg[NW + 1];                   // the waves' smallest wrap margins (+ the literal step's)
   __shared__ double wsh;                         // w for the end state (no register across the solve)
@@ -625,10 +628,10 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   double* cr = J.cbuf + (int64_t)s * J.c_stride + base;
   const PllCfg cfg = J.cfg;
 #ifdef SDR_PLL_SPEC_PROF    // phase timers (diagnostic builds only, tools/build_dbg.sh)
-  long long tp[8];
+  long long tp[16];
   int ntp = 0;
   tp[ntp++] = clock64();
-#define SPEC_TP() do { if (ntp < 8) tp[ntp++] = clock64(); } while (0)
+#define SPEC_TP() do { if (ntp < 16) tp[ntp++] = clock64(); } while (0)
 #else
 #define SPEC_TP() do {} while (0)
 #endif
@@ -670,6 +673,12 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   const int TE = (N + L - 1) / L;                // chunks in use; chunks 0 .. TE-2 are full
   const int k0 = 1 + tid * L;
   const int len = tid < TE ? min(L, (int)n - k0) : 0;   // steps of this thread's chunk
+  // the solve's matrix powers (Q = A^L: Q^e, e <= 64, and Q^(64 w)) into LDS; their loads go
+  // out with the staging's, so the solve never waits on memory (r06: a per-thread global load
+  // at the solve waited ~10 k cycles behind the other workgroups' staging traffic)
+  __shared__ d2v qt2[2 * QT_N];
+  d2v qv{0.0, 0.0};
+  if (tid < 2 * QT_N) qv = reinterpret_cast<const d2v*>(J.qtab)[(int64_t)(L / SB - 1) * 2 * QT_N + tid];
   // stage the sign codes, transposed -- step i of chunk j at i * CSTR + j -- so that the
   // threads' per-step reads of their own chunks are consecutive bytes; the global loads go
   // out SG at a time before the first is used.  (Slots of steps past N hold whatever was
@@ -706,6 +715,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       }
     }
   }
+  if (tid < 2 * QT_N) qt2[tid] = qv;
   __syncthreads();
   SPEC_TP();
   // r04b: a wave whose chunks are all full runs the step loops without a per-step "inside the
@@ -761,33 +771,43 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       if (wfull) corr(std::true_type{});
       else corr(std::false_type{});
     }
+    SPEC_TP();
     yb[tid] = d2v{(double)z.x, -(double)z.y};
     __syncthreads();
-    double sr = 0.0, si = 0.0;
-    for (int o = -2; o <= 2; ++o) {
+    // the 5-chunk sums around this chunk and around the one before it: each thread forms both
+    // angles, so their difference needs no second exchange (r06: 3 barriers instead of 5), and
+    // the unwrapped differences are summed in f32 (a guess: the check, not this, is exact)
+    double sr = 0.0, si = 0.0, qr = 0.0, qi = 0.0;
+    for (int o = -3; o <= 2; ++o) {
       const int j = tid + o;
-      if (j >= 0 && j < TE) { sr += yb[j].x; si += yb[j].y; }
+      if (j >= 0 && j < TE) {
+        const d2v v = yb[j];
+        if (o >= -2) { sr += v.x; si += v.y; }
+        if (o <= 1) { qr += v.x; qi += v.y; }
+      }
     }
-    const double ang = (double)atan2f((float)si, (float)sr);   // (a guess: f32 is plenty)
+    const float ang = atan2f((float)si, (float)sr), angp = atan2f((float)qi, (float)qr);
     if (pre > 0 && tid == 0) {                   // the pre-roll's seed: measured phase, span's integrator
-      x1s[0] = ang;
+      x1s[0] = (double)ang;
       x1s[1] = st_call[0] - kds;
     }
-    __syncthreads();
-    yb[tid].x = ang;
-    __syncthreads();
-    double d = 0.0;
+    float d = 0.f;
     if (tid >= 1 && tid < TE) {
-      d = ang - yb[tid - 1].x;
-      d -= k2Pi * rint(d * kInv2Pi);
+      d = ang - angp;
+      d -= 6.28318548f * rintf(d * 0.159154937f);
     }
     // inclusive prefix sum of the differences: within each wave by shuffles, then the waves'
     // totals
-    d = wave_prefix_sum(d, lane);
-    if (lane == 63) wsum[wv].x = d;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float u = __shfl_up(d, o, 64);
+      if (lane >= o) d += u;
+    }
+    if (lane == 63) wsum[wv].x = (double)d;
     __syncthreads();
-    for (int i = 0; i < wv; ++i) d += wsum[i].x;
-    yb[tid].x = d;                               // D_j
+    double D = (double)d;
+    for (int i = 0; i < wv; ++i) D += wsum[i].x;
+    yb[tid].x = D;                               // D_j
     __syncthreads();
   }
   SPEC_TP();
@@ -860,6 +880,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
         }
       }
     }
+    SPEC_TP();
     __syncthreads();                             // yb (D_j) read before tb reuses its space
     xs_p = p;                                    // the guess's chunk start (after the warm-up)
     xs_v = V;
@@ -893,84 +914,66 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     };
     if (wfull) guess(std::true_type{});
     else guess(std::false_type{});
+    SPEC_TP();
     xe_p = p;                                    // ... and its end
     xe_v = V;
   }
   if (__syncthreads_or(bad)) return false;       // a 0 / NaN input (the general form's case)
   SPEC_TP();
-  // Q = A^L and its squarings Q^(2^i), i < 10 (thread 0, into LDS: the scans read them as
-  // broadcasts instead of holding them in registers)
-  const double a00 = 1.0 - kC * kInv2Pi, a10 = -kA * kInv2Pi;
-  if (tid == 0) {
-    double P00 = 1.0, P01 = 0.0, P10 = 0.0, P11 = 1.0;
-    for (int i = 0; i < L; ++i) {                // P = A P
-      const double n00 = a00 * P00 + P10, n01 = a00 * P01 + P11;
-      const double n10 = a10 * P00 + P10, n11 = a10 * P01 + P11;
-      P00 = n00; P01 = n01; P10 = n10; P11 = n11;
-    }
-    Mat2 x{P00, P01, P10, P11};
-    for (int i = 0; i < 10; ++i, x = mmul(x, x)) qp[i] = x;
-  }
-  __syncthreads();
-  auto qpow = [&](int e) {                       // Q^e, e < 1024
-    Mat2 r{1.0, 0.0, 0.0, 1.0};
-    for (int i = 0; e > 0; ++i, e >>= 1)
-      if (e & 1) r = mmul(r, qp[i]);
-    return r;
-  };
+  SPEC_TP();                                     // (the phase timers' slot of the r05 Q-power phase)
+  // Q = A^L's powers from the job's table (qtab_host, built once per loop on the host, staged in
+  // LDS with the sign codes): Q^(2^i) for the scan's offsets, Q^(lane+1) and Q^tid = Q^(64 w)
+  // Q^lane for the chunk starts -- r06: instead of thread 0 forming them (A^L step by step, then
+  // the squarings, behind a barrier) and every thread multiplying up to 9 of them (phase timers:
+  // ~10 k of a pseudo-block's ~66 k cycles)
+  const Mat2* QT = reinterpret_cast<const Mat2*>(qt2);
+  auto qp = [&](int i) { return QT[1 << i]; };   // Q^(2^i), i <= 6
   double* tw = tb + wv * SB * TBS;               // this wave's transpose tile
   for (int round = 0; round < SPEC_IT; ++round) {
     // 2. solve: the chunk's response from zero state to the current integers, from the last
     // pass over it (the guess in round 0, the previous check after): z_j = x_end - Q x_start
     double zp, zv;
     {
-      const Mat2 Q = qp[0];
+      const Mat2 Q = qp(0);
       zp = xe_p - (Q.a * xs_p + Q.b * xs_v);
       zv = xe_v - (Q.c * xs_p + Q.d * xs_v);
     }
     // chunk starts y_j = Q^j x_1 + Y_{j-1}, Y_j = sum_{i<=j} Q^(j-i) z_i (Q = A^L): an inclusive
     // scan of the z_i within each wave by shuffles (offset o combines with Q^o), then across the
-    // waves through their totals (Y at a wave's end = its total + Q^64 Y at the previous end)
+    // waves through their totals (Y at a wave's end = its total + Q^64 Y at the previous end).
+    // Y_{j-1} of a wave's lane 0 is that carry itself (r06: no second exchange of the totals)
+    const Mat2 Ql = QT[lane + 1], Qj = mmul(QT[65 + wv], QT[lane]);   // Q^(lane+1), Q^tid
     double yp = tid < TE ? zp : 0.0, yv = tid < TE ? zv : 0.0;
+    double cp = 0.0, cv = 0.0;                   // Y at the end of the previous wave
     {
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const int o = 1 << i;
         const double up = __shfl_up(yp, o, 64), uv = __shfl_up(yv, o, 64);
         if (lane >= o) {
-          const Mat2 Qo = qp[i];
+          const Mat2 Qo = qp(i);
           yp = yp + (Qo.a * up + Qo.b * uv);
           yv = yv + (Qo.c * up + Qo.d * uv);
         }
       }
       if (lane == 63) wsum[wv] = d2v{yp, yv};
       __syncthreads();
-      // Y at the end of the previous wave, then Q^(lane+1) of it
-      double cp = 0.0, cv = 0.0;
+      SPEC_TP();
+      const Mat2 Q64 = qp(6);
       for (int i = 0; i < wv; ++i) {
-        const Mat2 Q64 = qp[6];
         const double np = wsum[i].x + (Q64.a * cp + Q64.b * cv), nv = wsum[i].y + (Q64.c * cp + Q64.d * cv);
         cp = np; cv = nv;
       }
-      const Mat2 Ql = qpow(lane + 1);
       yp = yp + (Ql.a * cp + Ql.b * cv);
       yv = yv + (Ql.c * cp + Ql.d * cv);
-      __syncthreads();                             // wsum read before it is rewritten
+      SPEC_TP();
     }
-    // Y_{j-1}: the previous lane's (lane 0: the previous wave's last, via LDS)
+    // Y_{j-1}: the previous lane's (lane 0: the carry); the check's barrier orders these wsum
+    // reads before the next round's writes
     double vp = __shfl_up(yp, 1, 64), vv = __shfl_up(yv, 1, 64);
-    if (lane == 63) wsum[wv] = d2v{yp, yv};
-    __syncthreads();
-    if (lane == 0) {
-      if (wv > 0) { vp = wsum[wv - 1].x; vv = wsum[wv - 1].y; }
-      else { vp = 0.0; vv = 0.0; }
-    }
-    {
-      const Mat2 Qj = qpow(tid);                   // Q^j x_1
-      vp = vp + (Qj.a * p1 + Qj.b * v1);
-      vv = vv + (Qj.c * p1 + Qj.d * v1);
-    }
-    __syncthreads();                             // wsum read before the next round writes it
+    if (lane == 0) { vp = cp; vv = cv; }
+    vp = vp + (Qj.a * p1 + Qj.b * v1);           // + Q^j x_1
+    vv = vv + (Qj.c * p1 + Qj.d * v1);
     SPEC_TP();
     // 3. check: the true step from y_j.  The phases go out as the theta row on every round (a
     // later round or the sequential kernel overwrites a failed one): each batch of SB steps
@@ -1041,6 +1044,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     };
     if (wfast) check(std::true_type{});
     else check(std::false_type{});
+    SPEC_TP();
     float mth = fminf(__uint_as_float(mlo), 1.f - __uint_as_float(mhi));
     xe_p = p;
     xe_v = V;
@@ -1053,8 +1057,10 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     SPEC_TP();
 #ifdef SDR_PLL_SPEC_PROF
     if (tid == 0 && nmiss == 0 && (bid == 0 || (bid % 479) == 3))
-      printf("spec_prof blk %d L %d: stage %lld corr %lld guess %lld solve %lld check %lld (%d marks)\n", bid, L,
-             tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], ntp);
+      printf("spec_prof blk %d L %d: stage %lld corrloop %lld corrscan %lld warm %lld guessloop %lld guesssync %lld "
+             "qpow %lld wscan %lld xscan %lld ystart %lld checkloop %lld checksync %lld (%d marks)\n", bid, L,
+             tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], tp[6] - tp[5], tp[7] - tp[6],
+             tp[8] - tp[7], tp[9] - tp[8], tp[10] - tp[9], tp[11] - tp[10], tp[12] - tp[11], ntp);
 #endif
     if (nmiss == 0) {
       if constexpr (LONG) {
@@ -1882,6 +1888,73 @@ int64_t sdr_pll_work_bytes(int njobs, int nstreams, int64_t n) {
   return R * (int64_t)sizeof(LongHdr) + R * nb * (int64_t)sizeof(LongBlk);
 }
 
+// The solve's matrix powers for loop c (QT_NL x QT_N matrices, row-major 2x2 doubles), formed
+// with the arithmetic the device used to (r05: thread 0 computed them in every workgroup):
+// Q = A^L as P <- A P, L times; Q^(2^i) by squaring; Q^e as the product of the Q^(2^i) of e's
+// bits, lowest first -- separate roundings (no contraction).
+namespace {
+struct HM2 { double a, b, c, d; };
+HM2 hmul(const HM2& x, const HM2& y) {
+#pragma clang fp contract(off)
+  return {x.a * y.a + x.b * y.c, x.a * y.b + x.b * y.d, x.c * y.a + x.d * y.c, x.c * y.b + x.d * y.d};
+}
+void qtab_host(const PllCfg& cfg, std::vector<double>* out) {
+#pragma clang fp contract(off)
+  const double kA = k2Pi * cfg.ki, kC = k2Pi * (cfg.kp + cfg.ki);
+  const double a00 = 1.0 - kC * kInv2Pi, a10 = -kA * kInv2Pi;
+  out->assign((size_t)QT_NL * QT_N * 4, 0.0);
+  for (int li = 0; li < QT_NL; ++li) {
+    const int L = (li + 1) * SB;
+    double P00 = 1.0, P01 = 0.0, P10 = 0.0, P11 = 1.0;
+    for (int i = 0; i < L; ++i) {
+      const double n00 = a00 * P00 + P10, n01 = a00 * P01 + P11;
+      const double n10 = a10 * P00 + P10, n11 = a10 * P01 + P11;
+      P00 = n00; P01 = n01; P10 = n10; P11 = n11;
+    }
+    HM2 q[10];
+    HM2 x{P00, P01, P10, P11};
+    for (int i = 0; i < 10; ++i, x = hmul(x, x)) q[i] = x;
+    auto pw = [&](int e) {                          // Q^e from the Q^(2^i) of e's bits, lowest first
+      HM2 r{1.0, 0.0, 0.0, 1.0};
+      for (int i = 0; e > 0; ++i, e >>= 1)
+        if (e & 1) r = hmul(r, q[i]);
+      return r;
+    };
+    HM2* t = reinterpret_cast<HM2*>(out->data()) + (size_t)li * QT_N;
+    for (int e = 0; e <= 64; ++e) t[e] = pw(e);
+    for (int w = 0; w < 8; ++w) t[65 + w] = pw(64 * w);
+  }
+}
+// device copies, per (device, kp, ki), for the life of the process (QT_NL x QT_N x 32 B = 12 KB each)
+struct QTab { int dev; double kp, ki; double* d; };
+hipError_t qtab_get(const PllCfg& cfg, const double** out) {
+  static std::mutex mu;
+  static std::vector<QTab> cache;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(mu);
+  for (const QTab& t : cache)
+    if (t.dev == dev && t.kp == cfg.kp && t.ki == cfg.ki) { *out = t.d; return hipSuccess; }
+  std::vector<double> h;
+  qtab_host(cfg, &h);
+  QTab t{dev, cfg.kp, cfg.ki, nullptr};
+  e = hipMalloc(&t.d, sizeof(double) * h.size());
+  if (e == hipSuccess) e = hipMemcpy(t.d, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return e;
+  cache.push_back(t);
+  *out = t.d;
+  return hipSuccess;
+}
+hipError_t qtab_fill(PllJobs& L) {
+  for (int q = 0; q < L.njobs; ++q) {
+    const hipError_t e = qtab_get(L.j[q].cfg, &L.j[q].qtab);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+}  // namespace
+
 hipError_t sdr_launch_pll_prep(const PllJobs& P, hipStream_t st) {
   bool vec;
   const hipError_t e = pll_check(P, &vec);
@@ -1904,6 +1977,7 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     // long call: every pseudo-block solved (from warm-up guesses), then the chain with its repairs
     L.qform = 0;
     e = long_setup(L);
+    if (e == hipSuccess) e = qtab_fill(L);
     if (e != hipSuccess) return e;
     const int R = L.njobs * L.nstreams;
     hipLaunchKernelGGL((pll_spec_kernel<512, true>), dim3((unsigned)(R * L.lg.nb)), dim3(512), 0, st, L);
@@ -1916,6 +1990,8 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     L.lpw = 0;
     L.qform = 0;
     L.nco_fused = P.nco_rows ? 1 : 0;
+    e = qtab_fill(L);
+    if (e != hipSuccess) return e;
     const dim3 g((unsigned)(L.njobs * L.nstreams));
     if (L.n > SPEC_N256) hipLaunchKernelGGL((pll_spec_kernel<512, false>), g, dim3(512), 0, st, L);
     else hipLaunchKernelGGL((pll_spec_kernel<256, false>), g, dim3(256), 0, st, L);

@@ -7,7 +7,7 @@
 #
 # steps:
 #   tests        the full -m gpu suite (+ smoke)                      -> pytest_gpu.txt, smoke.txt
-#   tests:<expr> the -m gpu tests matching -k <expr>                   -> pytest_<expr>.txt
+#   tests:<expr> the -m gpu tests matching -k <expr> (commas for spaces) -> pytest_<expr>.txt
 #   bench        python bench.py (the driver's default line)           -> bench_default.json
 #   bench:<name>:<args...>   bench.py with args (commas for spaces)     -> bench_<name>.json
 #   prof:<name>:<args...>    rocprofv3 --kernel-trace --stats of it     -> prof_<name>/, prof_<name>.json
@@ -29,7 +29,7 @@ for step in "$@"; do
       timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > "$O/pytest_gpu.txt" 2>&1
       timeout -k 10 200 python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' > "$O/smoke.txt" 2>&1 ;;
     tests:*)
-      k=${step#tests:}
+      k=$(sp "${step#tests:}")
       timeout -k 10 500 python -u -m pytest tests -m gpu -v -s --timeout 200 --timeout-method thread -k "$k" \
         > "$O/pytest_$(echo "$k" | tr -c 'a-zA-Z0-9_\n' '_').txt" 2>&1 ;;
     bench)
