@@ -829,9 +829,11 @@ def rx_measure(ctx, workload, args, rank, ws, steps, warmup, cpu=False):
     return result
 
 C5_B = 153_600                 # complex samples per reference block (src/fm_radio.cpp:23)
-# what the receivers materialise on their device-resident path: every output but the NCO rows
-# and the RDS LPF rows, intermediates the chain does not need (sdr_rx_set_keep; the same values)
-LEAN_KEEP = ("demod", "audio", "bpf_recovery", "bpf_extraction", "stereo", "left", "right", "extract", "pre_pll",
+# what the receivers materialise on their device-resident path: every output but the NCO rows,
+# the RDS LPF rows and (spans) the PLLs' f32 input rows -- intermediates the chain does not need
+# (sdr_rx_set_keep): the mixers form the NCO from the PLL phases, the RDS LPF runs inside the
+# composite resampler, the PLLs read their inputs as sign codes (the same values either way)
+LEAN_KEEP = ("demod", "audio", "bpf_extraction", "stereo", "left", "right", "extract",
              "resample_i", "resample_q", "rrc_i", "rrc_q")
 VALU_PEAK_TFLOPS = 157.3       # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 # f64 VALU issue: a wave64 f64 instruction holds its SIMD 4 cycles (half the f32 rate: 78.6

@@ -624,6 +624,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   }
   const PllJob& J = P.j[q];
   const float* in = J.in + (int64_t)s * J.in_stride + base;
+  const int8_t* in8 = J.in8 != nullptr ? J.in8 + (int64_t)s * J.in8_stride + base : nullptr;
   double* th = J.theta + (int64_t)s * J.th_stride + base;
   double* cr = J.cbuf + (int64_t)s * J.c_stride + base;
   const PllCfg cfg = J.cfg;
@@ -658,7 +659,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // sample 0: the literal general step (thread 0), as the loop kernels' general() (a
   // pre-roll's seed is set from the measured phase instead, below)
   if (tid == 0 && pre == 0) {
-    const double xv = (double)in[0];
+    const double xv = (double)(in8 != nullptr ? pll_decode(in8[0]) : in[0]);
     const double e = atan2(xv * (-st[3]), xv * st[2]);
     mg[NW] = (float)((kPi - fabs(e)) * kInv2Pi);  // the literal step's distance from the wrap
     const double integ = st[0] + cfg.ki * e;
@@ -692,9 +693,19 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     // (chunk SPEC_T, never in use)
     constexpr int SG = SPEC_T == 512 ? 32 : 40;
     static_assert(SG * SPEC_T >= (SPEC_T == 512 ? SPEC_NMAX : SPEC_N256) - 1, "one pass of SG loads covers a call");
+    // (a span's sign-code row: a quarter of the bytes, r06; its codes other than +-1 -- zeros,
+    // NaN -- are the solve's general-form case, 0, as the float row's)
     float xv[SG];
+    if (in8 != nullptr) {
+      int8_t cv[SG];
 #pragma unroll
-    for (int u = 0; u < SG; ++u) xv[u] = in[min(tid + u * SPEC_T, N - 1) + 1];
+      for (int u = 0; u < SG; ++u) cv[u] = in8[min(tid + u * SPEC_T, N - 1) + 1];
+#pragma unroll
+      for (int u = 0; u < SG; ++u) xv[u] = (cv[u] == 1 || cv[u] == -1) ? (float)cv[u] : 0.f;
+    } else {
+#pragma unroll
+      for (int u = 0; u < SG; ++u) xv[u] = in[min(tid + u * SPEC_T, N - 1) + 1];
+    }
     auto cod = [](float x) { return (int8_t)(x > 0.f ? 1 : (x < 0.f ? -1 : 0)); };
     if (SPEC_T % L == 0) {
       // element kk = tid + u SPEC_T: i = tid mod L for every u, j = tid / L + u SPEC_T / L
@@ -1141,7 +1152,8 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   return false;
 }
 
-__device__ void seq_run(const PllCfg& cfg, const float* in, double* th, int64_t n, const double* st, double* so);
+__device__ void seq_run(const PllCfg& cfg, const float* in, const int8_t* in8, double* th, int64_t n, const double* st,
+                        double* so);
 
 // A per-block call's recurrence the solve does not complete (a 0 / NaN input, a loop not yet
 // locked) runs sequentially in the same workgroup (one thread, seq_run's general form) --
@@ -1159,7 +1171,8 @@ __device__ void spec_fallback(const PllJobs& P, const int bid) {
   if (J.nco_q)
     J.nco_q[(int64_t)s * J.out_stride] = (float)((off > 0.0) ? sin((w * off + st[1]) * cfg.scale + cfg.adj) : 0.0);
   double so[6];
-  seq_run(cfg, J.in + (int64_t)s * J.in_stride, th, P.n, st, so);
+  seq_run(cfg, J.in + (int64_t)s * J.in_stride, J.in8 != nullptr ? J.in8 + (int64_t)s * J.in8_stride : nullptr, th, P.n,
+          st, so);
   th[P.n] = off;                                   // the NCO kernel's trigOffset
   for (int i = 0; i < 6; ++i) st[i] = so[i];
   stat_add(P.stats, SDR_PLL_ST_RECURRENCES, 1);
@@ -1269,8 +1282,10 @@ constexpr int LONG_FIXES = 24;         // repairs (re-solves at the chain's posi
 
 // The reference's recurrence run sequentially from state st over n steps (the general form:
 // literal first step from the state's (fI, fQ); 0 / NaN inputs by atan2 on the products; the
-// rest by the constants pll_c).  Phases into th[0..n), the end state into so.
-__device__ void seq_run(const PllCfg& cfg, const float* in, double* th, int64_t n, const double* st, double* so) {
+// rest by the constants pll_c).  Inputs from `in`, or decoded from the sign codes in8 when
+// given.  Phases into th[0..n), the end state into so.
+__device__ void seq_run(const PllCfg& cfg, const float* in, const int8_t* in8, double* th, int64_t n, const double* st,
+                        double* so) {
 #pragma clang fp contract(off)
   const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
   double integ = st[0], phase = st[1];
@@ -1280,7 +1295,7 @@ __device__ void seq_run(const PllCfg& cfg, const float* in, double* th, int64_t 
   float xa[G], xn[G];
   auto ld = [&](float (&v)[G], int64_t k0) {
 #pragma unroll
-    for (int i = 0; i < G; ++i) v[i] = k0 + i < n ? in[k0 + i] : 0.f;
+    for (int i = 0; i < G; ++i) v[i] = k0 + i < n ? (in8 != nullptr ? pll_decode(in8[k0 + i]) : in[k0 + i]) : 0.f;
   };
   ld(xa, 0);
   for (int64_t k0 = 0; k0 < n; k0 += G) {
@@ -1594,8 +1609,9 @@ __device__ void long_tail(const PllJobs& P, const int r, const int pos) {
     sincos_red<true>(reduce_2pi(arg), &s0[3], &s0[2]);
   }
   double so[6];
-  seq_run(cfg, J.in + (int64_t)s * J.in_stride + base, J.theta + (int64_t)s * J.th_stride + base, P.n - base, s0,
-          so);
+  seq_run(cfg, J.in + (int64_t)s * J.in_stride + base,
+          J.in8 != nullptr ? J.in8 + (int64_t)s * J.in8_stride + base : nullptr, J.theta + (int64_t)s * J.th_stride + base,
+          P.n - base, s0, so);
   for (int i = 0; i < 5; ++i) st[i] = so[i];
   st[5] = off0 + (double)P.n;
   H->pos = nb;
@@ -1628,8 +1644,9 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_fix_kernel(PllJobs P) {
       const int q = r / P.nstreams, s = r - q * P.nstreams;
       const PllJob& J = P.j[q];
       const int64_t base = (int64_t)pos * P.lg.pb;
-      seq_run(J.cfg, J.in + (int64_t)s * J.in_stride + base, J.theta + (int64_t)s * J.th_stride + base, long_len(P, pos),
-              B->x, B->e);
+      seq_run(J.cfg, J.in + (int64_t)s * J.in_stride + base,
+              J.in8 != nullptr ? J.in8 + (int64_t)s * J.in8_stride + base : nullptr,
+              J.theta + (int64_t)s * J.th_stride + base, long_len(P, pos), B->x, B->e);
       B->u[0] = B->x[0];
       B->u[1] = B->x[1];
       B->d[0] = B->d[1] = 0.0;
@@ -1960,6 +1977,8 @@ hipError_t sdr_launch_pll_prep(const PllJobs& P, hipStream_t st) {
   const hipError_t e = pll_check(P, &vec);
   if (e != hipSuccess) return e;
   if (pll_long(P) || spec_only(P)) return hipSuccess;   // the solve computes its constants where it uses them (pll_c)
+  for (int q = 0; q < P.njobs; ++q)
+    if (P.j[q].in8 != nullptr) return hipErrorInvalidValue;
   PllJobs L = P;
   L.qform = !pll_long(P) && vec && pll_lpw(P) == 1;
   if (P.n > 0)
@@ -1997,6 +2016,8 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     else hipLaunchKernelGGL((pll_spec_kernel<256, false>), g, dim3(256), 0, st, L);
     return hipGetLastError();
   }
+  for (int q = 0; q < P.njobs; ++q)                  // (the sequential kernels read float rows only)
+    if (P.j[q].in8 != nullptr) return hipErrorInvalidValue;
   L.lpw = pll_lpw(P);
   L.qform = vec && L.lpw == 1;
   const dim3 grid((unsigned)(L.njobs * ((L.nstreams + L.lpw - 1) / L.lpw)));

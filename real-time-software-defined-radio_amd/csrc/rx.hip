@@ -76,6 +76,8 @@ struct StageJob {
   int mma;               // the tiles run on the matrix cores (rx_mma_kernel); this launch keeps its zf
   int wgs;               // rx_mma_kernel: the job's workgroups (each runs every wgs-th tile)
   NcoSrc nco;            // PRE_NCO: where the NCO comes from
+  int8_t* y8;            // nullable: the outputs' sign codes too (sdr_nco.h pll_code: a PLL's input),
+  int64_t y8_stride;     //   y8_stride bytes apart; y may then be null (matrix-core jobs only)
 };
 
 // The front end's carried state, finished by the first stage launch after the FE kernel:
@@ -644,9 +646,13 @@ __device__ __forceinline__ void mma_run(const StageJob* Jf, int S, int64_t gw, i
     h8v fh[2], fl[2];
     f4v acc_h[F], acc_c[F];
     const bool head = m0 < T - 1;                    // the block's first T - 1 outputs: + lfilter zi
-    __amdgpu_buffer_rsrc_t ry[F];
+    __amdgpu_buffer_rsrc_t ry[F], r8[F];
 #pragma unroll
-    for (int f = 0; f < F; ++f) ry[f] = mm_rsrc(Jf[f].y + (int64_t)s * Jf[f].y_stride + m0, (J.n - m0) * 4);
+    for (int f = 0; f < F; ++f) {
+      // (a null row: an empty range -- its stores are dropped)
+      ry[f] = mm_rsrc(Jf[f].y + (Jf[f].y ? (int64_t)s * Jf[f].y_stride + m0 : 0), Jf[f].y ? (J.n - m0) * 4 : 0);
+      r8[f] = mm_rsrc(Jf[f].y8 + (Jf[f].y8 ? (int64_t)s * Jf[f].y8_stride + m0 : 0), Jf[f].y8 ? J.n - m0 : 0);
+    }
     frag(0, &fh[0], &fl[0]);
     static_for<0, NSTEP>([&](auto Q) {
       constexpr int q = Q, st = q % KS, c = q / KS;
@@ -678,6 +684,12 @@ __device__ __forceinline__ void mma_run(const StageJob* Jf, int S, int64_t gw, i
             if (n0 + 3 < T - 1) o.w += (float)zi[n0 + 3];
           }
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, o), ry[f], 4 * ol, 0, 0);
+          if (Jj.y8 != nullptr) {                    // uniform: the four outputs' sign codes, one dword
+            using sdrnco::pll_code;
+            const uint32_t cw = (uint32_t)(uint8_t)pll_code(o.x) | (uint32_t)(uint8_t)pll_code(o.y) << 8 |
+                                (uint32_t)(uint8_t)pll_code(o.z) << 16 | (uint32_t)(uint8_t)pll_code(o.w) << 24;
+            __builtin_amdgcn_raw_buffer_store_b32(cw, r8[f], ol, 0, 0);
+          }
           if (Jj.yh != nullptr) {                    // host rows (per-call runs): plain stores
             float* hb = Jj.yh + (int64_t)s * Jj.yh_stride;
             const int64_t n0 = m0 + ol;
@@ -1182,7 +1194,8 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
   auto al16 = [](const void* p, int64_t stride) { return p != nullptr && ((uintptr_t)p % 16) == 0 && stride % 4 == 0; };
   auto mmable = [&](const StageJob& j, int key) {
     return j.kind == JK_FIR && j.D == 1 && j.T == key && (j.pre == PRE_NONE || j.pre == PRE_SQUARE) &&
-           al16(j.x, j.x_stride) && al16(j.y, j.y_stride) && j.n >= (int64_t)MM_MIN_WIN * MM_WT &&
+           al16(j.x, j.x_stride) && (al16(j.y, j.y_stride) || (j.y == nullptr && j.y8 != nullptr)) &&
+           j.n >= (int64_t)MM_MIN_WIN * MM_WT &&
            j.n % 4 == 0 && j.n < (int64_t)1 << 28;      // (buffer ranges: 32-bit byte offsets)
   };
   for (StageJob& j : jobs) j.mma = 0;
@@ -1277,6 +1290,8 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
         jobs[m].zf = nullptr;                        // (written by that launch)
       }
     }
+  for (const StageJob& j : jobs)                     // sign-code outputs: the matrix-core tiles only
+    if (!j.mma && (j.y8 != nullptr || j.y == nullptr)) return hipErrorInvalidValue;
   for (int key : {151, 101, 0}) {
     StageJobs P{};
     P.nstreams = S;
@@ -1857,6 +1872,8 @@ struct sdr_rx {
   int64_t ths = 0;
   double* pllc = nullptr;              // PLL per-sample constants: 2 x S rows of cst per row set
   int64_t cst = 0;
+  int8_t* pcode = nullptr;             // spans: the PLLs' inputs as sign codes (sdr_nco.h pll_code): 2 x S rows
+  int64_t pcs = 0;                     //   of pcs bytes per row set
   char* pllw = nullptr;                // long blocks (M > SDR_PLL_BLOCK_MAX): the PLL's pseudo-block
   int64_t pllw_bytes = 0;              //   records, one region per row set
   void* pin_in = nullptr;              // pinned host staging (sdr_rx_run)
@@ -1997,7 +2014,9 @@ int rx_finalize(sdr_rx* r) {
   const int nsets = r->pipe ? r->nq : 1;
   const int64_t doubles = 2 * zl + 3 * S2 + 2 * 6 * S2 + nsets * (2 * S * r->ths + 2 * S * r->cst);
   r->pllw_bytes = round_up(sdr_pll_work_bytes(2, r->S, M), 256);
-  const size_t bytes = (size_t)floats * 4 + 64 + (size_t)doubles * 8 + 256 + (size_t)(nsets * r->pllw_bytes);
+  r->pcs = round_up(M + 16, 256);
+  const size_t code_bytes = (r->flags & (SDR_RX_STEREO | SDR_RX_RDS)) ? (size_t)(nsets * 2 * S * r->pcs) : 0;
+  const size_t bytes = (size_t)floats * 4 + 64 + (size_t)doubles * 8 + 256 + (size_t)(nsets * r->pllw_bytes) + code_bytes;
   TRY(set_dev(r->c));
   hipError_t e = hipMalloc(&r->mem, bytes);
   if (e != hipSuccess) return fail(SDR_ENOMEM, "sdr_rx: hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
@@ -2017,6 +2036,7 @@ int rx_finalize(sdr_rx* r) {
   r->theta = r->pll_state[1] + 6 * S2;
   r->pllc = r->theta + nsets * 2 * S * r->ths;
   r->pllw = reinterpret_cast<char*>(round_up((int64_t)(uintptr_t)(r->pllc + nsets * 2 * S * r->cst), 256));
+  r->pcode = code_bytes ? reinterpret_cast<int8_t*>(r->pllw + nsets * r->pllw_bytes) : nullptr;
   if ((r->flags & SDR_RX_RDS) && r->rds_up == CR_U && r->rds_down == CR_D) {
     std::vector<float> ct;
     cres_taps(r->taps[SDR_RX_F_RDS_LPF], r->taps[SDR_RX_F_RDS_ANTI], &ct);
@@ -2231,20 +2251,39 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   const bool au = r->flags & (SDR_RX_AUDIO | SDR_RX_STEREO), stx = r->flags & SDR_RX_STEREO,
              rd = r->flags & SDR_RX_RDS;
   const int64_t as = au ? r->out_stride[SDR_RX_O_AUDIO] : 0;
+  // What this block materialises beyond what the chain needs (sdr_rx_set_keep / the outputs a
+  // submit asks for)
+  auto kept = [&](int o) { return (r->keep_now >> o) & 1ull; };
+  // Spans (the matrix-core rows): the PLLs take their inputs as sign codes (sdr_nco.h pll_code,
+  // r06) -- all the recurrence reads of them -- stored by the pilot BPF's and the RDS x^2 + BPF's
+  // tiles beside (or, when those rows are not kept, instead of) their f32 rows
+  auto mm_taps = [&](int f) { const size_t t = r->taps[f].size(); return t == 101 || t == 151; };
+  const bool codes = (stx || rd) && r->pcode != nullptr && M >= (int64_t)MM_MIN_WIN * MM_WT && M % 4 == 0 &&
+                     M < ((int64_t)1 << 28) && (!stx || mm_taps(SDR_RX_F_PILOT)) && (!rd || mm_taps(SDR_RX_F_RDS_SQUARE));
+  int8_t* c8 = codes ? r->pcode + (int64_t)q * 2 * S * r->pcs : nullptr;   // [PLL k][stream] rows, pcs bytes apart
+  auto coded = [&](StageJob j, int k, int o) {
+    if (codes) {
+      j.y8 = c8 + (int64_t)k * S * r->pcs;
+      j.y8_stride = r->pcs;
+      if (!kept(o)) j.y = nullptr;
+    }
+    return j;
+  };
   // stage A: every filter of the demodulated signal (model/fmMonoBlock.py:101-105, :117,
   // :151; model/fmRDSblock.py:156)
   std::vector<StageJob> A;
   if (au) A.push_back(fir(SDR_RX_F_AUDIO, Z_AUDIO, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_AUDIO], as, r->audio_decim));
   if (stx) {
-    A.push_back(fir(SDR_RX_F_PILOT, Z_PILOT, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_BPF_RECOVERY], ms, 1));
+    A.push_back(coded(fir(SDR_RX_F_PILOT, Z_PILOT, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_BPF_RECOVERY], ms, 1), 0,
+                      SDR_RX_O_BPF_RECOVERY));
     A.push_back(fir(SDR_RX_F_STEREO_BPF, Z_BAND, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_BPF_EXTRACTION], ms, 1));
   }
   if (rd) A.push_back(fir(SDR_RX_F_RDS_EXTRACT, Z_EXTRACT, o[SDR_RX_O_DEMOD], M, ms, o[SDR_RX_O_RDS_EXTRACT], ms, 1));
   HIP_TRY(launch_stage(A, S, fs, &fst));
   HIP_TRY(mark(1 + SDR_RX_ST_A, fs));
   // stage B: RDS squaring non-linearity + BPF (model/fmRDSblock.py:161-164)
-  if (rd) HIP_TRY(launch_stage({fir(SDR_RX_F_RDS_SQUARE, Z_SQUARE, o[SDR_RX_O_RDS_EXTRACT], M, ms,
-                                    o[SDR_RX_O_RDS_PRE_PLL], ms, 1, PRE_SQUARE)}, S, fs));
+  if (rd) HIP_TRY(launch_stage({coded(fir(SDR_RX_F_RDS_SQUARE, Z_SQUARE, o[SDR_RX_O_RDS_EXTRACT], M, ms,
+                                          o[SDR_RX_O_RDS_PRE_PLL], ms, 1, PRE_SQUARE), 1, SDR_RX_O_RDS_PRE_PLL)}, S, fs));
   HIP_TRY(mark(1 + SDR_RX_ST_B, fs));
   // PLLs (model/fmMonoBlock.py:119, model/fmRDSblock.py:167): one lane per recurrence.
   // Pipelined, the three launches go to three streams: the per-sample constants with the
@@ -2254,11 +2293,9 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   // and constant rows alternate with the row set; set q is free once block k-2's back half
   // (which waited for its recurrence) is done.
   const bool plls = stx || rd;
-  // What this block materialises beyond what the chain needs (sdr_rx_set_keep / the outputs a
-  // submit asks for): the NCO rows, and the RDS LPF rows.  Without them the stage-C mixers
+  // Beyond the chain: the NCO rows, and the RDS LPF rows.  Without them the stage-C mixers
   // form the NCO from the PLL phase rows where they stage their inputs (PRE_NCO, sdr_nco.h) and
   // the RDS LPF + resampler is the composite filter (rx_cres_kernel), which runs either way.
-  auto kept = [&](int o) { return (r->keep_now >> o) & 1ull; };
   const bool cres = rd && r->ctaps != nullptr;
   const int tsl = stx ? (int)r->taps[SDR_RX_F_STEREO_LPF].size() : 151;
   const bool tiles_ok = (tsl == 101 || tsl == 151) && (r->audio_decim == 1 || r->audio_decim == 5);   // PRE_NCO tiles
@@ -2292,6 +2329,10 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       TRY(get_resp(c, r->pll[k], M, &resp));
       const int jq = P.njobs;
       P.j[P.njobs++] = PllJob{in, ms, r->pll_state[k], thk, r->ths, ni, nq, ms, r->pll[k], pck, r->cst, off, 1, resp};
+      if (codes) {
+        P.j[jq].in8 = c8 + (int64_t)k * S * r->pcs;
+        P.j[jq].in8_stride = r->pcs;
+      }
       NcoSrc& N = nsrc[k];
       N.theta = M >= 2 ? thk : nullptr;   // (M < 2: the sequential kernels' Q-form rows; mix from the NCO rows)
       N.th_stride = r->ths;
@@ -2430,7 +2471,8 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
   for (int oo = 0; oo < SDR_RX_NOUTPUTS; ++oo) {
     const bool nco_o = oo == SDR_RX_O_STEREO_NCO || oo == SDR_RX_O_RDS_NCO_I || oo == SDR_RX_O_RDS_NCO_Q;
     const bool lpf_o = oo == SDR_RX_O_RDS_LPF_I || oo == SDR_RX_O_RDS_LPF_Q;
-    r->made[oo] = need_out(r, oo) && (!nco_o || nco_rows) && (!lpf_o || lpf_rows);
+    const bool pin_o = oo == SDR_RX_O_BPF_RECOVERY || oo == SDR_RX_O_RDS_PRE_PLL;      // (codes: when kept)
+    r->made[oo] = need_out(r, oo) && (!nco_o || nco_rows) && (!lpf_o || lpf_rows) && (!pin_o || !codes || kept(oo));
   }
   HIP_TRY(mark(1 + SDR_RX_ST_E, st));
   if (r->pipe) HIP_TRY(hipEventRecord(r->ev_back[q], st));

@@ -100,7 +100,9 @@ struct PllJob {
   float* nco_i; float* nco_q; int64_t out_stride; PllCfg cfg; double* cbuf; int64_t c_stride;
   double off; int off_given;   // the prep kernel's trigOffset, when not read from state[5]
   const double* resp;          // long calls: the loop's response table (sdr_pll_resp_table), device
-  const double* qtab;          // the solve's matrix powers (pll.hip sdr_pll_qtab); set by the launcher
+  const double* qtab;          // the solve's matrix powers (pll.hip qtab_host); set by the launcher
+  const int8_t* in8;           // nullable: the input as sign codes (sdr_nco.h pll_code), in8_stride bytes
+  int64_t in8_stride;          //   apart per stream; read instead of `in` (long calls, spec-only calls)
 };
 // Long calls (n > SDR_PLL_BLOCK_MAX samples): the recurrence is cut into nb pseudo-blocks of
 // pb samples, solved in parallel from warm-up guesses of their start states and chained

@@ -76,6 +76,19 @@ __device__ __forceinline__ void sincos_red(double a, double* sv, double* cv) {
   *cv = (q == 1 || q == 2) ? -c0 : c0;
 }
 
+// The PLL's view of its input (model/fmPll.py:24-27): atan2(-x sin th, x cos th) depends on x
+// only through its sign -- and, for the literal general step, on the signs of the products when
+// x is a zero, or on a NaN.  A span's loop inputs therefore travel as one byte per sample
+// (r06): +1 / -1 for x > 0 / x < 0, 0 for +0, 2 for -0, 3 for NaN; decoded to the float with the
+// same atan2 (+-1, +-0, NaN).  The parallel solve reads +1 / -1 and treats the rest as its
+// general-form case, as it does the float row's zeros and NaNs.
+__device__ __forceinline__ int8_t pll_code(float v) {
+  return (int8_t)(v > 0.f ? 1 : v < 0.f ? -1 : v == 0.f ? (__builtin_signbit(v) ? 2 : 0) : 3);
+}
+__device__ __forceinline__ float pll_decode(int8_t c) {
+  return c == 1 ? 1.f : c == -1 ? -1.f : c == 0 ? 0.f : c == 2 ? -0.f : __builtin_nanf("");
+}
+
 }  // namespace sdrnco
 
 // ---- long calls: pseudo-block bookkeeping (device scratch PllJobs::work) --------------

@@ -333,7 +333,8 @@ def test_span_c5_timed_shape_eight_streams(sdr, gpu_ctx, oracle):
     streams in one receiver, spans of K = 256 blocks from device memory (sdr_rx_process_dev),
     i.e. a PLL job table of 16 recurrences x 275 pseudo-blocks chained in one launch, with the
     bench's keep set (no NCO or RDS LPF rows: the mixers form the NCO from the PLL phases, the
-    RDS LPF runs inside the composite resampler).  Two spans of a continuous stream per stream
+    RDS LPF runs inside the composite resampler; no f32 PLL-input rows: the PLLs read sign
+    codes).  Two spans of a continuous stream per stream
     (the second is the locked, timed state); the 8 streams are distinct windows of one
     synthetic capture.  Checked:
       (a) stream s of the 8-stream lean span == a 1-stream span over the same IQ that
@@ -357,7 +358,7 @@ def test_span_c5_timed_shape_eight_streams(sdr, gpu_ctx, oracle):
     row_bytes = rows.shape[1]
     del rows
     kw = dict(stereo=True, rds=True, iq_dtype=np.uint8)
-    lean = [nm for nm in NAMES if nm not in NCO_NAMES + ("lpf_i", "lpf_q")]
+    lean = [nm for nm in NAMES if nm not in NCO_NAMES + ("lpf_i", "lpf_q", "bpf_recovery", "pre_pll")]
     rx = sdr.Receiver(S, n, keep=lean, **kw)
     nb = long_blocks(K * (B5 // 10))
     stats = []
@@ -371,8 +372,9 @@ def test_span_c5_timed_shape_eight_streams(sdr, gpu_ctx, oracle):
     st = stats[-1]
     assert st["spec_r0"] == 2 * S * nb and st["sequential"] == 0 and st["long_stops"] == 0, st
     got = {name: rx.output(name) for name in lean}
-    with pytest.raises(ValueError, match="not materialised"):
-        rx.output("nco_i")
+    for name in ("nco_i", "pre_pll", "bpf_recovery"):
+        with pytest.raises(ValueError, match="not materialised"):
+            rx.output(name)
     rx.close()
     # (a) every stream against a 1-stream receiver over the same two spans, every output kept
     one = sdr.Receiver(1, n, **kw)
@@ -420,7 +422,7 @@ def test_keep_lean_equals_full(sdr, gpu_ctx, K):
     iq = np.stack([sdr.synth.fm_iq(calls * n, seed=120 + s, dtype=np.uint8) for s in range(S)])
     d = _lib.DeviceBuffer.from_array(gpu_ctx, iq)
     kw = dict(stereo=True, rds=True, iq_dtype=np.uint8)
-    lean_names = [nm for nm in NAMES if nm not in NCO_NAMES + ("lpf_i", "lpf_q")]
+    lean_names = [nm for nm in NAMES if nm not in NCO_NAMES + ("lpf_i", "lpf_q", "bpf_recovery", "pre_pll")]
     full, lean = sdr.Receiver(S, n, **kw), sdr.Receiver(S, n, keep=lean_names, **kw)
     for k in range(calls):
         for rx in (full, lean):
