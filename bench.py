@@ -523,8 +523,8 @@ def compact_line(result: dict) -> dict:
     out["devices"] = {"distinct": dv.get("distinct"), "ranks": dv.get("ranks")}
     cfg = result.get("config", {})
     out["config"] = _pick(cfg, ("blocks_per_step", "complex_per_step", "iq", "path"))
-    out["config"]["workload"] = (f"FE ({cfg.get('taps', '?')}-tap LPF, /10, atan2) + mono (151-tap LPF, /5): "
-                                 f"configs[1]+[2]") if "taps" in cfg else cfg.get("workload")
+    out["config"]["workload"] = (f"configs[1]+[2]: FE ({cfg.get('taps', '?')} taps, /10, atan2) + mono (151, /5)"
+                                 if "taps" in cfg else cfg.get("workload"))
     rf = result.get("roofline", {})
     out["roofline"] = _pick(rf, ("bound", "achieved", "peak", "unit", "frac", "traffic", "avg_launch_ms",
                                  "algorithmic_bytes_per_launch", "read_stream_gbs", "frac_of_stream_ceiling"))
@@ -532,7 +532,7 @@ def compact_line(result: dict) -> dict:
     cb = result.get("cpu_baseline")
     if cb is not None:
         c = _pick(cb, ("value", "unit", "cores", "kind"))
-        c["sample"] = (cb.get("sample") or "")[:80]
+        c["sample"] = (cb.get("sample") or "")[:48]
         ref = cb.get("reference_cpp_fe") or {}
         c["reference_cpp_fe"] = ref.get("value")
         out["cpu_baseline"] = c
@@ -554,12 +554,18 @@ def compact_line(result: dict) -> dict:
     if "c5" in result:
         r = result["c5"]
         pl = r.get("pll_solver") or {}
-        c5 = _pick(r, ("value", "ms_per_step", "stage_ms"))
+        # (stages by the receiver's names, include/sdr.h SDR_RX_ST_*: fe, A = filters of the demod,
+        # B = RDS x^2 + BPF, pll, C = stereo mixer + LPF, D = composite RDS filter, E = RRC)
+        sk = {"filters_of_demod": "A", "rds_square": "B", "mix_lpf": "C", "resample": "D", "rrc": "E"}
+        c5 = _pick(r, ("value", "ms_per_step"))
+        c5["stage_ms"] = {sk.get(k, k): v for k, v in (r.get("stage_ms") or {}).items()}
         c5["pll"] = {k: pl.get(k) for k in ("recurrences", "spec_r0", "sequential", "long_stops", "long_tail")}
         rl = r.get("roofline") or {}
-        c5["roofline"] = {"stage": rl.get("kernel_stage"), "bound": rl.get("bound"), "frac": rl.get("frac")}
+        c5["roofline"] = {"stage": sk.get(rl.get("kernel_stage"), rl.get("kernel_stage")), "bound": rl.get("bound"),
+                          "frac": rl.get("frac")}
         sr = (r.get("stage_roofline") or {}).get("stages") or {}
-        c5["stage_roofline"] = {k: [v.get("bound"), v.get("frac")] for k, v in sr.items()}
+        c5["stage_roofline"] = {sk.get(k, k): [v.get("bound"), round(v["frac"], 3) if v.get("frac") is not None else None]
+                                for k, v in sr.items()}
         c5["pll_roofline"] = (r.get("pll_roofline") or {}).get("frac")
         c5["cpu"] = cpu_v(r)
         out["c5"] = c5

@@ -307,7 +307,10 @@ int sdr_rx_fetch(sdr_rx* rx, int which, float* host, int64_t host_stride); /* sy
  * flags).  The NCO rows (SDR_RX_O_STEREO_NCO, _RDS_NCO_I/_Q) and the RDS LPF rows (_RDS_LPF_I/_Q)
  * are intermediates the chain itself does not need: without them the mixers form the NCO
  * from the PLL phases where they stage their inputs and the RDS LPF runs inside the composite
- * LPF + x19/80 resampler, so neither round-trips through HBM (the other outputs, which later
+ * LPF + x19/80 resampler, so neither round-trips through HBM.  On spans (rows of >= 32 768
+ * demod samples, the matrix-core tiles) the PLLs' f32 input rows (SDR_RX_O_BPF_RECOVERY,
+ * _RDS_PRE_PLL) are such intermediates too: the loops read their inputs as one sign-code
+ * byte per sample, which the producing tiles always store (the other outputs, which later
  * stages read, are always written; every output's values are the same either way).
  * sdr_rx_run / sdr_rx_submit materialise what they are asked for.  sdr_rx_fetch of an output
  * the latest block did not materialise is SDR_EINVAL (sdr_rx_output still gives its row). */

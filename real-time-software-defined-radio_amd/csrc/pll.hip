@@ -735,6 +735,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   // after a long call's pre-roll, so every step's wrap margin counts and every phase is stored.
   const bool wfull = __all(len == L);
   const bool wfast = wfull && __all(k0 >= pre);
+  const bool wpre = wfull && __all(k0 + L <= pre);      // (r06: the pre-roll wave of a full-length pseudo-block)
   // 0. where the locked phase estimate goes within the block, measured from the input: a
   // locked loop keeps its angle th_{k-1} = w (off + k) + phaseEst_{k-1} on the input tone's
   // phase, so z_j = sum over chunk j of x_k exp(-i w (off + k)) ~ (A/2) exp(i phaseEst) (+ an
@@ -997,8 +998,9 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     // smallest / largest fract(t) of the block's own steps, as f32 bit patterns (non-negative:
     // integer min / max order them; the margin is min(lo, 1 - hi))
     unsigned mlo = 0x3f800000u, mhi = 0u;
-    auto check = [&](auto FC) __attribute__((always_inline)) {
-      constexpr bool F = decltype(FC)::value;
+    // PO (a wave of pre-roll chunks only, F too): no phases to store, no wrap margins of its own
+    auto check = [&](auto FC, auto POC) __attribute__((always_inline)) {
+      constexpr bool F = decltype(FC)::value, PO = decltype(POC)::value;
       double kd = off + (double)k0;
       for (int i0 = 0; i0 < L; i0 += SB) {
         int cd[SB / 2];                          // (half a batch of codes at a time: registers)
@@ -1022,7 +1024,10 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
           const double S = p + V;
           const double nV = fma(kA, f, V - kB), np = fma(kC, f, S);
           const unsigned fb = __float_as_uint((float)f);
-          if constexpr (F) {
+          if constexpr (PO) {
+            V = nV;
+            p = np;
+          } else if constexpr (F) {
             V = nV;
             p = np;
             mlo = min(mlo, fb);
@@ -1035,8 +1040,9 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
             mhi = max(mhi, own ? fb : 0u);
           }
           if (act) mrel[tid * MSTR + i] = r;
-          tw[u * TBS + lane] = thval(p, k0 + i);
+          if constexpr (!PO) tw[u * TBS + lane] = thval(p, k0 + i);
         }
+        if constexpr (PO) continue;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1053,8 +1059,9 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     };
-    if (wfast) check(std::true_type{});
-    else check(std::false_type{});
+    if (wfast) check(std::true_type{}, std::false_type{});
+    else if (wpre) check(std::true_type{}, std::true_type{});
+    else check(std::false_type{}, std::false_type{});
     SPEC_TP();
     float mth = fminf(__uint_as_float(mlo), 1.f - __uint_as_float(mhi));
     xe_p = p;
@@ -1789,10 +1796,16 @@ bool pll_long(const PllJobs& P) { return long_n(P.n); }
 // most SPEC_NMAX - 1 steps (its LDS image)
 constexpr int LONG_PRE_MAX = 2048;
 constexpr int LONG_PB = SPEC_NMAX - 1 - LONG_PRE_MAX;
+// r06: pseudo-blocks of exactly LONG_PB steps (the last one shorter) whenever that leaves the
+// last at least 2 steps -- so that with the LONG_PRE_MAX + 1-step pre-roll (warm_len) a middle
+// pseudo-block's solve is SPEC_NMAX steps: 512 full chunks of 32, every wave on the full-chunk
+// loops, and the pre-roll exactly the first wave's chunks (r05 balanced the lengths, 14 299 at
+// a C5 span: the last wave ran its partial chunk's predicated loops and the workgroup's
+// barriers waited for it -- the phase timers' guess and check barriers)
 void long_geom(int64_t n, int64_t* pb, int* nb) {
   const int64_t k = (n + LONG_PB - 1) / LONG_PB;
   *nb = (int)k;
-  *pb = (n + k - 1) / k;
+  *pb = n - (k - 1) * LONG_PB >= 2 ? LONG_PB : (n + k - 1) / k;
 }
 
 // the loop's linear form on the start error (dphaseEst, dV): A = [[1 - kC/2pi, 1], [-kA/2pi, 1]]
@@ -1839,7 +1852,11 @@ void loop_bounds(const PllCfg& c, double* c1, double* c2) {
 // seed's error (the measured phase: ~0.1 rad) within LONG_ACCEPT (the stereo loop: ~1 500),
 // unless that exceeds LONG_PRE_MAX = 2 048 (the RDS loop would need ~15 000) -- then 1 024
 // steps, enough for the linear bound; such blocks are fixed up from the chained start.
+// Full-length pseudo-blocks (long_geom) take LONG_PRE_MAX + 1 = 2 049 for both loops.
 int warm_len(const PllCfg& c, double c1, int64_t pb) {
+  // full-length pseudo-blocks: the pre-roll fills the solve (SPEC_NMAX steps), longer than
+  // either loop needs (below) -- chunk-aligned: the first wave's 64 x 32 steps exactly
+  if (pb == LONG_PB) return SPEC_NMAX - LONG_PB;
   constexpr int cap = LONG_PRE_MAX;
   const double rate = -0.5 * std::log1p(-std::min(std::max(c.kp, 1e-12), 0.999));
   const double want = std::log(std::max(c1, 1.0) * 0.1 / LONG_ACCEPT) / rate;   // from a 0.1 rad seed

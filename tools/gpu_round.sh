@@ -12,6 +12,7 @@
 #   bench:<name>:<args...>   bench.py with args (commas for spaces)     -> bench_<name>.json
 #   prof:<name>:<args...>    rocprofv3 --kernel-trace --stats of it     -> prof_<name>/, prof_<name>.json
 #   pmc:<name>:<counters>:<args...>  one --pmc pass (counters comma-separated) -> pmc_<name>/
+#   trace:<name>:<args...>   rocprofv3 --hip-trace --kernel-trace --stats of it (host API calls) -> trace_<name>/
 #   dist:<n>:<args...>       torchrun with n ranks on this box (--allow-wrap) -> dist<n>.json
 # e.g. tools/gpu_round.sh gpurun_out/r04 tests bench prof:c5s8:--workload,c5,--steps,5,--no-cpu
 set -e
@@ -42,6 +43,11 @@ for step in "$@"; do
       cd /tmp
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$name" -o prof \
         -- python3 "$R/bench.py" $(sp "$args") > "$O/prof_$name.json" 2> "$O/prof_$name.err" ;;
+    trace:*)
+      IFS=: read -r _ name args <<< "$step"
+      cd /tmp
+      timeout -k 10 400 rocprofv3 --hip-trace --kernel-trace --stats --output-format csv -d "$O/trace_$name" -o trace \
+        -- python3 "$R/bench.py" $(sp "$args") > "$O/trace_$name.json" 2> "$O/trace_$name.err" ;;
     pmc:*)
       IFS=: read -r _ name ctrs args <<< "$step"
       cd /tmp
