@@ -126,8 +126,11 @@ int get_resp(sdr_ctx* c, const PllCfg& cfg, int64_t n, const double** out) {
   t.kp = cfg.kp;
   t.ki = cfg.ki;
   t.pb = pb;
-  HIP_TRY(hipMalloc(&t.dev, sizeof(double) * h.size()));
+  // the f64 rows, then the same rows in f32 (NcoSrc::resp32, sdr_resp32)
+  std::vector<float> hf(h.begin(), h.end());
+  HIP_TRY(hipMalloc(&t.dev, sizeof(double) * h.size() + sizeof(float) * hf.size()));
   HIP_TRY(hipMemcpy(t.dev, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(t.dev + h.size(), hf.data(), sizeof(float) * hf.size(), hipMemcpyHostToDevice));
   c->resp.push_back(t);
   *out = t.dev;
   return SDR_OK;

@@ -2159,6 +2159,9 @@ int sdr_rx_set_pipeline(sdr_rx* r, int on) {
   if (r->ready) return fail(SDR_EINVAL, "sdr_rx_set_pipeline: the receiver has processed a block");
   if (on && !r->front) {
     TRY(set_dev(r->c));
+    // (default priorities: an A/B of a high-priority PLL stream, a high-priority front stream and
+    // low-priority front + PLL streams on one box measured C5 339-349 k against 352-355 k MS/s
+    // for equal priorities, profiles/r06/e/prio_ab.txt)
     HIP_TRY(hipStreamCreateWithFlags(&r->front, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&r->mid, hipStreamNonBlocking));
     for (int q = 0; q < 3; ++q) {
@@ -2349,6 +2352,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
         N.nb = nb;
         N.pb = pb;
         N.resp = resp;
+        N.resp32 = resp32_of(resp, pb);
       }
       return SDR_OK;
     };

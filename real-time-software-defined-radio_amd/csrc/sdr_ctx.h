@@ -69,6 +69,10 @@ int get_taps(sdr_ctx* c, const double* b, int T, const TapSet** out, int max_T =
 // the device response table of loop cfg for a long call of n steps (cached per context);
 // *out = NULL when n is not a long call
 int get_resp(sdr_ctx* c, const PllCfg& cfg, int64_t n, const double** out);
+// the f32 copy get_resp stores after a table of pseudo-block length pb (2 (pb + 5) doubles)
+inline const float* resp32_of(const double* resp, int64_t pb) {
+  return resp != nullptr ? reinterpret_cast<const float*>(resp + 2 * (pb + 5)) : nullptr;
+}
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

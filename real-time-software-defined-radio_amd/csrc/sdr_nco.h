@@ -127,6 +127,7 @@ struct NcoSrc {
   int64_t blk_stride, pb;
   int nb;                  // pseudo-blocks of the call
   const double* resp;
+  const float* resp32;     // the same table in f32 (the matrix-core mixers' response: an angle <= 0.15 rad)
 };
 
 // The recurrence's phaseEst for step kk of a long call's pseudo-block B whose solve stored
@@ -309,14 +310,14 @@ __device__ __forceinline__ void nco_f32x4(const NcoSrc& N, const NcoTile& T, int
   nco_poly2({y[2], y[3]}, {q[2], q[3]}, &c[2], &sn[2]);
 }
 
-// nco_f32x4 in two halves, for consumers that software-pipeline their loads (rx.hip's matrix-
-// core mixers): nco4_load issues every load of inputs i .. i+3 (i >= 1 odd) -- the phase pairs
-// and, when the tile's pseudo-blocks carry a linear response (lin: uniform), the response rows
-// -- and nco4_eval forms the four cos / sin with nco_f32x4's arithmetic exactly.
+// The matrix-core mixers' loads of inputs i .. i+3 (i >= 1 odd), issued ahead of their use
+// (software-pipelined, rx.hip): the phase pairs and, when the tile's pseudo-blocks carry a
+// linear response (lin: uniform), the response rows (f32, r06).
 struct Nco4Ld {
   typedef double d2n __attribute__((ext_vector_type(2)));
+  typedef float f2n __attribute__((ext_vector_type(2)));
   d2n t01, t23;
-  d2n rr[4];
+  f2n rr[4];
 };
 __device__ __forceinline__ bool nco_tile_lin(const NcoTile& T) {
   return T.d0[0] != 0.0 || T.d1[0] != 0.0 || T.d0[1] != 0.0 || T.d1[1] != 0.0;
@@ -324,6 +325,7 @@ __device__ __forceinline__ bool nco_tile_lin(const NcoTile& T) {
 // (i odd: the four phases phaseEst_{i-1} .. phaseEst_{i+2} are two aligned pairs, t01 and t23)
 __device__ __forceinline__ void nco4_load(const NcoSrc& N, const NcoTile& T, int64_t i, bool lin, Nco4Ld* L) {
   typedef Nco4Ld::d2n d2n;
+  typedef Nco4Ld::f2n f2n;
   const double* th = T.th + i - 1;
   L->t01 = *reinterpret_cast<const d2n*>(th);
   L->t23 = *reinterpret_cast<const d2n*>(th + 2);
@@ -334,33 +336,10 @@ __device__ __forceinline__ void nco4_load(const NcoSrc& N, const NcoTile& T, int
     const int64_t j0 = i - 1;
     const int64_t k0 = j0 - (j0 >= T.bound ? T.bound : T.kb);
     const int64_t kk = k0 > 0 ? k0 : (int64_t)0;                  // (>= 0: clamped rows)
-    const d2n* rr = reinterpret_cast<const d2n*>(N.resp) + (kk + 1);
+    const f2n* rr = reinterpret_cast<const f2n*>(N.resp32) + (kk + 1);
 #pragma unroll
     for (int e = 0; e < 4; ++e) L->rr[e] = rr[e];
   }
-}
-__device__ __forceinline__ void nco4_eval(const NcoSrc& N, const NcoTile& T, int64_t i, const Nco4Ld& L, bool lin,
-                                          float (&c)[4], float (&sn)[4]) {
-#pragma clang fp contract(off)
-  const double st[4] = {L.t01.x, L.t01.y, L.t23.x, L.t23.y};   // phaseEst_{i-1} .. phaseEst_{i+2}
-  double p[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int64_t j = i - 1 + e;
-    const bool h = j >= T.bound;
-    const double sh = h ? T.sh[1] : T.sh[0];
-    p[e] = fma(sh, sdrnco::kP1, fma(sh, sdrnco::kP2, st[e]));
-    if (lin) {
-      const double d0 = h ? T.d0[1] : T.d0[0], d1 = h ? T.d1[1] : T.d1[0];
-      if (d0 != 0.0 || d1 != 0.0) p[e] = p[e] + (L.rr[e].x * d0 + L.rr[e].y * d1);
-    }
-  }
-  float y[4];
-  int q[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) nco_angle(N, T.off, i + e, p[e], &y[e], &q[e]);
-  nco_poly2({y[0], y[1]}, {q[0], q[1]}, &c[0], &sn[0]);
-  nco_poly2({y[2], y[3]}, {q[2], q[3]}, &c[2], &sn[2]);
 }
 
 // The matrix-core mixers' angle, per window (rx.hip rx_stereomm_kernel / rx_cresmm_kernel):
@@ -376,7 +355,7 @@ __device__ __forceinline__ void nco4_eval(const NcoSrc& N, const NcoTile& T, int
 // full magnitude).  The f32 polynomials are nco_poly2's.
 struct NcoWin {
   double base[2];          // per pseudo-block half h (as NcoTile)
-  double sd0[2], sd1[2];   // scale d, per half (the linear response)
+  float sd0[2], sd1[2];    // scale d, per half (the linear response, formed in f32: r06)
   double ws, scale;
   int64_t kw;              // the reference sample
 };
@@ -397,8 +376,8 @@ __device__ __forceinline__ NcoWin nco_win(const NcoSrc& N, const NcoTile& T, int
   for (int h = 0; h < 2; ++h) {
     const double f = N.scale * T.sh[h];
     W.base[h] = r + (f - rint(f)) * sdrnco::k2Pi;
-    W.sd0[h] = N.scale * T.d0[h];
-    W.sd1[h] = N.scale * T.d1[h];
+    W.sd0[h] = (float)(N.scale * T.d0[h]);
+    W.sd1[h] = (float)(N.scale * T.d1[h]);
   }
   return W;
 }
@@ -409,20 +388,18 @@ __device__ __forceinline__ void nco4_eval_w(const NcoTile& T, const NcoWin& W, i
   constexpr double k2oPi = 0.6366197723675814;
   constexpr double Q1 = 1.5707963705062866, Q2 = -4.3711390001862426e-08;   // 2-part pi/2 (|n| < 2^29)
   const double st[4] = {L.t01.x, L.t01.y, L.t23.x, L.t23.y};   // phaseEst_{i-1} .. phaseEst_{i+2} (stored)
-  const double dk = (double)(int)(i - W.kw);
-  double tb0 = fma(W.ws, dk, W.base[0]), tb1 = fma(W.ws, dk, W.base[1]);
+  const int dk = (int)(i - W.kw);
   float y[4];
   int q[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t j = i - 1 + e;
     const bool h = j >= T.bound;
-    if (e > 0) {                                      // the next output: + ws
-      tb0 = tb0 + W.ws;
-      tb1 = tb1 + W.ws;
-    }
-    double a = fma(st[e], W.scale, h ? tb1 : tb0);
-    if (lin) a = a + (L.rr[e].x * (h ? W.sd0[1] : W.sd0[0]) + L.rr[e].y * (h ? W.sd1[1] : W.sd1[0]));
+    // (r06: the base of output i + e in one fma, and the linear response -- an angle of at most
+    // 0.3 scale rad -- in f32 (its rounding ~1e-8 rad, below the f32 cos / sin): 7 f64
+    // operations a sample instead of 10)
+    double a = fma(st[e], W.scale, fma(W.ws, (double)(dk + e), h ? W.base[1] : W.base[0]));
+    if (lin) a = a + (double)fmaf(L.rr[e].x, h ? W.sd0[1] : W.sd0[0], L.rr[e].y * (h ? W.sd1[1] : W.sd1[0]));
     const double n = rint(a * k2oPi);
     double r = fma(-n, Q1, a);
     r = fma(-n, Q2, r);
