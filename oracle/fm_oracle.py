@@ -38,17 +38,61 @@ def lfilter_fir(b, x, zi=None):
 
 
 def lfilter_decim(b, x, zi, decim):
-    """lfilter(...)[::decim] (model/fmMonoBlock.py:94-95,105)."""
-    y, zf = lfilter_fir(b, x, zi)
-    return y[::decim].copy(), zf
+    """lfilter(...)[::decim] (model/fmMonoBlock.py:94-95,105) and the final state, computing
+    only the kept outputs (the checker's speed: scipy.signal.upfirdn, the same sums as
+    lfilter_fir's in another order -- tests/test_oracle.py::test_decim_and_resample_fast_forms)."""
+    b = np.asarray(b, dtype=np.float64)
+    x = np.asarray(x, dtype=np.float64)
+    T, n = len(b), len(x)
+    y = signal.upfirdn(b, x, 1, decim)[:(n + decim - 1) // decim] if n else np.zeros(0)
+    zi = np.zeros(T - 1) if zi is None else np.asarray(zi, dtype=np.float64)
+    m = np.arange(0, min(n, T - 1), decim)
+    y[m // decim] += zi[m]
+    k = np.arange(T - 1)
+    zf = np.where(n + k < T - 1, zi[np.minimum(n + k, T - 2)], 0.0)
+    idx = n - (T - 1) + k                                  # the last T - 1 inputs (zero before the start)
+    tail = np.where(idx >= 0, x[np.clip(idx, 0, max(n - 1, 0))] if n else 0.0, 0.0)
+    zf = zf + np.convolve(b, tail)[T - 1:2 * T - 2]
+    return y, zf
 
 
-def resample(x, b, zi, up, down):
-    """Zero-stuff by `up`, anti-image lfilter, [::down] * up (model/fmRDSblock.py:184-199)."""
+def resample_literal(x, b, zi, up, down):
+    """Zero-stuff by `up`, anti-image lfilter, [::down] * up (model/fmRDSblock.py:184-199),
+    literally (the zero-stuffed stream through lfilter_fir)."""
     u = np.zeros(len(x) * up)
     u[::up] = x
     y, zf = lfilter_fir(b, u, zi)
     return y[::down] * up, zf
+
+
+def resample(x, b, zi, up, down):
+    """resample_literal's values computed polyphase (the checker's speed: only the taps that meet
+    a nonzero stuffed sample are summed, up times fewer products; the same sums in another
+    order -- tests/test_oracle.py::test_resample_polyphase_equals_literal): output n of the
+    stuffed stream is sum_i b[n mod up + up i] x[n // up - i] (+ zi[n], n < T - 1), its final
+    state zf[k] = sum_{j > k, j = N + k mod up} b[j] x[(N + k - j) / up] (+ zi[N + k])."""
+    b = np.asarray(b, dtype=np.float64)
+    x = np.asarray(x, dtype=np.float64)
+    T, nx = len(b), len(x)
+    N = nx * up
+    n = np.arange(0, N, down)
+    r, q = n % up, n // up
+    y = np.zeros(len(n))
+    for i in range((T + up - 1) // up):
+        j = r + up * i
+        qi = q - i
+        ok = (j < T) & (qi >= 0)
+        y[ok] += b[j[ok]] * x[qi[ok]]
+    zi = np.asarray(zi, dtype=np.float64)
+    head = n < T - 1
+    y[head] += zi[n[head]]
+    k = np.arange(T - 1)
+    zf = np.where(N + k < T - 1, zi[np.minimum(N + k, T - 2)], 0.0)
+    # the stuffed stream's last T - 1 samples (zero before its start): zf = (b * tail)[T-1 .. 2T-3]
+    m = N - (T - 1) + k
+    tail = np.where((m >= 0) & (m % up == 0), x[np.clip(m // up, 0, nx - 1)] if nx else 0.0, 0.0)
+    zf = zf + np.convolve(b, tail)[T - 1:2 * T - 2]
+    return y * up, zf
 
 
 # ---- FM discriminator ---------------------------------------------------------------
@@ -208,8 +252,7 @@ def mono_stereo_blocks(iq, block_complex, rf_taps=151, audio_taps=151, stereo=Tr
         o = {"nco": nco}
         if c is chains[0] or k >= alt_from - 1:
             mixed = np.multiply(nco[0:len(r["bpf_extraction"])], r["bpf_extraction"]) * 2
-            s_f, c["st_zi"] = lfilter_fir(st_b, mixed, c["st_zi"])
-            o["stereo"] = s_f[::5].copy()
+            o["stereo"], c["st_zi"] = lfilter_decim(st_b, mixed, c["st_zi"], 5)
             o["left"] = (r["audio"] + o["stereo"]) / 2
             o["right"] = (r["audio"] - o["stereo"]) / 2
         return o
@@ -218,12 +261,10 @@ def mono_stereo_blocks(iq, block_complex, rf_taps=151, audio_taps=151, stereo=Tr
     while (k + 1) * B < len(iq) and (nblocks is None or k < nblocks):   # strict "<" as :80
         blk = iq[k * B:(k + 1) * B]
         r = {}
-        i_f, zi_i = lfilter_fir(rf_b, blk[0::2], zi_i)
-        q_f, zi_q = lfilter_fir(rf_b, blk[1::2], zi_q)
-        r["i_ds"], r["q_ds"] = i_f[::10].copy(), q_f[::10].copy()
+        r["i_ds"], zi_i = lfilter_decim(rf_b, blk[0::2], zi_i, 10)
+        r["q_ds"], zi_q = lfilter_decim(rf_b, blk[1::2], zi_q, 10)
         r["demod"], phase = demod_fn(r["i_ds"], r["q_ds"], phase)
-        a_f, au_zi = lfilter_fir(au_b, r["demod"], au_zi)
-        r["audio"] = a_f[::5].copy()
+        r["audio"], au_zi = lfilter_decim(au_b, r["demod"], au_zi, 5)
         r["phase"] = phase
         if stereo:
             r["bpf_recovery"], rec_zi = lfilter_fir(pil_b, r["demod"], rec_zi)
@@ -331,9 +372,9 @@ def rds_blocks(iq_u8, block_values=307200, taps=151, nblocks=None, demod_fn=fm_d
     while (k + 1) * block_values < len(iq) and (nblocks is None or k < nblocks):   # :127
         blk = iq[k * block_values:(k + 1) * block_values]
         r = {}
-        i_f, zi_i = lfilter_fir(rf_b, blk[0::2], zi_i)
-        q_f, zi_q = lfilter_fir(rf_b, blk[1::2], zi_q)
-        r["demod"], phase = demod_fn(i_f[::10].copy(), q_f[::10].copy(), phase)
+        i_ds, zi_i = lfilter_decim(rf_b, blk[0::2], zi_i, 10)
+        q_ds, zi_q = lfilter_decim(rf_b, blk[1::2], zi_q, 10)
+        r["demod"], phase = demod_fn(i_ds, q_ds, phase)
         r["extract"], ex_zi = lfilter_fir(co["extract"], r["demod"], ex_zi)
         r["pre_pll"], sq_zi = lfilter_fir(co["square"], np.square(r["extract"]), sq_zi)
         r.update(rds_tail(r, chains[0], r["pre_pll"]))

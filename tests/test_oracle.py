@@ -54,6 +54,26 @@ def test_rds_chain_matches_golden(oracle, golden):
             assert maxabs(r[key], g[key][k]) < 1e-9 * scale, (key, k)
 
 
+@pytest.mark.parametrize("n", [1, 7, 149, 150, 151, 1000, 15360])
+def test_decim_and_resample_fast_forms(oracle, n):
+    """The checker's fast forms compute the literal statements' values: lfilter_decim ==
+    lfilter_fir(...)[::D] with its zf (upfirdn, only the kept outputs), resample == the
+    zero-stuffed lfilter (polyphase), on carried states, for short and long blocks."""
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n)
+    rf, au = oracle.mono_coeffs(151, 151)
+    for b, D in ((rf, 10), (au, 5)):
+        zi = rng.standard_normal(len(b) - 1)
+        y, zf = oracle.lfilter_fir(b, x, zi)
+        y2, zf2 = oracle.lfilter_decim(b, x, zi, D)
+        assert y2.shape == y[::D].shape and maxabs(y2, y[::D]) < TIGHT and maxabs(zf2, zf) < TIGHT
+    for b, up, down in ((oracle.rds_coeffs(151)["anti_img"], 19, 80), (oracle.mode1_coeffs()["res"], 24, 125)):
+        zi = rng.standard_normal(len(b) - 1)
+        y, zf = oracle.resample_literal(x, b, zi, up, down)
+        y2, zf2 = oracle.resample(x, b, zi, up, down)
+        assert y2.shape == y.shape and maxabs(y2, y) < TIGHT and maxabs(zf2, zf) < TIGHT
+
+
 def test_oracle_alt_chain_is_the_chain(oracle, golden):
     """The second fmPll + downstream chain the span tests run on the device's loop inputs
     (alt_in / alt_from, tests/test_span.py): fed the oracle's own inputs, it reproduces the main
