@@ -876,6 +876,7 @@ def pll_roofline(stage_ms_pll, S, K, B, steps_per_span, path=None):
             "source": os.path.relpath(path, ROOT) + " (SQ counts per span call) + this run's PLL stage time"}
 
 
+SIMDS, CLOCK_HZ = 256 * 4, 2.4e9   # MI355X: 256 CUs x 4 SIMDs; nominal clock (the chip runs lower under load)
 MFMA_F16_PEAK_TFLOPS = 2500.0    # dense f16 / bf16 matrix-core peak (MI355X_MICROARCH.md; not the 2:1-sparse figure)
 MFMA_I8_PEAK_TOPS = 5000.0       # dense int8 matrix-core peak: 2x the f16 rate per clock (MI355X_MICROARCH.md)
 C5_PMC = os.path.join(ROOT, "profiles", "r06", "c5_pmc.json")
@@ -915,6 +916,15 @@ def c5_stage_roofline(stage_ms, S, K, B, path=C5_PMC):
         if c.get("f64_wave_instr"):
             g = c["f64_wave_instr"] / sec
             e["f64_issue"] = {"achieved_g_wave_instr_s": round(g / 1e9, 1), "frac": round(g / F64_WAVE_INSTR_PEAK, 4)}
+        # the SIMDs' vector issue and matrix pipes: busy cycles (SQ_ACTIVE_INST_VALU counts quad-cycles)
+        # over the stage's SIMD-cycles at the nominal 2.4 GHz
+        simd_cycles = SIMDS * CLOCK_HZ * sec
+        if c.get("valu_active_quad_cycles"):
+            e["valu_issue"] = {"busy_simd_cycles": c["valu_active_quad_cycles"] * 4,
+                               "frac": round(4 * c["valu_active_quad_cycles"] / simd_cycles, 4)}
+        if c.get("mfma_busy_cycles"):
+            e["mfma_busy"] = {"busy_simd_cycles": c["mfma_busy_cycles"],
+                              "frac": round(c["mfma_busy_cycles"] / simd_cycles, 4)}
         lim = {k: v["frac"] for k, v in e.items() if isinstance(v, dict)}
         if lim:
             e["bound"] = max(lim, key=lim.get)
@@ -1068,10 +1078,14 @@ def c5_measure(ctx, S, K, steps, warmup, rank, ws, pipeline=True, cpu=False, arg
         # the line's roofline: the dominant stage's own, against the ceiling it comes closest to
         d = sr["stages"].get(dom)
         if d is not None and "bound" in d:
-            unit = {"hbm": "GB/s", "mfma_f16": "TFLOP/s", "mfma_i8": "TOP/s", "f64_issue": "G f64 wave-instr/s"}[d["bound"]]
-            ach = next(v for k, v in d[d["bound"]].items() if k.startswith("achieved"))
+            unit = {"hbm": "GB/s", "mfma_f16": "TFLOP/s", "mfma_i8": "TOP/s", "f64_issue": "G f64 wave-instr/s",
+                    "valu_issue": "SIMD-cycles", "mfma_busy": "SIMD-cycles"}[d["bound"]]
+            b = d[d["bound"]]
+            ach = next(v for k, v in b.items() if k.startswith("achieved") or k.startswith("busy"))
             peak = {"hbm": HBM_PEAK_GBS, "mfma_f16": MFMA_F16_PEAK_TFLOPS, "mfma_i8": MFMA_I8_PEAK_TOPS,
-                    "f64_issue": round(F64_WAVE_INSTR_PEAK / 1e9, 1)}[d["bound"]]
+                    "f64_issue": round(F64_WAVE_INSTR_PEAK / 1e9, 1),
+                    "valu_issue": round(SIMDS * CLOCK_HZ * d["ms"] * 1e-3),
+                    "mfma_busy": round(SIMDS * CLOCK_HZ * d["ms"] * 1e-3)}[d["bound"]]
             out["roofline"] = {"bound": d["bound"], "kernel_stage": dom, "achieved": ach, "peak": peak, "unit": unit,
                                "frac": d["frac"], "traffic": c5_stage_bytes(dom),
                                "note": ("the dominant stage's own ceiling (stage_roofline); traffic: its HBM bytes per "

@@ -8,7 +8,8 @@ usage: python3 tools/pmc_c5.py OUT.json DIR [DIR ...]
   DIR: a pass's output dir (holding pmc_counter_collection.csv); the passes are merged.
 Counters used when present: FETCH_SIZE (x 2: the gfx950 wide-read correction,
 MI355X_MICROARCH.md), WRITE_SIZE, SQ_INSTS_VALU_MFMA_MOPS_F16 / _I8 (x 512 = executed
-matrix-core ops), SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64, SQ_INSTS_VALU, SQ_WAVES.
+matrix-core ops), SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64, SQ_INSTS_VALU, SQ_WAVES,
+SQ_ACTIVE_INST_VALU (quad-cycles of vector issue), SQ_VALU_MFMA_BUSY_CYCLES (matrix-pipe cycles).
 
 The stages are the receiver's timing stages (csrc/rx.hip, sdr_rx_stage_ms):
   fe                fe_mfma_demod_kernel<151>
@@ -92,14 +93,16 @@ def main():
                                 "SQ_INSTS_VALU_TRANS_F64") if c in acc]
         if f64:
             s["f64_wave_instr"] = sum(f64)
-        for c, key in (("SQ_INSTS_VALU", "valu_wave_instr"), ("SQ_WAVES", "waves")):
+        for c, key in (("SQ_INSTS_VALU", "valu_wave_instr"), ("SQ_WAVES", "waves"),
+                       ("SQ_ACTIVE_INST_VALU", "valu_active_quad_cycles"),
+                       ("SQ_VALU_MFMA_BUSY_CYCLES", "mfma_busy_cycles")):
             if c in acc:
                 s[key] = acc[c]
         stages[st] = s
     res = {"config": {"workload": "c5", "streams": 8, "span": 256, "block_complex": 153_600},
            "note": ("per span call (medians over a kernel's dispatches, summed over the stage's kernels): HBM bytes "
-                    "(FETCH_SIZE x 2, WRITE_SIZE), executed matrix-core ops (MOPS x 512), f64 VALU wave-instructions; "
-                    "tools/pmc_c5.py"),
+                    "(FETCH_SIZE x 2, WRITE_SIZE), executed matrix-core ops (MOPS x 512), f64 VALU wave-instructions, "
+                    "vector-issue quad-cycles (SQ_ACTIVE_INST_VALU), matrix-pipe busy cycles; tools/pmc_c5.py"),
            "stages": stages, "kernels": kernels, "sources": [os.path.relpath(d) for d in dirs]}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
