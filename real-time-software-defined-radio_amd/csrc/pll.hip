@@ -477,6 +477,8 @@ constexpr int SB = 8;                        // steps per batch of LDS reads in 
 // (SPEC_T = 256 takes up to SPEC_N256 steps: L <= 40), QT_N 2x2 matrices of Q = A^L --
 // Q^e for e = 0 .. 64, then Q^(64 w) for w = 0 .. 7 (the waves of a 512-thread solve)
 constexpr int QT_N = 65 + 8, QT_NL = 5;
+// compact phase rows: lines per pseudo-block (pb <= LONG_PB = SPEC_NMAX - 1 - 2048, below)
+constexpr int TH32_LINES = (SPEC_NMAX - 1 - 2048) / TH32_LINE;
 
 // ---- long calls: pseudo-block bookkeeping (device scratch P.work; LongBlk / LongHdr in
 // sdr_nco.h, which the receiver's mixers read too) ---------------------------------------
@@ -628,6 +630,16 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   double* th = J.theta + (int64_t)s * J.th_stride + base;
   double* cr = J.cbuf + (int64_t)s * J.c_stride + base;
   const PllCfg cfg = J.cfg;
+  // compact phase rows (sdr_nco.h, LONG with J.th32): the pseudo-block's lines (a, s), set each
+  // round by the thread whose steps hold a line's first row, read by every thread's stores
+  const bool t32 = LONG && J.th32 != 0;
+  Th32Line* tl = nullptr;
+  if constexpr (LONG) {
+    __shared__ Th32Line tl_[TH32_LINES];
+    tl = tl_;
+  }
+  double* rowp = J.theta + (int64_t)s * J.th_stride;   // the stream's row (compact: residuals, then lines)
+  const int64_t rb = base + pre;                        // the pseudo-block's first row
 #ifdef SDR_PLL_SPEC_PROF    // phase timers (diagnostic builds only, tools/build_dbg.sh)
   long long tp[16];
   int ntp = 0;
@@ -942,6 +954,21 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   auto qp = [&](int i) { return QT[1 << i]; };   // Q^(2^i), i <= 6
   double* tw = tb + wv * SB * TBS;               // this wave's transpose tile
   for (int round = 0; round < SPEC_IT; ++round) {
+    // compact rows: the line whose first row (row kk = 0 mod 32 of the pseudo-block, step
+    // kk + pre) is among the rows from this thread's start state (row k0 - 1) to its last step
+    // but one -- at most one, L <= 32; the ranges tile the solve -- from this thread's last
+    // pass over its chunk: its start and its slope.  (The pseudo-block's last row, when it
+    // starts a line, is left to the end of the solve.)  Written before the scan's barrier, read
+    // by the stores after it
+    if (t32 && tid < TE) {
+      const int kk = ((max(k0 - 1, pre) - pre) + TH32_LINE - 1) & ~(TH32_LINE - 1);
+      if (kk + pre < k0 + len - 1) {
+        const double sl = (xe_p - xs_p) / (double)len;
+        const Th32Line ln{fma(sl, (double)(kk + pre - (k0 - 1)), xs_p), sl};
+        tl[kk / TH32_LINE] = ln;
+        th32_lines(rowp, P.n)[(rb + kk) / TH32_LINE] = ln;
+      }
+    }
     // 2. solve: the chunk's response from zero state to the current integers, from the last
     // pass over it (the guess in round 0, the previous check after): z_j = x_end - Q x_start
     double zp, zv;
@@ -1052,7 +1079,15 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
           const int ch = r8 * SB + cw;                   // chunk within the wave
           const int k = 1 + (wv * 64 + ch) * L + i0 + u;
           const double v = tw[u * TBS + ch];
-          if (F || (k >= pre && k < (int)n)) th[k] = v;
+          const bool keep = F || (k >= pre && k < (int)n);
+          if (t32) {                                     // (uniform) its residual against its line
+            const int kk = k - pre;
+            const Th32Line ln = tl[min(max(kk, 0) / TH32_LINE, TH32_LINES - 1)];
+            const float rv = th32_residual(ln, kk & (TH32_LINE - 1), v);
+            if (keep) th32_res(rowp)[rb + kk] = rv;
+          } else if (keep) {
+            th[k] = v;
+          }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1104,7 +1139,10 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       }
       // done: the caller-visible results exactly as the loop kernels leave them
       if (tid == 0) {
-        if (pre == 0) th[0] = thval(p1, 0);
+        if (pre == 0) {
+          if (t32) th32_res(rowp)[rb] = th32_residual(tl[0], 0, p1);
+          else th[0] = thval(p1, 0);
+        }
         if constexpr (!LONG) {
           J.nco_i[(int64_t)s * J.out_stride] = (float)st[4];
           if (J.nco_q)
@@ -1114,6 +1152,11 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       }
       __syncthreads();                           // st[1], st[4] read before the last chunk writes st
       if (tid == TE - 1) {
+        if (t32 && ((n - 1 - pre) & (TH32_LINE - 1)) == 0) {   // the last row starts a line: the line is its own
+          const int64_t kl = rb + (n - 1 - pre);
+          th32_lines(rowp, P.n)[kl / TH32_LINE] = Th32Line{p, 0.0};
+          th32_res(rowp)[kl] = 0.f;
+        }
         const double arg = wsh * ((off + (double)(n - 1)) + 1.0) + p;
         if constexpr (!LONG) th[n] = off;
         st_out[0] = V + kds;
@@ -1160,7 +1203,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
 }
 
 __device__ void seq_run(const PllCfg& cfg, const float* in, const int8_t* in8, double* th, int64_t n, const double* st,
-                        double* so);
+                        double* so, float* r32 = nullptr, Th32Line* lines = nullptr);
 
 // A per-block call's recurrence the solve does not complete (a 0 / NaN input, a loop not yet
 // locked) runs sequentially in the same workgroup (one thread, seq_run's general form) --
@@ -1290,9 +1333,11 @@ constexpr int LONG_FIXES = 24;         // repairs (re-solves at the chain's posi
 // The reference's recurrence run sequentially from state st over n steps (the general form:
 // literal first step from the state's (fI, fQ); 0 / NaN inputs by atan2 on the products; the
 // rest by the constants pll_c).  Inputs from `in`, or decoded from the sign codes in8 when
-// given.  Phases into th[0..n), the end state into so.
+// given.  Phases into th[0..n), the end state into so -- or, compact rows (lines != null, th
+// the first row of a line), residuals into r32[0..n) against lines[k / 32], each line set at
+// its first row from the phase there and the integrator (the loop's mean step).
 __device__ void seq_run(const PllCfg& cfg, const float* in, const int8_t* in8, double* th, int64_t n, const double* st,
-                        double* so) {
+                        double* so, float* r32, Th32Line* lines) {
 #pragma clang fp contract(off)
   const double w = 2.0 * kPi * (cfg.freq / cfg.fs);
   double integ = st[0], phase = st[1];
@@ -1300,6 +1345,7 @@ __device__ void seq_run(const PllCfg& cfg, const float* in, const int8_t* in8, d
   // inputs 16 at a time, one group ahead (a load per step would wait out the memory latency)
   constexpr int G = 16;
   float xa[G], xn[G];
+  Th32Line ln{0.0, 0.0};
   auto ld = [&](float (&v)[G], int64_t k0) {
 #pragma unroll
     for (int i = 0; i < G; ++i) v[i] = k0 + i < n ? (in8 != nullptr ? pll_decode(in8[k0 + i]) : in[k0 + i]) : 0.f;
@@ -1327,7 +1373,15 @@ __device__ void seq_run(const PllCfg& cfg, const float* in, const int8_t* in8, d
       }
       integ = integ + cfg.ki * e;
       phase = phase + cfg.kp * e + integ;
-      th[k] = phase;
+      if (lines != nullptr) {
+        if ((k & (TH32_LINE - 1)) == 0) {
+          ln = Th32Line{phase, integ};
+          lines[k / TH32_LINE] = ln;
+        }
+        r32[k] = th32_residual(ln, (int)(k & (TH32_LINE - 1)), phase);
+      } else {
+        th[k] = phase;
+      }
     }
 #pragma unroll
     for (int i = 0; i < G; ++i) xa[i] = xn[i];
@@ -1616,9 +1670,10 @@ __device__ void long_tail(const PllJobs& P, const int r, const int pos) {
     sincos_red<true>(reduce_2pi(arg), &s0[3], &s0[2]);
   }
   double so[6];
+  double* rowp = J.theta + (int64_t)s * J.th_stride;
   seq_run(cfg, J.in + (int64_t)s * J.in_stride + base,
-          J.in8 != nullptr ? J.in8 + (int64_t)s * J.in8_stride + base : nullptr, J.theta + (int64_t)s * J.th_stride + base,
-          P.n - base, s0, so);
+          J.in8 != nullptr ? J.in8 + (int64_t)s * J.in8_stride + base : nullptr, rowp + base, P.n - base, s0, so,
+          J.th32 ? th32_res(rowp) + base : nullptr, J.th32 ? th32_lines(rowp, P.n) + base / TH32_LINE : nullptr);
   for (int i = 0; i < 5; ++i) st[i] = so[i];
   st[5] = off0 + (double)P.n;
   H->pos = nb;
@@ -1651,9 +1706,11 @@ __global__ __launch_bounds__(CHAIN_T) void pll_long_fix_kernel(PllJobs P) {
       const int q = r / P.nstreams, s = r - q * P.nstreams;
       const PllJob& J = P.j[q];
       const int64_t base = (int64_t)pos * P.lg.pb;
+      double* rowp = J.theta + (int64_t)s * J.th_stride;
       seq_run(J.cfg, J.in + (int64_t)s * J.in_stride + base,
-              J.in8 != nullptr ? J.in8 + (int64_t)s * J.in8_stride + base : nullptr,
-              J.theta + (int64_t)s * J.th_stride + base, long_len(P, pos), B->x, B->e);
+              J.in8 != nullptr ? J.in8 + (int64_t)s * J.in8_stride + base : nullptr, rowp + base, long_len(P, pos),
+              B->x, B->e, J.th32 ? th32_res(rowp) + base : nullptr,
+              J.th32 ? th32_lines(rowp, P.n) + base / TH32_LINE : nullptr);
       B->u[0] = B->x[0];
       B->u[1] = B->x[1];
       B->d[0] = B->d[1] = 0.0;
@@ -1741,7 +1798,7 @@ __global__ __launch_bounds__(256) void nco_long_kernel(PllJobs P) {
 #pragma unroll
   for (int i = 0; i < NCO_NR; ++i) {
     const int64_t k = k0 + (int64_t)i * 256;
-    phv[i] = k < kend ? ph[k] : 0.0;
+    phv[i] = k < kend ? (J.th32 ? th32_stored(ph, P.n, k) : ph[k]) : 0.0;
   }
   float* oi = J.nco_i + (int64_t)s * J.out_stride + 1;
   float* oq = J.nco_q ? J.nco_q + (int64_t)s * J.out_stride + 1 : nullptr;
@@ -1802,6 +1859,7 @@ constexpr int LONG_PB = SPEC_NMAX - 1 - LONG_PRE_MAX;
 // loops, and the pre-roll exactly the first wave's chunks (r05 balanced the lengths, 14 299 at
 // a C5 span: the last wave ran its partial chunk's predicated loops and the workgroup's
 // barriers waited for it -- the phase timers' guess and check barriers)
+static_assert(TH32_LINES * TH32_LINE >= LONG_PB, "compact rows: a pseudo-block's lines fit the solve's table");
 void long_geom(int64_t n, int64_t* pb, int* nb) {
   const int64_t k = (n + LONG_PB - 1) / LONG_PB;
   *nb = (int)k;
@@ -1880,6 +1938,12 @@ hipError_t long_setup(PllJobs& L) {
     for (int i = 0; i < 4; ++i) { L.lg.phi[q][i] = f[i]; L.lg.phi_last[q][i] = g[i]; }
     L.lg.warm[q] = warm_len(c, L.lg.c1[q], L.lg.pb);
   }
+  return hipSuccess;
+}
+// compact phase rows (PllJob::th32): long calls whose pseudo-blocks start on a line only
+hipError_t th32_check(const PllJobs& L) {
+  for (int q = 0; q < L.njobs; ++q)
+    if (L.j[q].th32 && (!pll_long(L) || L.lg.pb % TH32_LINE != 0)) return hipErrorInvalidValue;
   return hipSuccess;
 }
 }  // namespace
@@ -2013,6 +2077,7 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     // long call: every pseudo-block solved (from warm-up guesses), then the chain with its repairs
     L.qform = 0;
     e = long_setup(L);
+    if (e == hipSuccess) e = th32_check(L);
     if (e == hipSuccess) e = qtab_fill(L);
     if (e != hipSuccess) return e;
     const int R = L.njobs * L.nstreams;
@@ -2020,6 +2085,7 @@ hipError_t sdr_launch_pll_loop(const PllJobs& P, hipStream_t st) {
     hipLaunchKernelGGL(pll_long_fix_kernel, dim3((unsigned)R), dim3(CHAIN_T), 0, st, L);
     return hipGetLastError();
   }
+  if (th32_check(P) != hipSuccess) return hipErrorInvalidValue;    // (compact rows: long calls only)
   if (spec_only(P)) {
     // one launch: every recurrence solved in parallel, or sequentially in its own workgroup
     // when the solve cannot complete it (lpw = 0 tells the kernel so)
@@ -2054,6 +2120,7 @@ hipError_t sdr_launch_pll_nco(const PllJobs& P, hipStream_t st) {
     e = long_setup(L);
     if (e != hipSuccess) return e;
   }
+  if (th32_check(L) != hipSuccess) return hipErrorInvalidValue;
   if (pll_long(P)) {
     if (!P.nco_rows) return hipSuccess;                // the consumer forms the NCO (sdr_nco.h)
     for (int q = 0; q < P.njobs; ++q)

@@ -122,7 +122,8 @@ __device__ __forceinline__ void nco_at(const NcoSrc& N, int s, int64_t k, float*
     return;
   }
   const NcoTile T = nco_tile(N, s, k - 1);
-  const double p = nco_tile_p(N, T, k - 1, T.th[k - 1]);
+  const double p = nco_tile_p(N, T, k - 1, N.th32 ? th32_stored(T.th, N.n, k - 1) : T.th[k - 1]);   // (compact rows: the
+                                                                                                     // stereo mixer's final states)
   ncof2 c2, s2;
   nco_f32x2(N, T.off, k, p, p, &c2, &s2);
   *c = c2.x;
@@ -996,7 +997,8 @@ constexpr int SM_NG = SM_LU / 4, SM_NQ = (SM_NG + 63) / 64;
 template <bool MIX> constexpr int sm_wpe() { return MIX ? 2 : 4; }   // waves per SIMD (registers; LDS: 4 x 39.7 KB)
 static_assert(SM_D * 15 + SM_KOFF < 32 * SM_KS && SM_KOFF >= 150 && SM_KOFF % 2 == 1, "LPF window");
 
-template <bool MIX>
+// TH32 (MIX): the pilot loop's phase rows are compact (sdr_nco.h, PllJob::th32)
+template <bool MIX, bool TH32 = false>
 __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(sm_wpe<MIX>()))) void rx_decmm_kernel(StageJobs P,
                                                                                                              int wgs) {
   const StageJob& J = P.j[0];                        // (in the kernel arguments: no private copy)
@@ -1057,7 +1059,7 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(sm_wpe<MI
   MixLd gb[PD];
   auto ldg = [&](const Win& v, int j, MixLd* gg) {
     const int64_t i0 = v.a + 4 * min(l + 64 * j, SM_NG - 1);
-    if constexpr (MIX) mix_load(J.nco, v.nt, v.x, i0, v.lin, gg);
+    if constexpr (MIX) mix_load<TH32>(J.nco, v.nt, v.x, i0, v.lin, gg);
     else __builtin_memcpy(&gg->x, v.x + (i0 > 0 ? i0 : (int64_t)0), sizeof(float4));
   };
   Win cur{}, nxt{};
@@ -1095,7 +1097,7 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(sm_wpe<MI
         float u[4];
         if constexpr (MIX) {
           float xv[4], c[4], sn[4];
-          mix_eval(cur.nt, nwin, i0, n, gc, cur.lin, c0, 0.f, xv, c, sn);
+          mix_eval<TH32>(cur.nt, nwin, i0, n, gc, cur.lin, c0, 0.f, xv, c, sn);
 #pragma unroll
           for (int e = 0; e < 4; ++e) u[e] = pre_op(PRE_NCO, xv[e], c[e], gain);
         } else {                                     // (the edges as mix_eval)
@@ -1222,7 +1224,8 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
       fe_done = true;
     }
     const unsigned grid = (unsigned)(wgs + Q.nzf * S + (Q.fe.on ? S : 0));
-    if (mix) hipLaunchKernelGGL(rx_decmm_kernel<true>, dim3(grid), dim3(RX_NT), 0, st, Q, wgs);
+    if (mix && j.nco.th32) hipLaunchKernelGGL((rx_decmm_kernel<true, true>), dim3(grid), dim3(RX_NT), 0, st, Q, wgs);
+    else if (mix) hipLaunchKernelGGL(rx_decmm_kernel<true>, dim3(grid), dim3(RX_NT), 0, st, Q, wgs);
     else hipLaunchKernelGGL(rx_decmm_kernel<false>, dim3(grid), dim3(RX_NT), 0, st, Q, wgs);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1292,6 +1295,8 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
     }
   for (const StageJob& j : jobs)                     // sign-code outputs: the matrix-core tiles only
     if (!j.mma && (j.y8 != nullptr || j.y == nullptr)) return hipErrorInvalidValue;
+  for (const StageJob& j : jobs)                     // compact phase rows: the matrix-core stereo mixer only
+    if (!j.mma && j.pre == PRE_NCO && j.nco.th32) return hipErrorInvalidValue;
   for (int key : {151, 101, 0}) {
     StageJobs P{};
     P.nstreams = S;
@@ -2327,6 +2332,18 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     int64_t pb = 0;
     int nb = 0;
     const bool lng = sdr_pll_long_geom(M, &pb, &nb);
+    // the pilot loop's phase rows in the compact form (sdr_nco.h, r06) when the matrix-core
+    // stereo mixer is their only reader (launch_stage's `mix` conditions; nco_long_kernel
+    // decodes them for a kept NCO row): half the bytes of the solve's stores and the mixer's loads
+    auto a16 = [](const void* p, int64_t stride) { return p != nullptr && ((uintptr_t)p % 16) == 0 && stride % 4 == 0; };
+#ifdef SDR_NO_TH32   // diagnostic builds only (tools/build_dbg.sh): the full rows, for an A/B of the outputs
+    const bool th32 = false;
+#else
+    const bool th32 = lng && pb % TH32_LINE == 0 && stx && tsl == 151 && r->audio_decim == 5 &&
+                      M >= (int64_t)MM_MIN_WIN * MM_WT && M % 4 == 0 && M < ((int64_t)1 << 28) &&
+                      o[SDR_RX_O_BPF_EXTRACTION] != nullptr && a16(o[SDR_RX_O_STEREO], as) &&
+                      a16(o[SDR_RX_O_AUDIO], as) && a16(o[SDR_RX_O_LEFT], as) && a16(o[SDR_RX_O_RIGHT], as);
+#endif
     auto add = [&](int k, const float* in, double* thk, float* ni, float* nq, double* pck) -> int {
       const double* resp = nullptr;
       TRY(get_resp(c, r->pll[k], M, &resp));
@@ -2338,6 +2355,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       }
       NcoSrc& N = nsrc[k];
       N.theta = M >= 2 ? thk : nullptr;   // (M < 2: the sequential kernels' Q-form rows; mix from the NCO rows)
+      if (k == 0 && th32) P.j[jq].th32 = N.th32 = 1;
       N.th_stride = r->ths;
       N.nco_i = ni;
       N.nco_q = nq;

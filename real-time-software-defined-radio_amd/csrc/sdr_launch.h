@@ -103,6 +103,8 @@ struct PllJob {
   const double* qtab;          // the solve's matrix powers (pll.hip qtab_host); set by the launcher
   const int8_t* in8;           // nullable: the input as sign codes (sdr_nco.h pll_code), in8_stride bytes
   int64_t in8_stride;          //   apart per stream; read instead of `in` (long calls, spec-only calls)
+  int th32;                    // long calls: the phase rows in the compact form (sdr_nco.h "compact
+                               //   phase rows"); set by the receiver for the pilot loop of a span
 };
 // Long calls (n > SDR_PLL_BLOCK_MAX samples): the recurrence is cut into nb pseudo-blocks of
 // pb samples, solved in parallel from warm-up guesses of their start states and chained

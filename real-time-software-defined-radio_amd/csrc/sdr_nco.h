@@ -112,6 +112,41 @@ __host__ __device__ inline const LongBlk* long_blk0(const void* work, int njobs,
          (int64_t)r * nb;
 }
 
+// ---- compact phase rows (r06: the pilot loop of a span, PllJob::th32) ----------------------
+// A long call's phase row in 4.5 B a step instead of 8: per line c of 32 rows (rows 32 c ..
+// 32 c + 31 of the stream's row; pseudo-blocks start on a line, pb = 0 mod 32) a line {a, s}
+// (f64) and per row an f32 residual r_k, with
+//   stored_k = fma(s, k - 32 c, a) + r_k.
+// The solve sets a line's (a, s) from the trajectory of its previous pass over the line's
+// first row (its start and its slope per step), so r_k is the loop's deviation from a straight
+// line over 32 steps -- <= 0.3 rad at acquisition, ~0.1 rad of detector jitter when locked (the
+// pilot loop, Kp = 0.027) -- and its f32 rounding <= 2e-8 rad (tools/th32_err.py, against the
+// NCO's 1e-7 check).  Inside the row's own allocation (th_stride >= n + 1 doubles): residuals at
+// bytes [0, 4 n), the lines from byte th32_lines_at(n) (<= 4.5 n + 32 <= 8 n: n > 16 385 for
+// every long call), the trigOffset slot th[n] (byte 8 n) unchanged.
+constexpr int TH32_LINE = 32;
+struct Th32Line { double a, s; };
+__host__ __device__ inline int64_t th32_lines_at(int64_t n) { return (4 * n + 15) / 16 * 16; }
+__device__ __forceinline__ float* th32_res(double* row) { return reinterpret_cast<float*>(row); }
+__device__ __forceinline__ const float* th32_res(const double* row) { return reinterpret_cast<const float*>(row); }
+__device__ __forceinline__ Th32Line* th32_lines(double* row, int64_t n) {
+  return reinterpret_cast<Th32Line*>(reinterpret_cast<char*>(row) + th32_lines_at(n));
+}
+__device__ __forceinline__ const Th32Line* th32_lines(const double* row, int64_t n) {
+  return reinterpret_cast<const Th32Line*>(reinterpret_cast<const char*>(row) + th32_lines_at(n));
+}
+// the residual of a stored phase against its line (the writers' one formula)
+__device__ __forceinline__ float th32_residual(const Th32Line& L, int o, double stored) {
+#pragma clang fp contract(off)
+  return (float)(stored - fma(L.s, (double)o, L.a));
+}
+// stored_k of a compact row of n steps
+__device__ __forceinline__ double th32_stored(const double* row, int64_t n, int64_t k) {
+#pragma clang fp contract(off)
+  const Th32Line L = th32_lines(row, n)[k >> 5];
+  return fma(L.s, (double)(int)(k & 31), L.a) + (double)th32_res(row)[k];
+}
+
 // Where one PLL job's NCO comes from, for every stream of a receiver block.
 struct NcoSrc {
   const double* theta;     // phase rows (th_stride apart); theta[n] = the call's trigOffset
@@ -128,6 +163,7 @@ struct NcoSrc {
   int nb;                  // pseudo-blocks of the call
   const double* resp;
   const float* resp32;     // the same table in f32 (the matrix-core mixers' response: an angle <= 0.15 rad)
+  int th32;                // the phase rows are compact (PllJob::th32): the matrix-core mixer's TH32 form only
 };
 
 // The recurrence's phaseEst for step kk of a long call's pseudo-block B whose solve stored
@@ -316,19 +352,31 @@ __device__ __forceinline__ void nco_f32x4(const NcoSrc& N, const NcoTile& T, int
 struct Nco4Ld {
   typedef double d2n __attribute__((ext_vector_type(2)));
   typedef float f2n __attribute__((ext_vector_type(2)));
-  d2n t01, t23;
+  d2n t01, t23;            // the four stored phases (TH32: t01 = the line {a, s}, t23 unused)
+  float4 r;                // TH32: the four residuals
   f2n rr[4];
 };
 __device__ __forceinline__ bool nco_tile_lin(const NcoTile& T) {
   return T.d0[0] != 0.0 || T.d1[0] != 0.0 || T.d0[1] != 0.0 || T.d1[1] != 0.0;
 }
-// (i odd: the four phases phaseEst_{i-1} .. phaseEst_{i+2} are two aligned pairs, t01 and t23)
+// (i odd: the four phases phaseEst_{i-1} .. phaseEst_{i+2} are two aligned pairs, t01 and t23;
+// TH32: rows i-1 .. i+2 are one 16-B run of residuals in one line -- i - 1 = 0 mod 4 -- and the
+// line is 16 B)
+template <bool TH32 = false>
 __device__ __forceinline__ void nco4_load(const NcoSrc& N, const NcoTile& T, int64_t i, bool lin, Nco4Ld* L) {
   typedef Nco4Ld::d2n d2n;
   typedef Nco4Ld::f2n f2n;
-  const double* th = T.th + i - 1;
-  L->t01 = *reinterpret_cast<const d2n*>(th);
-  L->t23 = *reinterpret_cast<const d2n*>(th + 2);
+  if constexpr (TH32) {
+    // (clamped into the row: a chunk wholly past its end -- a window's tail, its inputs 0 --
+    // must still form a finite angle, and past the residuals lie the lines)
+    const int64_t j0 = min(i - 1, N.n - 4);
+    L->r = *reinterpret_cast<const float4*>(th32_res(T.th) + j0);
+    L->t01 = *reinterpret_cast<const d2n*>(th32_lines(T.th, N.n) + (j0 >> 5));
+  } else {
+    const double* th = T.th + i - 1;
+    L->t01 = *reinterpret_cast<const d2n*>(th);
+    L->t23 = *reinterpret_cast<const d2n*>(th + 2);
+  }
   if (lin) {
     // the four steps' rows are consecutive from the chunk's first step's block base: a chunk
     // that crosses into the next pseudo-block reads that block's first rows from the table's
@@ -382,6 +430,7 @@ __device__ __forceinline__ NcoWin nco_win(const NcoSrc& N, const NcoTile& T, int
   return W;
 }
 // cos / sin (f32) of outputs i .. i+3 (i odd: L from nco4_load) from the window's angle base
+template <bool TH32 = false>
 __device__ __forceinline__ void nco4_eval_w(const NcoTile& T, const NcoWin& W, int64_t i, const Nco4Ld& L, bool lin,
                                             float (&c)[4], float (&sn)[4]) {
 #pragma clang fp contract(off)
@@ -389,6 +438,18 @@ __device__ __forceinline__ void nco4_eval_w(const NcoTile& T, const NcoWin& W, i
   constexpr double Q1 = 1.5707963705062866, Q2 = -4.3711390001862426e-08;   // 2-part pi/2 (|n| < 2^29)
   const double st[4] = {L.t01.x, L.t01.y, L.t23.x, L.t23.y};   // phaseEst_{i-1} .. phaseEst_{i+2} (stored)
   const int dk = (int)(i - W.kw);
+  // TH32: stored_{i-1+e} = a + s (o + e) + r_e (o: row i - 1 within its line; the group never
+  // crosses a line or a pseudo-block, pb = 0 mod 32), folded per group into
+  //   angle = G + (ws + scale s) (dk + e) + scale r_e,  G = base_h + scale (a + s (o - dk))
+  // -- 3 f64 operations a sample, as the full rows' 2 plus the residual's conversion
+  const float rv[4] = {L.r.x, L.r.y, L.r.z, L.r.w};
+  double G = 0.0, W2 = 0.0;
+  if constexpr (TH32) {
+    const bool h0 = i - 1 >= T.bound;
+    const int o = (int)((i - 1) & 31);
+    W2 = fma(W.scale, L.t01.y, W.ws);
+    G = fma(W.scale, fma(L.t01.y, (double)(o - dk), L.t01.x), h0 ? W.base[1] : W.base[0]);
+  }
   float y[4];
   int q[4];
 #pragma unroll
@@ -398,7 +459,9 @@ __device__ __forceinline__ void nco4_eval_w(const NcoTile& T, const NcoWin& W, i
     // (r06: the base of output i + e in one fma, and the linear response -- an angle of at most
     // 0.3 scale rad -- in f32 (its rounding ~1e-8 rad, below the f32 cos / sin): 7 f64
     // operations a sample instead of 10)
-    double a = fma(st[e], W.scale, fma(W.ws, (double)(dk + e), h ? W.base[1] : W.base[0]));
+    double a;
+    if constexpr (TH32) a = fma((double)rv[e], W.scale, fma(W2, (double)(dk + e), G));
+    else a = fma(st[e], W.scale, fma(W.ws, (double)(dk + e), h ? W.base[1] : W.base[0]));
     if (lin) a = a + (double)fmaf(L.rr[e].x, h ? W.sd0[1] : W.sd0[0], L.rr[e].y * (h ? W.sd1[1] : W.sd1[0]));
     const double n = rint(a * k2oPi);
     double r = fma(-n, Q1, a);
@@ -421,15 +484,17 @@ struct MixLd {
 };
 // (lin: whether to read the response rows -- true always for the RDS loop, whose blocks all
 // carry one; the pilot loop's rarely do, and a uniform branch then costs little)
+template <bool TH32 = false>
 __device__ __forceinline__ void mix_load(const NcoSrc& N, const NcoTile& T, const float* xr, int64_t i0, bool lin,
                                          MixLd* L) {
   __builtin_memcpy(&L->x, xr + (i0 > 0 ? i0 : (int64_t)0), sizeof(float4));   // (4-B aligned)
-  nco4_load(N, T, i0 > 1 ? i0 : (int64_t)1, lin, &L->t);
+  nco4_load<TH32>(N, T, i0 > 1 ? i0 : (int64_t)1, lin, &L->t);
 }
 // the chunk's inputs (0 outside [0, n)) and cos / sin (NCO[0]: the carried c0 / s0)
+template <bool TH32 = false>
 __device__ __forceinline__ void mix_eval(const NcoTile& T, const NcoWin& W, int64_t i0, int64_t n, const MixLd& L,
                                          bool lin, float c0, float s0, float (&xv)[4], float (&c)[4], float (&sn)[4]) {
-  nco4_eval_w(T, W, i0, L.t, lin, c, sn);
+  nco4_eval_w<TH32>(T, W, i0, L.t, lin, c, sn);
   // per chunk, not per sample: i0 = -3 (only x[0], with NCO[0]), i0 = n - 3 (the last three),
   // wholly outside the row, or interior
   const bool head = i0 == -3, tail = i0 == n - 3, out = (i0 < 0 && !head) || i0 >= n;

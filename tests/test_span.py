@@ -43,8 +43,12 @@ FLIP_SPAN, FLIP_REL, FLIP_MAX = 3, 1.5e-2, 3
 FLIP_NEAR = {"bpf_recovery": 2e-6, "pre_pll": 5e-6}
 FLIP_DEPS = {"bpf_recovery": ("nco", "stereo", "left", "right"),
              "pre_pll": ("nco_i", "nco_q", "lpf_i", "lpf_q", "resample_i", "resample_q", "rrc_i", "rrc_q")}
-# the device's NCO rows against the oracle's fmPll run on the device's own loop inputs
-NCO_REPLAY = 1e-7
+# the device's NCO rows against the oracle's fmPll run on the device's own loop inputs: the f32
+# rounding of the NCO value (<= 6e-8) plus, for the pilot loop's compact phase rows (sdr_nco.h,
+# r06), the f32 rounding of a row's residual against its 32-step line -- <= 5e-8 rad while the
+# loop acquires (|residual| up to ~0.3 rad, tools/th32_err.py), ~1e-8 once locked.  Measured:
+# 1.11e-7 in block 0 of seed 70 (the acquisition), 3e-8 in the locked blocks.
+NCO_REPLAY = 1.5e-7
 
 
 def _flips(src, got, want):
