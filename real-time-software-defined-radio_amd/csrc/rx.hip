@@ -1295,8 +1295,6 @@ hipError_t launch_stage(std::vector<StageJob> jobs, int S, hipStream_t st, const
     }
   for (const StageJob& j : jobs)                     // sign-code outputs: the matrix-core tiles only
     if (!j.mma && (j.y8 != nullptr || j.y == nullptr)) return hipErrorInvalidValue;
-  for (const StageJob& j : jobs)                     // compact phase rows: the matrix-core stereo mixer only
-    if (!j.mma && j.pre == PRE_NCO && j.nco.th32) return hipErrorInvalidValue;
   for (int key : {151, 101, 0}) {
     StageJobs P{};
     P.nstreams = S;
@@ -1645,6 +1643,7 @@ __host__ __device__ constexpr int cm_fi(int rt, int st) { return (rt == 0 ? 0 : 
 constexpr int CM_NF = cm_st1(0) - cm_st0(0) + cm_st1(1) - cm_st0(1);
 static_assert(cm_st1(1) <= CM_KS && CM_NF == 13, "row tiles' K steps");
 
+template <bool TH32 = false>   // TH32: the RDS loop's phase rows are compact (sdr_nco.h, PllJob::th32)
 __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(2))) void rx_cresmm_kernel(CresJob J,
                                                                                                const float* amat, int wgs) {
   __shared__ __attribute__((aligned(16))) _Float16 img[4][4 * CM_LU];   // per wave: I hi, I lo, Q hi, Q lo
@@ -1697,7 +1696,7 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(2))) void
   static_assert(CM_NQ % PD == 0, "ring slots line up across windows");
   MixLd gb[PD];
   auto ldg = [&](const Win& v, int j, MixLd* gg) {
-    mix_load(J.nco, v.nt, v.x, v.a + 4 * min(l + 64 * j, CM_NG - 1), true, gg);
+    mix_load<TH32>(J.nco, v.nt, v.x, v.a + 4 * min(l + 64 * j, CM_NG - 1), true, gg);
   };
   Win cur{}, nxt{};
   if (gw < total) {
@@ -1720,7 +1719,7 @@ __global__ __launch_bounds__(RX_NT) __attribute__((amdgpu_waves_per_eu(2))) void
         if constexpr (j + PD < CM_NQ) ldg(cur, j + PD, &gb[j % PD]);
         else ldg(more ? nxt : cur, j + PD - CM_NQ, &gb[j % PD]);
         float xv[4], c[4], sn[4];
-        mix_eval(cur.nt, nwin, a + 4 * q, n, gc, lin, c0, s0, xv, c, sn);
+        mix_eval<TH32>(cur.nt, nwin, a + 4 * q, n, gc, lin, c0, s0, xv, c, sn);
         h4v hv, lv;
         mm_split4(make_float4(xv[0] * c[0], xv[1] * c[1], xv[2] * c[2], xv[3] * c[3]), &hv, &lv);
         *reinterpret_cast<h4v*>(Ih + 4 * q) = hv;
@@ -2332,17 +2331,15 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
     int64_t pb = 0;
     int nb = 0;
     const bool lng = sdr_pll_long_geom(M, &pb, &nb);
-    // the pilot loop's phase rows in the compact form (sdr_nco.h, r06) when the matrix-core
-    // stereo mixer is their only reader (launch_stage's `mix` conditions; nco_long_kernel
-    // decodes them for a kept NCO row): half the bytes of the solve's stores and the mixer's loads
-    auto a16 = [](const void* p, int64_t stride) { return p != nullptr && ((uintptr_t)p % 16) == 0 && stride % 4 == 0; };
+    // the loops' phase rows in the compact form (sdr_nco.h, r06): half the bytes of the solve's
+    // stores and of the mixers' loads.  Every reader decodes them -- the matrix-core mixers
+    // (TH32 forms), the VALU tiles and final states (nco_f32x4, nco_at), the NCO kernel -- so
+    // the form depends only on the call's geometry (pseudo-blocks on a line), never on what a
+    // block keeps
 #ifdef SDR_NO_TH32   // diagnostic builds only (tools/build_dbg.sh): the full rows, for an A/B of the outputs
-    const bool th32 = false;
+    const bool th32 = false, th32r = false;
 #else
-    const bool th32 = lng && pb % TH32_LINE == 0 && stx && tsl == 151 && r->audio_decim == 5 &&
-                      M >= (int64_t)MM_MIN_WIN * MM_WT && M % 4 == 0 && M < ((int64_t)1 << 28) &&
-                      o[SDR_RX_O_BPF_EXTRACTION] != nullptr && a16(o[SDR_RX_O_STEREO], as) &&
-                      a16(o[SDR_RX_O_AUDIO], as) && a16(o[SDR_RX_O_LEFT], as) && a16(o[SDR_RX_O_RIGHT], as);
+    const bool th32 = lng && pb % TH32_LINE == 0 && stx, th32r = lng && pb % TH32_LINE == 0 && rd;
 #endif
     auto add = [&](int k, const float* in, double* thk, float* ni, float* nq, double* pck) -> int {
       const double* resp = nullptr;
@@ -2355,7 +2352,7 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       }
       NcoSrc& N = nsrc[k];
       N.theta = M >= 2 ? thk : nullptr;   // (M < 2: the sequential kernels' Q-form rows; mix from the NCO rows)
-      if (k == 0 && th32) P.j[jq].th32 = N.th32 = 1;
+      if ((k == 0 && th32) || (k == 1 && th32r)) P.j[jq].th32 = N.th32 = 1;
       N.th_stride = r->ths;
       N.nco_i = ni;
       N.nco_q = nq;
@@ -2465,7 +2462,10 @@ int sdr_rx_process_dev(sdr_rx* r, const void* iq, int64_t iq_stride) {
       if (M >= (int64_t)MM_MIN_WIN * MM_WT && M % 4 == 0 && J.nco.theta != nullptr) {
         const int64_t wins = ceil_div(r->R, CM_WO) * S;
         const int wgs = (int)std::min<int64_t>(CM_WGS, ceil_div(wins, 4));
-        hipLaunchKernelGGL(rx_cresmm_kernel, dim3((unsigned)(S + wgs)), dim3(RX_NT), 0, st, J, r->ctaps + CR_NTAPS, wgs);
+        if (J.nco.th32)
+          hipLaunchKernelGGL(rx_cresmm_kernel<true>, dim3((unsigned)(S + wgs)), dim3(RX_NT), 0, st, J, r->ctaps + CR_NTAPS, wgs);
+        else
+          hipLaunchKernelGGL(rx_cresmm_kernel<false>, dim3((unsigned)(S + wgs)), dim3(RX_NT), 0, st, J, r->ctaps + CR_NTAPS, wgs);
       } else {
         hipLaunchKernelGGL(rx_cres_kernel, dim3((unsigned)grid), dim3(CR_NT), 0, st, J);
       }

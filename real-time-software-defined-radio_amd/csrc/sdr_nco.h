@@ -312,10 +312,16 @@ __device__ __forceinline__ void nco_f32x2(const NcoSrc& N, double off, int64_t k
 __device__ __forceinline__ void nco_f32x4(const NcoSrc& N, const NcoTile& T, int64_t i, float (&c)[4], float (&sn)[4]) {
 #pragma clang fp contract(off)
   typedef double d2n __attribute__((ext_vector_type(2)));
-  const double* th = T.th + i - 2;
-  const d2n t01 = *reinterpret_cast<const d2n*>(th), t23 = *reinterpret_cast<const d2n*>(th + 2),
-            t45 = *reinterpret_cast<const d2n*>(th + 4);
-  const double st[4] = {t01.y, t23.x, t23.y, t45.x};       // phaseEst_{i-1} .. phaseEst_{i+2}
+  double st[4];                                            // phaseEst_{i-1} .. phaseEst_{i+2}
+  if (N.th32) {                                            // (compact rows, sdr_nco.h: kept RDS LPF rows)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) st[e] = th32_stored(T.th, N.n, i - 1 + e);
+  } else {
+    const double* th = T.th + i - 2;
+    const d2n t01 = *reinterpret_cast<const d2n*>(th), t23 = *reinterpret_cast<const d2n*>(th + 2),
+              t45 = *reinterpret_cast<const d2n*>(th + 4);
+    st[0] = t01.y; st[1] = t23.x; st[2] = t23.y; st[3] = t45.x;
+  }
   double p[4];
   bool lin = false;
   double d0[4], d1[4];
