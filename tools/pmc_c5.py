@@ -13,11 +13,13 @@ SQ_ACTIVE_INST_VALU (quad-cycles of vector issue), SQ_VALU_MFMA_BUSY_CYCLES (mat
 
 The stages are the receiver's timing stages (csrc/rx.hip, sdr_rx_stage_ms):
   fe                fe_mfma_demod_kernel<151>
-  filters_of_demod  rx_mma_kernel<151, 3> (pilot, stereo, RDS-extract BPFs) + rx_decmm_kernel<false> (audio LPF)
+  filters_of_demod  rx_mma_kernel<151, 3> (pilot, stereo, RDS-extract BPFs) + rx_decmm_kernel<false, false> (audio LPF)
   rds_square        the first rx_mma_kernel<151, 1> dispatch of a span call (x^2 + BPF)
   pll               pll_spec_kernel<512, true> + pll_long_fix_kernel
-  mix_lpf           rx_decmm_kernel<true> (stereo mixer + LPF + L/R, its NCO formed from the PLL phases)
-  resample          rx_cresmm_kernel (RDS I/Q mixers + LPF + x19/80 resampler, composite)
+  mix_lpf           rx_decmm_kernel<true, true> (stereo mixer + LPF + L/R, its NCO formed from the PLL's compact phase rows)
+  resample          rx_cresmm_kernel<true> (RDS I/Q mixers + LPF + x19/80 resampler, composite; compact rows)
+(round-6 closing passes before the compact rows: rx_decmm_kernel<false> / <true>, rx_cresmm_kernel --
+the names are matched by ALIASES)
   rrc               the second rx_mma_kernel<151, 1> dispatch of a span call (RRC I/Q)
 Values are medians over the dispatches of a kernel (its span calls), summed over a stage's kernels."""
 import csv
@@ -29,13 +31,15 @@ from collections import defaultdict
 
 STAGES = {
     "fe": ["fe_mfma_demod_kernel<151>"],
-    "filters_of_demod": ["rx_mma_kernel<151, 3>", "rx_decmm_kernel<false>"],
+    "filters_of_demod": ["rx_mma_kernel<151, 3>", "rx_decmm_kernel<false, false>"],
     "rds_square": ["rx_mma_kernel<151, 1>#0"],
     "pll": ["pll_spec_kernel<512, true>", "pll_long_fix_kernel"],
-    "mix_lpf": ["rx_decmm_kernel<true>"],
-    "resample": ["rx_cresmm_kernel"],
+    "mix_lpf": ["rx_decmm_kernel<true, true>"],
+    "resample": ["rx_cresmm_kernel<true>"],
     "rrc": ["rx_mma_kernel<151, 1>#1"],
 }
+ALIASES = {"rx_decmm_kernel<false>": "rx_decmm_kernel<false, false>", "rx_decmm_kernel<true>": "rx_decmm_kernel<true, true>",
+           "rx_cresmm_kernel": "rx_cresmm_kernel<true>"}
 TWO_PER_CALL = "rx_mma_kernel<151, 1>"      # rds_square, then rrc, in every span call's launch order
 
 
@@ -54,7 +58,7 @@ def load(d):
     with open(path) as fh:
         for r in csv.DictReader(fh):
             e = rows[int(r["Dispatch_Id"])]
-            e["name"] = short(r["Kernel_Name"])
+            e["name"] = ALIASES.get(short(r["Kernel_Name"]), short(r["Kernel_Name"]))
             e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     return rows
 
