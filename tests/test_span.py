@@ -413,6 +413,36 @@ def test_span_c5_timed_shape_eight_streams(sdr, gpu_ctx, oracle):
         del mono, rds
 
 
+def test_span_mixers_equal_their_nco_rows(sdr, gpu_ctx, oracle):
+    """The span's mixers form their NCO from the PLL's compact phase rows (sdr_nco.h, r06) --
+    the stereo mixer on the matrix cores, the kept RDS LPF rows on the VALU tiles -- instead of
+    reading NCO rows.  Pinned against the NCO rows the NCO kernel writes from the same phases
+    (materialised here): the reference's mixer + LPF statements (model/fmMonoBlock.py:155-162,
+    model/fmRDSblock.py:173-182) run on the host over those rows and the device's own mixer
+    inputs reproduce the device's stereo and RDS LPF rows."""
+    K = 4
+    iq = sdr.synth.fm_iq(K * B5 + 1, seed=71, dtype=np.uint8)[None, :]
+    rx = sdr.Receiver(1, K * B5, stereo=True, rds=True, iq_dtype=np.uint8)
+    names = ["nco", "bpf_extraction", "stereo", "nco_i", "nco_q", "extract", "lpf_i", "lpf_q"]
+    got = rx.process(iq[:, :2 * K * B5], fetch=names)
+    g = {k: np.asarray(got[k][0], dtype=np.float64) for k in names}
+    n = len(g["bpf_extraction"])
+    _, _, st_b = oracle.stereo_coeffs(151)
+    lpf = oracle.rds_coeffs(151)["lpf"]
+    stereo, _ = oracle.lfilter_decim(st_b, g["nco"][:n] * g["bpf_extraction"] * 2, np.zeros(150), 5)
+    lpf_i, _ = oracle.lfilter_fir(lpf, g["extract"] * g["nco_i"][:n] * 2, np.zeros(150))
+    lpf_q, _ = oracle.lfilter_fir(lpf, g["extract"] * g["nco_q"][:n] * 2, np.zeros(150))
+    errs = {}
+    for name, want in (("stereo", stereo), ("lpf_i", lpf_i), ("lpf_q", lpf_q)):
+        assert g[name].shape == want.shape, name
+        errs[name] = maxabs(g[name], want) / max(float(np.max(np.abs(want))), 1e-3)
+    print("mixers vs their NCO rows, max error relative to peak:", {k: f"{v:.1e}" for k, v in errs.items()})
+    # (measured 2.9e-7 / 4.3e-7 / 2.0e-7: the mixers' f32 cos / sin against the rows' f64 ones
+    # rounded to f32, and f32 mixing against the host's f64)
+    for name, tol in (("stereo", 1e-6), ("lpf_i", 2e-6), ("lpf_q", 1e-6)):
+        assert errs[name] < tol, (name, errs[name])
+
+
 @pytest.mark.parametrize("K", [1, 4])
 def test_keep_lean_equals_full(sdr, gpu_ctx, K):
     """sdr_rx_set_keep without the NCO and RDS LPF rows (the bench's receivers): every output
