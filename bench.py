@@ -486,7 +486,9 @@ def main():
         del d_iq, d_dm, d_au
         cpu = ws == 1 and not args.no_cpu and rank == 0
         extras = {
-            "c5": c5_measure(ctx, 8, 256, 5, 2, rank, ws, cpu=cpu, args=args),
+            # (the standalone --workload c5 line's 10 timed spans after 10 warm-up spans: the
+            # same measurement; r06 ran 5 after 2, ~8 % below the standalone line on one box)
+            "c5": c5_measure(ctx, 8, 256, 10, 10, rank, ws, cpu=cpu, args=args),
             "c5_1stream": c5_measure(ctx, 1, 256, 10, 2, rank, ws),
             "u8": u8_measure(ctx, 128, 50, 10, rank),
             # configs[2] / [3] at fmMonoBlock.py's 51 200-sample blocks: the per-block drop-in path

@@ -641,6 +641,9 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   double* rowp = J.theta + (int64_t)s * J.th_stride;   // the stream's row (compact: residuals, then lines)
   const int64_t rb = base + pre;                        // the pseudo-block's first row
 #ifdef SDR_PLL_SPEC_PROF    // phase timers (diagnostic builds only, tools/build_dbg.sh)
+#ifndef SDR_PLL_SPEC_PROF_TID
+#define SDR_PLL_SPEC_PROF_TID 0   // the thread whose timers print (-D...=448: wave 7, a storing wave)
+#endif
   long long tp[16];
   int ntp = 0;
   tp[ntp++] = clock64();
@@ -1109,7 +1112,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     const int nmiss = __syncthreads_count(miss);
     SPEC_TP();
 #ifdef SDR_PLL_SPEC_PROF
-    if (tid == 0 && nmiss == 0 && (bid == 0 || (bid % 479) == 3))
+    if (tid == SDR_PLL_SPEC_PROF_TID && nmiss == 0 && (bid == 0 || (bid % 479) == 3))
       printf("spec_prof blk %d L %d: stage %lld corrloop %lld corrscan %lld warm %lld guessloop %lld guesssync %lld "
              "qpow %lld wscan %lld xscan %lld ystart %lld checkloop %lld checksync %lld (%d marks)\n", bid, L,
              tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], tp[6] - tp[5], tp[7] - tp[6],
