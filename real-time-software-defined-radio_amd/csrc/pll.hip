@@ -1029,8 +1029,16 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     // integer min / max order them; the margin is min(lo, 1 - hi))
     unsigned mlo = 0x3f800000u, mhi = 0u;
     // PO (a wave of pre-roll chunks only, F too): no phases to store, no wrap margins of its own
-    auto check = [&](auto FC, auto POC) __attribute__((always_inline)) {
-      constexpr bool F = decltype(FC)::value, PO = decltype(POC)::value;
+    // AF (compact rows, a32 wave of full chunks after a pre-roll of 1 mod 32 steps: each chunk
+    // is exactly its own line): the residuals against the chunk's own start, a flat line {vp, 0}
+    // -- one subtraction a step from a value the check holds anyway, no line lookup per store.
+    // (Such chunks follow the loop's acquisition, which the first pseudo-block of a stream
+    // holds: a locked loop moves ~0.1 rad in 32 steps, f32 rounding ~6e-9 rad; a loop drifting
+    // 1 rad in 32 steps still rounds to 6e-8.)
+    auto check = [&](auto FC, auto POC, auto AC) __attribute__((always_inline)) {
+      constexpr bool F = decltype(FC)::value, PO = decltype(POC)::value, AF = decltype(AC)::value;
+      if constexpr (AF)   // (its line: the pseudo-block's line tid - (pre >> 5), pre = 1 mod 32 and L = 32)
+        th32_lines(rowp, P.n)[(rb >> 5) + tid - (pre >> 5)] = Th32Line{xs_p, 0.0};
       double kd = off + (double)k0;
       for (int i0 = 0; i0 < L; i0 += SB) {
         int cd[SB / 2];                          // (half a batch of codes at a time: registers)
@@ -1070,7 +1078,8 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
             mhi = max(mhi, own ? fb : 0u);
           }
           if (act) mrel[tid * MSTR + i] = r;
-          if constexpr (!PO) tw[u * TBS + lane] = thval(p, k0 + i);
+          if constexpr (AF) tw[u * TBS + lane] = p - xs_p;
+          else if constexpr (!PO) tw[u * TBS + lane] = thval(p, k0 + i);
         }
         if constexpr (PO) continue;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1083,7 +1092,9 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
           const int k = 1 + (wv * 64 + ch) * L + i0 + u;
           const double v = tw[u * TBS + ch];
           const bool keep = F || (k >= pre && k < (int)n);
-          if (t32) {                                     // (uniform) its residual against its line
+          if constexpr (AF) {
+            th32_res(rowp)[rb + (k - pre)] = (float)v;   // (F: every step kept)
+          } else if (t32) {                              // (uniform) its residual against its line
             const int kk = k - pre;
             const Th32Line ln = tl[min(max(kk, 0) / TH32_LINE, TH32_LINES - 1)];
             const float rv = th32_residual(ln, kk & (TH32_LINE - 1), v);
@@ -1097,9 +1108,20 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     };
-    if (wfast) check(std::true_type{}, std::false_type{});
-    else if (wpre) check(std::true_type{}, std::true_type{});
-    else check(std::false_type{}, std::false_type{});
+    if constexpr (LONG) {
+      // (three forms, so the solve stays within its registers: a long call's full waves are
+      // AF when their pseudo-block allows it -- every middle pseudo-block of a span -- and take
+      // the general form otherwise: its first and last pseudo-blocks, repairs, calls without
+      // compact rows)
+      if (wfast && t32 && L == TH32_LINE && (pre & (TH32_LINE - 1)) == 1)
+        check(std::true_type{}, std::false_type{}, std::true_type{});
+      else if (wpre) check(std::true_type{}, std::true_type{}, std::false_type{});
+      else check(std::false_type{}, std::false_type{}, std::false_type{});
+    } else {
+      if (wfast) check(std::true_type{}, std::false_type{}, std::false_type{});
+      else if (wpre) check(std::true_type{}, std::true_type{}, std::false_type{});
+      else check(std::false_type{}, std::false_type{}, std::false_type{});
+    }
     SPEC_TP();
     float mth = fminf(__uint_as_float(mlo), 1.f - __uint_as_float(mhi));
     xe_p = p;

@@ -29,18 +29,32 @@ def parse(path):
     return rows
 
 
+# Kernels allowed a bounded spill, each with the measurement that justifies it ("Build
+# gate").  Only kernels without counted waits may appear here -- never the FE kernels.
+ALLOW = {
+    # the long-call solve: 20 B/lane -- three loop-invariant values stored before the round loop,
+    # reloaded once a round (a pseudo-block solves in one round when locked); the AF check form
+    # that costs them took the PLL stage 0.301-0.305 -> 0.283-0.290 ms (profiles/r06/close2/af/)
+    "_ZN12_GLOBAL__N_115pll_spec_kernelILi512ELb1EEEv7PllJobs": 20,
+}
+
+
 def main(paths):
     rows = [r for p in paths for r in parse(p)]
     if not rows:
         print("kres_gate: no kernel resource remarks found", file=sys.stderr)
         return 1
-    bad = [r for r in rows if r.get("ScratchSize", "0") != "0" or r.get("Dynamic", "False") not in ("False", "0")]
+
+    def over(r):
+        return int(r.get("ScratchSize", "0")) > ALLOW.get(r["name"], 0)
+    bad = [r for r in rows if over(r) or r.get("Dynamic", "False") not in ("False", "0")]
     for r in bad:
         print(f"kres_gate: {r['name']} ({r['file']}): scratch {r.get('ScratchSize')} B/lane, "
               f"dynamic stack {r.get('Dynamic')}", file=sys.stderr)
     if bad:
         return 1
-    print(f"kres_gate: {len(rows)} kernels, no scratch")
+    allowed = [f"{r['name']} {r.get('ScratchSize')} B" for r in rows if r.get("ScratchSize", "0") != "0"]
+    print(f"kres_gate: {len(rows)} kernels, no scratch" + (f" but the allowed {allowed}" if allowed else ""))
     return 0
 
 
