@@ -502,6 +502,23 @@ __device__ __forceinline__ double wave_prefix_sum(double v, int lane) {   // inc
   return v;
 }
 
+// DPP moves for the wave scans (r06: instead of ds_bpermute shuffles, ~100+ cycles each in a
+// dependent chain): lanes whose source lies outside the pattern, or in rows ROWS leaves out,
+// keep `old`.  CTRL: row_shr:n = 0x110 + n (within rows of 16), row_bcast:15 = 0x142 (lane 15
+// of rows 0 / 2 into rows 1 / 3 with ROWS = 0xa), row_bcast:31 = 0x143 (lane 31 into rows 2, 3
+// with ROWS = 0xc), wave_shr:1 = 0x138.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp_f32(float old, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROWS, 0xf, false));
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ double dpp_f64(double old, double v) {
+  const long long o = __double_as_longlong(old), x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)x, CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(x >> 32), CTRL, ROWS, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // a wave-uniform f64 held in SGPRs (readfirstlane of both halves): the compiler computes
 // uniform f64 values on the VALU and would otherwise keep them in VGPRs
 __device__ __forceinline__ double sgpr_d(double x) {
@@ -640,6 +657,15 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   }
   double* rowp = J.theta + (int64_t)s * J.th_stride;   // the stream's row (compact: residuals, then lines)
   const int64_t rb = base + pre;                        // the pseudo-block's first row
+  // the row's lines, formed once here and held in SGPRs (readfirstlane: otherwise the compiler
+  // reloads the call's length from the kernel arguments where the solve first needs it -- a
+  // scalar load and an lgkmcnt(0) wait after the guess barrier)
+  Th32Line* lrow = nullptr;
+  if (t32) {
+    const uintptr_t a = (uintptr_t)th32_lines(rowp, P.n);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    lrow = reinterpret_cast<Th32Line*>(((uintptr_t)hi << 32) | lo);
+  }
 #ifdef SDR_PLL_SPEC_PROF    // phase timers (diagnostic builds only, tools/build_dbg.sh)
 #ifndef SDR_PLL_SPEC_PROF_TID
 #define SDR_PLL_SPEC_PROF_TID 0   // the thread whose timers print (-D...=448: wave 7, a storing wave)
@@ -823,13 +849,15 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       d = ang - angp;
       d -= 6.28318548f * rintf(d * 0.159154937f);
     }
-    // inclusive prefix sum of the differences: within each wave by shuffles, then the waves'
-    // totals
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const float u = __shfl_up(d, o, 64);
-      if (lane >= o) d += u;
-    }
+    // inclusive prefix sum of the differences: within each wave by DPP moves (within rows of
+    // 16, then rows 1 / 3 from lane 15 of rows 0 / 2, then rows 2, 3 from lane 31), then the
+    // waves' totals
+    d += dpp_f32<0x111>(0.f, d);
+    d += dpp_f32<0x112>(0.f, d);
+    d += dpp_f32<0x114>(0.f, d);
+    d += dpp_f32<0x118>(0.f, d);
+    d += dpp_f32<0x142, 0xa>(0.f, d);
+    d += dpp_f32<0x143, 0xc>(0.f, d);
     if (lane == 63) wsum[wv].x = (double)d;
     __syncthreads();
     double D = (double)d;
@@ -947,7 +975,6 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
   }
   if (__syncthreads_or(bad)) return false;       // a 0 / NaN input (the general form's case)
   SPEC_TP();
-  SPEC_TP();                                     // (the phase timers' slot of the r05 Q-power phase)
   // Q = A^L's powers from the job's table (qtab_host, built once per loop on the host, staged in
   // LDS with the sign codes): Q^(2^i) for the scan's offsets, Q^(lane+1) and Q^tid = Q^(64 w)
   // Q^lane for the chunk starts -- r06: instead of thread 0 forming them (A^L step by step, then
@@ -969,9 +996,10 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
         const double sl = (xe_p - xs_p) / (double)len;
         const Th32Line ln{fma(sl, (double)(kk + pre - (k0 - 1)), xs_p), sl};
         tl[kk / TH32_LINE] = ln;
-        th32_lines(rowp, P.n)[(rb + kk) / TH32_LINE] = ln;
+        lrow[(rb + kk) / TH32_LINE] = ln;
       }
     }
+    SPEC_TP();                                   // (the phase timers: the compact rows' lines)
     // 2. solve: the chunk's response from zero state to the current integers, from the last
     // pass over it (the guess in round 0, the previous check after): z_j = x_end - Q x_start
     double zp, zv;
@@ -987,18 +1015,24 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     const Mat2 Ql = QT[lane + 1], Qj = mmul(QT[65 + wv], QT[lane]);   // Q^(lane+1), Q^tid
     double yp = tid < TE ? zp : 0.0, yv = tid < TE ? zv : 0.0;
     double cp = 0.0, cv = 0.0;                   // Y at the end of the previous wave
+    SPEC_TP();                                   // (the phase timers: z and the Q powers)
     {
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const int o = 1 << i;
-        const double up = __shfl_up(yp, o, 64), uv = __shfl_up(yv, o, 64);
-        if (lane >= o) {
-          const Mat2 Qo = qp(i);
-          yp = yp + (Qo.a * up + Qo.b * uv);
-          yv = yv + (Qo.c * up + Qo.d * uv);
-        }
-      }
+      // (r06: DPP moves -- offsets 1, 2, 4, 8 within rows of 16, a lane past its row's start
+      // adding Q^o x the lane o before it; then rows 1 / 3 take Q^((lane & 15) + 1) x lane 15 of
+      // rows 0 / 2, and rows 2, 3 Q^((lane & 31) + 1) x lane 31: the same sums as the shuffled
+      // Hillis-Steele scan, associated differently, which the check's exactness does not see)
+      auto step = [&](const Mat2& Qo, double up, double uv) {
+        yp = yp + (Qo.a * up + Qo.b * uv);
+        yv = yv + (Qo.c * up + Qo.d * uv);
+      };
+      step(qp(0), dpp_f64<0x111>(0.0, yp), dpp_f64<0x111>(0.0, yv));
+      step(qp(1), dpp_f64<0x112>(0.0, yp), dpp_f64<0x112>(0.0, yv));
+      step(qp(2), dpp_f64<0x114>(0.0, yp), dpp_f64<0x114>(0.0, yv));
+      step(qp(3), dpp_f64<0x118>(0.0, yp), dpp_f64<0x118>(0.0, yv));
+      step(QT[(lane & 15) + 1], dpp_f64<0x142, 0xa>(0.0, yp), dpp_f64<0x142, 0xa>(0.0, yv));
+      step(QT[(lane & 31) + 1], dpp_f64<0x143, 0xc>(0.0, yp), dpp_f64<0x143, 0xc>(0.0, yv));
       if (lane == 63) wsum[wv] = d2v{yp, yv};
+      SPEC_TP();                                 // (the phase timers: the scan's shuffles / its barrier)
       __syncthreads();
       SPEC_TP();
       const Mat2 Q64 = qp(6);
@@ -1012,8 +1046,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     }
     // Y_{j-1}: the previous lane's (lane 0: the carry); the check's barrier orders these wsum
     // reads before the next round's writes
-    double vp = __shfl_up(yp, 1, 64), vv = __shfl_up(yv, 1, 64);
-    if (lane == 0) { vp = cp; vv = cv; }
+    double vp = dpp_f64<0x138>(cp, yp), vv = dpp_f64<0x138>(cv, yv);   // (wave_shr:1; lane 0 keeps the carry)
     vp = vp + (Qj.a * p1 + Qj.b * v1);           // + Q^j x_1
     vv = vv + (Qj.c * p1 + Qj.d * v1);
     SPEC_TP();
@@ -1038,7 +1071,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     auto check = [&](auto FC, auto POC, auto AC) __attribute__((always_inline)) {
       constexpr bool F = decltype(FC)::value, PO = decltype(POC)::value, AF = decltype(AC)::value;
       if constexpr (AF)   // (its line: the pseudo-block's line tid - (pre >> 5), pre = 1 mod 32 and L = 32)
-        th32_lines(rowp, P.n)[(rb >> 5) + tid - (pre >> 5)] = Th32Line{xs_p, 0.0};
+        lrow[(rb >> 5) + tid - (pre >> 5)] = Th32Line{xs_p, 0.0};
       double kd = off + (double)k0;
       for (int i0 = 0; i0 < L; i0 += SB) {
         int cd[SB / 2];                          // (half a batch of codes at a time: registers)
@@ -1136,9 +1169,10 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
 #ifdef SDR_PLL_SPEC_PROF
     if (tid == SDR_PLL_SPEC_PROF_TID && nmiss == 0 && (bid == 0 || (bid % 479) == 3))
       printf("spec_prof blk %d L %d: stage %lld corrloop %lld corrscan %lld warm %lld guessloop %lld guesssync %lld "
-             "qpow %lld wscan %lld xscan %lld ystart %lld checkloop %lld checksync %lld (%d marks)\n", bid, L,
-             tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], tp[6] - tp[5], tp[7] - tp[6],
-             tp[8] - tp[7], tp[9] - tp[8], tp[10] - tp[9], tp[11] - tp[10], tp[12] - tp[11], ntp);
+             "lines %lld zq %lld wshfl %lld wbar %lld xscan %lld ystart %lld checkloop %lld checksync %lld (%d marks)\n",
+             bid, L, tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4], tp[6] - tp[5],
+             tp[7] - tp[6], tp[8] - tp[7], tp[9] - tp[8], tp[10] - tp[9], tp[11] - tp[10], tp[12] - tp[11],
+             tp[13] - tp[12], tp[14] - tp[13], ntp);
 #endif
     if (nmiss == 0) {
       if constexpr (LONG) {
@@ -1179,7 +1213,7 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       if (tid == TE - 1) {
         if (t32 && ((n - 1 - pre) & (TH32_LINE - 1)) == 0) {   // the last row starts a line: the line is its own
           const int64_t kl = rb + (n - 1 - pre);
-          th32_lines(rowp, P.n)[kl / TH32_LINE] = Th32Line{p, 0.0};
+          lrow[kl / TH32_LINE] = Th32Line{p, 0.0};
           th32_res(rowp)[kl] = 0.f;
         }
         const double arg = wsh * ((off + (double)(n - 1)) + 1.0) + p;

@@ -32,10 +32,8 @@ def parse(path):
 # Kernels allowed a bounded spill, each with the measurement that justifies it ("Build
 # gate").  Only kernels without counted waits may appear here -- never the FE kernels.
 ALLOW = {
-    # the long-call solve: 20 B/lane -- three loop-invariant values stored before the round loop,
-    # reloaded once a round (a pseudo-block solves in one round when locked); the AF check form
-    # that costs them took the PLL stage 0.301-0.305 -> 0.283-0.290 ms (profiles/r06/close2/af/)
-    "_ZN12_GLOBAL__N_115pll_spec_kernelILi512ELb1EEEv7PllJobs": 20,
+    # (empty: r06's one entry -- the long-call solve's 20 B/lane with the compact rows' AF check
+    # form -- went when its wave scans moved from ds_bpermute shuffles to DPP moves)
 }
 
 
