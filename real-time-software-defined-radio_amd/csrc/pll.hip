@@ -737,7 +737,22 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
     // (a span's sign-code row: a quarter of the bytes, r06; its codes other than +-1 -- zeros,
     // NaN -- are the solve's general-form case, 0, as the float row's)
     float xv[SG];
-    if (in8 != nullptr) {
+    // (r06: a full-length pseudo-block's sign codes as each thread's own chunk -- 32 codes, two
+    // 16-B loads instead of 32 byte loads; chunk j's steps 1 + 32 j .. 32 + 32 j start on a 16-B
+    // boundary after the 2 049-step pre-roll -- written into its column)
+    // (first: only a long call's first solve has pre-rolls; the repair kernel's registers are full)
+    const bool fast8 = first && SPEC_T == 512 && in8 != nullptr && L == 32 && N == SPEC_T * 32 &&
+                       ((uintptr_t)(in8 + 1) % 16) == 0;
+    if (fast8) {
+      const int4* src = reinterpret_cast<const int4*>(in8 + 1 + 32 * tid);
+      const int4 q0 = src[0], q1 = src[1];
+      const int w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int e = 0; e < 32; ++e) {
+        const int c = (int)(int8_t)(w[e >> 2] >> (8 * (e & 3)));
+        code[e * CSTR + tid] = (int8_t)((c == 1 || c == -1) ? c : 0);
+      }
+    } else if (in8 != nullptr) {
       int8_t cv[SG];
 #pragma unroll
       for (int u = 0; u < SG; ++u) cv[u] = in8[min(tid + u * SPEC_T, N - 1) + 1];
@@ -748,7 +763,9 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       for (int u = 0; u < SG; ++u) xv[u] = in[min(tid + u * SPEC_T, N - 1) + 1];
     }
     auto cod = [](float x) { return (int8_t)(x > 0.f ? 1 : (x < 0.f ? -1 : 0)); };
-    if (SPEC_T % L == 0) {
+    if (fast8) {
+      // (staged above)
+    } else if (SPEC_T % L == 0) {
       // element kk = tid + u SPEC_T: i = tid mod L for every u, j = tid / L + u SPEC_T / L
       const int i = tid % L, j0 = tid / L, js = SPEC_T / L;
 #pragma unroll
