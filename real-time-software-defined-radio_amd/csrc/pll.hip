@@ -1052,10 +1052,17 @@ __device__ __forceinline__ bool spec_body(const PllJobs& P, const int bid, const
       SPEC_TP();                                 // (the phase timers: the scan's shuffles / its barrier)
       __syncthreads();
       SPEC_TP();
-      const Mat2 Q64 = qp(6);
-      for (int i = 0; i < wv; ++i) {
-        const double np = wsum[i].x + (Q64.a * cp + Q64.b * cv), nv = wsum[i].y + (Q64.c * cp + Q64.d * cv);
-        cp = np; cv = nv;
+      // the carry, Y at the previous wave's end = sum over the waves before of Q^(64 (wv-1-i))
+      // x their totals (QT[65 + w] = Q^(64 w)): independent products, not a chain of wv
+      // dependent steps (r06: the last wave waited out seven)
+#pragma unroll
+      for (int i = 0; i < NW - 1; ++i) {
+        if (i < wv) {
+          const Mat2 M = QT[65 + wv - 1 - i];
+          const d2v t = wsum[i];
+          cp = cp + (M.a * t.x + M.b * t.y);
+          cv = cv + (M.c * t.x + M.d * t.y);
+        }
       }
       yp = yp + (Ql.a * cp + Ql.b * cv);
       yv = yv + (Ql.c * cp + Ql.d * cv);
